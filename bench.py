@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: signal elements triaged per second (batched DiffRaw+Merge of
+checkNewSignal against maxSignal), BASELINE.json config 2 per GPU:
+
+  4096 programs x 64 calls x 4096 PCs (synthetic KCOV traces)
+  -> K1+K2 edge derivation (setup, timed separately as `stages.edge_ms`)
+  -> one step = restore maxSignal to the 10M-element M0, then triage the whole
+     batch (K3 probe + decide), outputs: per-record new bits, per-call flags,
+     updated maxSignal and newSignal.
+
+N=1: one GPU, one process.  N>1 (torchrun, one rank per GPU): maxSignal is
+hash-sharded over the ranks (10M elements per rank), each rank owns its own
+4096-program slice of the batch (weak scaling), records are routed to their
+owner with RCCL all-to-all (syzkaller_amd/dist.py).
+
+Prints one JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PROBE_BYTES_PER_REC = 12.0  # 4 B element read + 8 B maxSignal slot read
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--programs", type=int, default=4096, help="programs per GPU")
+    ap.add_argument("--calls", type=int, default=64)
+    ap.add_argument("--pcs", type=int, default=4096)
+    ap.add_argument("--m0", type=int, default=10_000_000, help="maxSignal elements per GPU")
+    ap.add_argument("--skew", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, calls_per_prog, target_s):
+    """The oracle (single-threaded C restatement of checkNewSignal/pkg/signal,
+    oracle/oracle.c) on a bounded sample: the first S programs of this batch
+    against the same M0."""
+    from oracle import oracle as O
+
+    h_cs = cs.cpu().numpy().view(np.uint64)
+    h_cnt = cnt.cpu().numpy().view(np.uint32)
+    h_prio = prio.cpu().numpy()
+    e = m0e.cpu().numpy().view(np.uint32)
+    p = m0p.cpu().numpy()
+    nprog_total = h_cnt.size // calls_per_prog
+
+    def run(nprog):
+        nc = nprog * calls_per_prog
+        end = int(h_cs[nc - 1]) + int(h_cnt[nc - 1])
+        h_sigs = sigs[:end].cpu().numpy().view(np.uint32)
+        ms = O.deserialize(e, p)
+        t = time.perf_counter()
+        O.triage_batch_into(ms, h_sigs, h_cs[:nc], h_cnt[:nc], h_prio[:nc])
+        dt = time.perf_counter() - t
+        return int(h_cnt[:nc].sum()), dt
+
+    n = 8
+    recs, dt = run(n)
+    est = max(1, min(nprog_total, int(n * target_s / max(dt, 1e-3))))
+    if est > n:
+        n = est
+        recs, dt = run(n)
+    return {"value": recs / dt, "unit": "elems/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} programs ({recs} signal elements) of the same batch vs the same M0, "
+                      f"oracle/oracle.c single thread, {dt:.2f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if a.gpus != 1 or world != 1:
+            raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    distributed = world > 1
+    if distributed:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+    from syzkaller_amd.device import Device
+
+    dev = Device(local)
+    dev.L.syzsig_ctx_set_timing(dev.eng.h, 1)
+    cfg = synth.synth_default(skew=a.skew)
+    P, C, L = a.programs, a.calls, a.pcs
+    # ---- setup: traces -> K1+K2 (timed as a stage, not part of `value`)
+    cl = torch.full((P * C,), L, dtype=torch.int32)
+    pcs, cs, cl, prio = dev.synth_traces(cfg, rank * P, P, C, cl)
+    pidx = torch.arange(P + 1, dtype=torch.int32, device=dev.dev) * C
+    sigs = torch.empty(pcs.numel(), dtype=torch.int32, device=dev.dev)
+    cnt = torch.empty(P * C, dtype=torch.int32, device=dev.dev)
+    comp = torch.empty(P, dtype=torch.int32, device=dev.dev)
+    edge_ms = []
+    for i in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        dev.edge_derive(pcs, cs, cl, pidx, sigs, cnt, comp)
+        torch.cuda.synchronize()
+        edge_ms.append((time.perf_counter() - t) * 1e3)
+    npc = pcs.numel()
+    del pcs
+    nrec = int(cnt.to(torch.int64).sum().item())
+    # ---- M0 (maxSignal before the batch): 10M elements per GPU
+    if distributed:
+        from syzkaller_amd.dist import GpuShardOps, ShardedTriage, owner_of_torch
+
+        ge, gp = dev.synth_m0(cfg, 2048, a.m0 * world)
+        own = owner_of_torch(ge, world) == rank
+        m0e, m0p = ge[own].contiguous(), gp[own].contiguous()
+        del ge, gp
+    else:
+        m0e, m0p = dev.synth_m0(cfg, 2048, a.m0)
+    ms = dev.deserialize(m0e, m0p)
+    pristine = ms.clone()
+    ns = S.Signal.make(4_000_000, dev.eng)
+    b, bits, cnew = dev.batch(sigs, cs, cnt, prio)
+    if distributed:
+        sharded = ShardedTriage(GpuShardOps(dev), ms, ns)
+
+    def step():
+        ms.copy_from(pristine)
+        ns.clear()
+        if distributed:
+            return sharded.step((b, bits, cnew), prio, rank * P * C)[2]
+        return dev.triage(ms, ns, sigs, cs, cnt, prio, new_bits=bits, call_new=cnew)[2]
+
+    for _ in range(a.warmup):
+        step()
+    stats = []
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        stats.append(step())
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    total_rec = nrec
+    if distributed:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev.dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        tr = torch.tensor([nrec], dtype=torch.int64, device=dev.dev)
+        dist.all_reduce(tr)
+        total_rec = int(tr.item())
+    ms_per_step = dt / a.steps * 1e3
+    value = total_rec * a.steps / dt
+    s0 = stats[-1]
+    probe_ms = float(np.mean([s["probe_ms"] for s in stats]))
+    decide_ms = float(np.mean([s["decide_ms"] for s in stats]))
+    probe_units = s0["received"] if distributed else nrec
+    achieved = PROBE_BYTES_PER_REC * probe_units / (probe_ms * 1e-3) / 1e9
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "signal elems triaged/sec (Diff+Merge)",
+            "value": value,
+            "unit": "elems/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": "BASELINE config 2: 1xMI355X batch triage per GPU, "
+                                   f"{P} programs x {C} calls x {L} PCs vs {a.m0} -element maxSignal"
+                                   + (f" shard (hash-sharded over {world} GPUs, RCCL all-to-all)" if distributed else ""),
+                       "programs_per_gpu": P, "calls": C, "pcs_per_call": L, "m0_per_gpu": a.m0,
+                       "records_per_gpu": nrec, "pcs_per_gpu": npc, "skew": a.skew,
+                       "parallelism": f"shard{world}" if distributed else "single"},
+            "roofline": {"bound": "hbm", "kernel": "k_probe", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": probe_units,
+                         "avg_launch_ms": probe_ms},
+            "stages": {"edge_ms": float(np.median(edge_ms)), "probe_ms": probe_ms, "decide_ms": decide_ms,
+                       "edge_pcs_per_s": npc / (np.median(edge_ms) * 1e-3)},
+            "triage": {k: v for k, v in s0.items() if k not in ("probe_ms", "decide_ms")},
+        }
+    if rank == 0 and world == 1 and not a.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, C, a.cpu_seconds)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,217 @@
+/*
+ * syzsig.h -- C ABI of libsyzsig, the MI355X coverage-signal triage engine.
+ *
+ * This is the drop-in boundary for syzkaller's per-execution coverage-signal
+ * path.  Each entry point names the reference interface it replaces
+ * (paths relative to the upstream syzkaller tree); INTEGRATION.md shows the
+ * cgo binding that keeps pkg/signal's Go API and its callers unchanged.
+ *
+ * Conventions
+ *  - Every function returns int status: SYZSIG_OK (0) or a negative errno-style
+ *    code; syzsig_last_error() gives a message (thread-local).
+ *  - A `syzsig_set*` is a device-resident Signal.  NULL is Go's nil Signal:
+ *    Len()==0, usable as a receiver, and syzsig_merge allocates it
+ *    (signal.go:121-125).  Results that Go returns as nil come back as NULL.
+ *  - Host arrays passed in are copied during the call and never retained (cgo
+ *    pointer rules; CallInfo.Signal aliases executor shmem, pkg/ipc/ipc.go:410).
+ *  - Sets are not thread-safe; callers serialize like the reference does
+ *    (fuzzer.signalMu, syz-fuzzer/fuzzer.go:55; mgr.mu, syz-manager/manager.go:66).
+ *  - "_dev" / batch entry points take device pointers and run on the context's
+ *    stream (syzsig_ctx_set_stream); they return after the work completes.
+ */
+#ifndef SYZSIG_H
+#define SYZSIG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SYZSIG_OK 0
+#define SYZSIG_EIO (-5)        /* HIP runtime / device error */
+#define SYZSIG_ENOMEM (-12)
+#define SYZSIG_EINVAL (-22)
+#define SYZSIG_ERANGE (-34)    /* a size limit of this ABI exceeded */
+#define SYZSIG_ECORRUPT (-74)  /* panic("corrupted Serial"), pkg/signal/signal.go:60-62 */
+
+#define SYZSIG_ABI_VERSION 1
+
+typedef struct syzsig_ctx syzsig_ctx;
+typedef struct syzsig_set syzsig_set;
+
+int syzsig_abi_version(void);
+const char* syzsig_last_error(void);
+
+/* ---- context: one per process and GPU ---- */
+int syzsig_ctx_create(int device, syzsig_ctx** out);
+void syzsig_ctx_destroy(syzsig_ctx* ctx);
+/* Run subsequent work on `stream` (a hipStream_t; NULL = the context's own). */
+int syzsig_ctx_set_stream(syzsig_ctx* ctx, void* stream);
+void* syzsig_ctx_stream(syzsig_ctx* ctx);
+/* Record HIP events around the triage kernels (batch stats probe_ms/decide_ms). */
+int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable);
+
+/* ---- pkg/signal/signal.go ---- */
+
+/* make(Signal, hint): an empty, non-nil Signal. */
+int syzsig_set_make(syzsig_ctx* ctx, uint64_t hint, syzsig_set** out);
+void syzsig_set_free(syzsig_set* s);
+/* Deep copy (Go copies alias; this is for callers that need a snapshot). */
+int syzsig_set_clone(syzsig_ctx* ctx, const syzsig_set* s, syzsig_set** out);
+/* Make s empty keeping its storage (grabNewSignal's `fuzzer.newSignal = nil`,
+ * syz-fuzzer/fuzzer.go:478-486, without a free/alloc round trip). */
+int syzsig_set_clear(syzsig_ctx* ctx, syzsig_set* s);
+/* Copy src's contents over dst (same capacity required); for snapshot/restore. */
+int syzsig_set_copy_from(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src);
+/* Len / Empty, signal.go:23-29. */
+uint64_t syzsig_len(const syzsig_set* s);
+int syzsig_empty(const syzsig_set* s);
+/* Capacity in slots (diagnostics, bench accounting). */
+uint64_t syzsig_capacity(const syzsig_set* s);
+
+/* FromRaw, signal.go:31-40 (NULL when n == 0). */
+int syzsig_from_raw(syzsig_ctx* ctx, const uint32_t* raw, uint64_t n, uint8_t prio, syzsig_set** out);
+/* Serialize, signal.go:42-57.  Order is unspecified (Go: map order).  Writes
+ * min(cap, Len) entries and sets *n_out = Len. */
+int syzsig_serialize(syzsig_ctx* ctx, const syzsig_set* s, uint32_t* elems, int8_t* prios,
+                     uint64_t cap, uint64_t* n_out);
+/* Deserialize, signal.go:59-71: SYZSIG_ECORRUPT if n_elems != n_prios; NULL
+ * when empty; a later duplicate element overwrites an earlier one. */
+int syzsig_deserialize(syzsig_ctx* ctx, const uint32_t* elems, uint64_t n_elems, const int8_t* prios,
+                       uint64_t n_prios, syzsig_set** out);
+/* Same, elems/prios already in device memory. */
+int syzsig_deserialize_dev(syzsig_ctx* ctx, const uint32_t* d_elems, const int8_t* d_prios, uint64_t n,
+                           syzsig_set** out);
+/* Diff, signal.go:73-88 (s may be NULL). */
+int syzsig_diff(syzsig_ctx* ctx, const syzsig_set* s, const syzsig_set* s1, syzsig_set** out);
+/* DiffRaw, signal.go:90-102 (prio compared as int8). */
+int syzsig_diff_raw(syzsig_ctx* ctx, const syzsig_set* s, const uint32_t* raw, uint64_t n, uint8_t prio,
+                    syzsig_set** out);
+/* Intersection, signal.go:104-115: NULL if s1 empty, else non-nil (maybe empty). */
+int syzsig_intersection(syzsig_ctx* ctx, const syzsig_set* s, const syzsig_set* s1, syzsig_set** out);
+/* (*Signal).Merge, signal.go:117-131: max prio; allocates *s if NULL. */
+int syzsig_merge(syzsig_ctx* ctx, syzsig_set** s, const syzsig_set* s1);
+
+/* Minimize, signal.go:133-166.  Contexts as Serial arrays: context i owns
+ * elems/prios[ctx_off[i] .. ctx_off[i+1]) (elements distinct within a context,
+ * as Serialize produces).  Sort order is (Len desc, index asc) -- a fixed
+ * instance of the reference's unstable sort.Slice.  Writes the indices of the
+ * surviving contexts, ascending, to out_idx (capacity nctx); *n_out = count.
+ * hint_distinct: expected distinct elements (e.g. corpusSignal.Len()), or 0. */
+int syzsig_minimize(syzsig_ctx* ctx, const uint64_t* ctx_off, const uint32_t* elems, const int8_t* prios,
+                    uint64_t nctx, uint64_t hint_distinct, uint64_t* out_idx, uint64_t* n_out);
+/* Same over device arrays; d_keep[i] = 1 iff context i survives. */
+int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, const uint32_t* d_elems,
+                        const int8_t* d_prios, uint64_t nctx, uint64_t hint_distinct, uint8_t* d_keep,
+                        uint64_t* n_out);
+
+/* ---- syz-fuzzer/fuzzer.go:494-511 checkNewSignal (+ signalPrio :513-521 by caller) ----
+ * One program's CallInfo signals in host memory: call i's raw signal is
+ * sigs[call_start[i] .. +call_len[i]) with prio call_prio[i].  Sequential over
+ * calls as the reference: call i sees merges of calls < i.  Writes indices of
+ * calls with new signal to out_calls (capacity ncalls), *n_out = count;
+ * merges into *max_signal and *new_signal (allocating NULL ones).
+ * new_bits (optional, ceil(nrec/32) words): bit r set iff sigs[r] is in its
+ * call's DiffRaw result. */
+int syzsig_check_new_signal(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_signal,
+                            const uint32_t* sigs, uint64_t nrec, const uint64_t* call_start,
+                            const uint32_t* call_len, const uint8_t* call_prio, uint32_t ncalls,
+                            uint32_t* out_calls, uint32_t* n_out, uint32_t* new_bits);
+
+/* ---- batch triage (device pointers): checkNewSignal over a whole batch ----
+ * Serial order = call index order (program-major, call-minor).  Call ranges
+ * [call_start, call_start+call_len) must lie inside [0, nrec) and be disjoint.
+ * Outputs are zeroed by the call. */
+typedef struct {
+	const uint32_t* sigs;       /* nrec raw signal elements */
+	const uint64_t* call_start; /* ncalls */
+	const uint32_t* call_len;   /* ncalls */
+	const uint8_t* call_prio;   /* ncalls, signalPrio values */
+	uint64_t ncalls;
+	uint64_t nrec;
+	uint32_t* new_bits;         /* out: ceil(nrec/32) words, bit r = record r is new */
+	uint8_t* call_new;          /* out: ncalls, 1 = call has new signal */
+} syzsig_batch;
+
+typedef struct {
+	uint64_t records;        /* records processed */
+	uint64_t candidates;     /* records that passed the maxSignal prio filter */
+	uint64_t changed;        /* elements whose maxSignal prio changed (incl. new) */
+	uint64_t inserted;       /* elements new to maxSignal */
+	uint64_t new_signal_len; /* Len of *new_signal after the batch */
+	uint64_t retries;        /* capacity-overflow restarts */
+	uint64_t runs;           /* sub-batches (one per <=4 distinct prios) */
+	double probe_ms;         /* device time of the probe kernel(s) (0 unless timing enabled) */
+	double decide_ms;        /* device time of the decide kernel(s) (0 unless timing enabled) */
+} syzsig_batch_stats;
+
+int syzsig_triage_batch(syzsig_ctx* ctx, syzsig_set* max_signal, syzsig_set** new_signal,
+                        const syzsig_batch* b, syzsig_batch_stats* stats);
+
+/* ---- executor/executor.h:492-528 + :677-706 on device (K1 edge + K2 dedup) ----
+ * Raw KCOV traces for nprog programs; program p owns calls
+ * [prog_call[p], prog_call[p+1]); call c's PCs are pcs[call_start[c] .. +call_len[c])
+ * (call_len < 262144, executor_linux.cc:186-187).  Each program runs with a
+ * fresh 8192-slot dedup table shared by its calls in order, like one forked
+ * executor child.  Call c's emitted signals land at sigs[call_start[c] ..
+ * +sig_cnt[c]); completed[p] = calls whose record was published (a PC failing
+ * cover_check aborts the rest of the program); later calls get sig_cnt = 0.
+ * d_sigs has npc entries (same indexing as d_pcs). */
+int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, uint64_t npc, const uint64_t* d_call_start,
+                           const uint32_t* d_call_len, uint64_t ncalls, const uint32_t* d_prog_call,
+                           uint64_t nprog, uint32_t* d_sigs, uint32_t* d_sig_cnt, uint32_t* d_completed);
+
+/* ---- hash-sharded maxSignal across GPUs (one process per GPU) ----
+ * The batch is split by program range over G GPUs (serial order = GPU-major);
+ * every record is routed to the GPU owning its element
+ * (owner = syz::owner_of(elem, G)), packed as
+ *   elem << 32 | level << 24 | serial      (serial < 2^24, level < 4)
+ * where serial is its call's position in the batch's global serial order and
+ * level the rank of its call's prio in `levels` (ascending int8, <= 4 entries,
+ * the union of the prios of all GPUs' calls).
+ *
+ * partition: d_send (b->nrec entries) receives the records grouped by owner,
+ * owner g's group at [send_off[g], send_off[g] + send_counts[g]) with
+ * send_off the exclusive prefix sum (host arrays, nshards entries each);
+ * d_send_pos[r] = where record r went. */
+int syzsig_shard_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
+                               const int8_t* levels, uint32_t nlevels, uint32_t nshards,
+                               uint64_t* d_send, uint32_t* d_send_pos, uint64_t* send_counts);
+/* Owner side: triage received records against the local shard of maxSignal;
+ * d_new_flags[i] = 1 iff received record i is new (checkNewSignal's DiffRaw
+ * result for its call).  Serial order comes from the records' serial fields. */
+int syzsig_triage_records_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set** new_signal,
+                              const uint64_t* d_recs, uint64_t nrec, const int8_t* levels,
+                              uint32_t nlevels, uint8_t* d_new_flags, syzsig_batch_stats* stats);
+/* Source side: d_back_flags (send order, returned by the owners) -> b->new_bits
+ * and b->call_new (both zeroed here first). */
+int syzsig_shard_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* d_send_pos,
+                                 const uint8_t* d_back_flags);
+
+/* ---- synthetic workload (deterministic; host and device give identical data) ---- */
+typedef struct {
+	uint64_t seed;
+	uint32_t nblocks_log2, region_log2, nsys, skew, restart_log2;
+	uint32_t errno_permille, any_permille, bad_pc_ppm;
+} syzsig_synth_cfg;
+
+void syzsig_synth_default(syzsig_synth_cfg* cfg);
+/* Per call c of a batch (prog_base + p for program p): call_prio and the raw trace
+ * of call_len[c] PCs at pcs[call_start[c]..]. */
+int syzsig_synth_traces_host(const syzsig_synth_cfg* cfg, uint64_t prog_base, uint64_t nprog,
+                             uint32_t calls_per_prog, const uint64_t* call_start, const uint32_t* call_len,
+                             uint64_t* pcs, uint8_t* call_prio);
+int syzsig_synth_traces_dev(syzsig_ctx* ctx, const syzsig_synth_cfg* cfg, uint64_t prog_base,
+                            uint64_t nprog, uint32_t calls_per_prog, const uint64_t* d_call_start,
+                            const uint32_t* d_call_len, uint64_t* d_pcs, uint8_t* d_call_prio);
+int syzsig_synth_m0_host(const syzsig_synth_cfg* cfg, uint64_t known_sys, uint64_t n, uint32_t* elems,
+                         int8_t* prios);
+int syzsig_synth_m0_dev(syzsig_ctx* ctx, const syzsig_synth_cfg* cfg, uint64_t known_sys, uint64_t n,
+                        uint32_t* d_elems, int8_t* d_prios);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SYZSIG_H */

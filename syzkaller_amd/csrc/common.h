@@ -1,0 +1,215 @@
+// common.h -- definitions shared by host and device code of libsyzsig.
+//
+// Slot encoding of a device-resident Signal (pkg/signal/signal.go:17,
+// `type Signal map[elemType]prioType`), one u64 per slot:
+//
+//      63            32 31      10   9        8       7       0
+//     +----------------+----------+--------+---------+---------+
+//     |  elem (u32)    |    0     |HASPRIO | PRESENT | prio^0x80|
+//     +----------------+----------+--------+---------+---------+
+//
+// slot == 0 is EMPTY.  A live entry has PRESENT|HASPRIO, so for one key the
+// unsigned order of slot words equals the signed order of prio (int8 biased by
+// 0x80): atomicMax on the whole word is exactly the max-prio Merge rule of
+// signal.go:117-131.  PRESENT without HASPRIO is the batch-transient "absent at
+// batch start" marker used by triage (it orders below every live prio, as Go's
+// `!ok` does in DiffRaw, signal.go:93).
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define SYZ_HD __host__ __device__ __forceinline__
+#else
+#define SYZ_HD static inline
+#endif
+
+namespace syz {
+
+constexpr uint32_t kBucketSlots = 8;        // 8 x u64 = one 64-B bucket
+constexpr uint64_t kSlotEmpty = 0;
+constexpr uint32_t kStatePresent = 0x100;
+constexpr uint32_t kStateHasPrio = 0x200;
+constexpr uint32_t kStateLive = kStatePresent | kStateHasPrio;
+
+SYZ_HD uint64_t make_slot(uint32_t key, int8_t prio)
+{
+	return ((uint64_t)key << 32) | kStateLive | (uint32_t)((uint8_t)prio ^ 0x80u);
+}
+SYZ_HD uint64_t make_absent(uint32_t key) { return ((uint64_t)key << 32) | kStatePresent; }
+SYZ_HD uint32_t slot_key(uint64_t s) { return (uint32_t)(s >> 32); }
+SYZ_HD bool slot_live(uint64_t s) { return (s & kStateHasPrio) != 0; }
+SYZ_HD int8_t slot_prio(uint64_t s) { return (int8_t)((uint8_t)s ^ 0x80u); }
+SYZ_HD uint32_t prio_biased(int8_t p) { return (uint8_t)p ^ 0x80u; }
+
+// murmur3 fmix32: bucket index of an element inside one table.
+SYZ_HD uint32_t fmix32(uint32_t h)
+{
+	h ^= h >> 16;
+	h *= 0x85ebca6bu;
+	h ^= h >> 13;
+	h *= 0xc2b2ae35u;
+	h ^= h >> 16;
+	return h;
+}
+
+// Owner shard of an element in an N-way hash-partitioned maxSignal.  Independent
+// of fmix32 (different multiplier/offset), so slots stay uniform inside a shard.
+SYZ_HD uint32_t owner_of(uint32_t e, uint32_t nshards)
+{
+	uint32_t h = fmix32(e * 0x9E3779B1u + 0x7F4A7C15u);
+	return (uint32_t)(((uint64_t)h * nshards) >> 32);
+}
+
+// executor/executor.h:677-685 -- the edge hash of the reference executor.
+SYZ_HD uint32_t exec_hash(uint32_t a)
+{
+	a = (a ^ 61) ^ (a >> 16);
+	a = a + (a << 3);
+	a = a ^ (a >> 4);
+	a = a * 0x27d4eb2du;
+	a = a ^ (a >> 15);
+	return a;
+}
+
+// executor/executor_linux.cc:196-204 (x86_64 text/modules range).
+SYZ_HD bool cover_check(uint64_t pc)
+{
+	return pc >= 0xffffffff80000000ull && pc < 0xffffffffff000000ull;
+}
+
+constexpr uint32_t kDedupSize = 8u << 10;   // executor.h:687 dedup_table_size
+constexpr uint32_t kCoverSize = 256u << 10; // executor.h:25 kCoverSize (per-call PC limit)
+
+// ---------------------------------------------------------------------------
+// Synthetic KCOV workload (DESIGN.md "Workload").  Deterministic and identical
+// on host and device, so host checkers and device kernels see the same traces.
+// ---------------------------------------------------------------------------
+
+SYZ_HD uint64_t splitmix64(uint64_t* s)
+{
+	uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+	return z ^ (z >> 31);
+}
+
+SYZ_HD uint64_t seed_mix(uint64_t seed, uint64_t a, uint64_t b)
+{
+	uint64_t s = seed ^ (a * 0xD1B54A32D192ED03ull) ^ (b * 0xAEF17502108EF2D9ull);
+	splitmix64(&s);
+	return s;
+}
+
+constexpr uint64_t kPcBase = 0xffffffff81000000ull;
+
+struct SynthCfg {
+	uint64_t seed;          // 20181015 in every config
+	uint32_t nblocks_log2;  // basic blocks B = 2^nblocks_log2 (20)
+	uint32_t region_log2;   // per-syscall region W = 2^region_log2 blocks (8)
+	uint32_t nsys;          // distinct syscalls (4096)
+	uint32_t skew;          // 0 uniform syscall choice, 1 power-skewed (hot edges)
+	uint32_t restart_log2;  // walk returns to the syscall entry w.p. 2^-restart_log2 (5)
+	uint32_t errno_permille;// call fails (errno != 0) w.p. /1000 (300)
+	uint32_t any_permille;  // call contains an ANY pointer w.p. /1000 (100)
+	uint32_t bad_pc_ppm;    // out-of-range PC rate per PC, parts per million (0)
+};
+
+SYZ_HD uint64_t synth_pc(uint32_t block) { return kPcBase + 5ull * block; }
+
+// Entry block of syscall s.
+SYZ_HD uint32_t synth_entry(const SynthCfg& c, uint32_t s)
+{
+	return fmix32(s * 0x9E3779B1u + 0x01234567u) & ((1u << c.nblocks_log2) - 1);
+}
+
+struct SynthCall {
+	uint32_t sysno;
+	uint8_t failed;  // errno != 0
+	uint8_t any;     // prog.CallContainsAny
+};
+
+SYZ_HD SynthCall synth_call(const SynthCfg& c, uint64_t prog, uint32_t call)
+{
+	uint64_t s = seed_mix(c.seed, prog, 0x100000000ull + call);
+	uint64_t r = splitmix64(&s);
+	SynthCall sc;
+	if (c.skew) {
+		uint64_t x = (r >> 40) & 0xFFFFFF;  // u in [0,1) as 24-bit fixed point
+		uint64_t t = (x * x) >> 24;
+		t = (t * t) >> 24;                  // u^4
+		sc.sysno = (uint32_t)((t * c.nsys) >> 24);
+	} else {
+		sc.sysno = (uint32_t)(r % c.nsys);
+	}
+	uint64_t r2 = splitmix64(&s);
+	sc.failed = (uint8_t)((r2 % 1000) < c.errno_permille);
+	sc.any = (uint8_t)(((r2 >> 20) % 1000) < c.any_permille);
+	return sc;
+}
+
+// syz-fuzzer/fuzzer.go:513-521 signalPrio.
+SYZ_HD uint8_t signal_prio(uint8_t failed, uint8_t any)
+{
+	uint8_t prio = 0;
+	if (!failed)
+		prio |= 1 << 1;
+	if (!any)
+		prio |= 1 << 0;
+	return prio;
+}
+
+// The raw KCOV trace of one call: a walk inside its syscall's region,
+// x <- (4x + 1 + r%4) mod W, restarting at the entry w.p. 2^-restart_log2.
+SYZ_HD void synth_trace(const SynthCfg& c, uint64_t prog, uint32_t call, uint64_t* out, uint32_t n)
+{
+	SynthCall sc = synth_call(c, prog, call);
+	uint32_t entry = synth_entry(c, sc.sysno);
+	uint32_t bmask = (1u << c.nblocks_log2) - 1, wmask = (1u << c.region_log2) - 1;
+	uint32_t rmask = (1u << c.restart_log2) - 1;
+	uint64_t s = seed_mix(c.seed, prog, call);
+	uint32_t x = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		uint64_t r = splitmix64(&s);
+		uint64_t pc = synth_pc((entry + x) & bmask);
+		if (c.bad_pc_ppm && ((r >> 40) % 1000000) < c.bad_pc_ppm)
+			pc = 0x1000ull + i;  // outside cover_check's range: aborts the program
+		out[i] = pc;
+		if ((r & rmask) == 0)
+			x = 0;
+		else
+			x = (4 * x + 1 + (uint32_t)((r >> 8) & 3)) & wmask;
+	}
+}
+
+// Element i of the synthetic initial maxSignal M0: the first n_known elements
+// enumerate the edge signals of syscalls [0, known_sys) (every in-region edge,
+// restart edge and entry signal, exactly as write_coverage_signal would derive
+// them), the rest are uniform u32; prio uniform in 0..3.
+SYZ_HD uint32_t synth_known_per_sys(const SynthCfg& c) { return (1u << c.region_log2) * 5 + 1; }
+
+SYZ_HD void synth_m0_elem(const SynthCfg& c, uint64_t i, uint64_t n_known, uint32_t* elem, int8_t* prio)
+{
+	uint64_t s = seed_mix(c.seed ^ 0x4D30u, i, 7);
+	uint64_t r = splitmix64(&s);
+	*prio = (int8_t)(r & 3);
+	if (i >= n_known) {
+		*elem = (uint32_t)(r >> 32);
+		return;
+	}
+	uint32_t per = synth_known_per_sys(c);
+	uint32_t sys = (uint32_t)(i / per), k = (uint32_t)(i % per);
+	uint32_t W = 1u << c.region_log2, bmask = (1u << c.nblocks_log2) - 1;
+	uint32_t entry = synth_entry(c, sys);
+	if (k == 0) {  // first PC of a call: sig = pc ^ 0
+		*elem = (uint32_t)synth_pc(entry);
+		return;
+	}
+	k -= 1;
+	uint32_t x = k / 5, j = k % 5;
+	uint32_t from = (uint32_t)synth_pc((entry + x) & bmask);
+	uint32_t to_x = j < 4 ? ((4 * x + 1 + j) & (W - 1)) : 0;  // j == 4: restart edge
+	*elem = (uint32_t)synth_pc((entry + to_x) & bmask) ^ exec_hash(from);
+}
+
+}  // namespace syz

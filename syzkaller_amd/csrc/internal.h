@@ -1,0 +1,254 @@
+// internal.h -- private structures and device primitives of libsyzsig.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "../../include/syzsig.h"
+#include "common.h"
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+namespace syz {
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what, const char* file, int line);
+}  // namespace syz
+
+#define SYZ_HIP(expr)                                                              \
+	do {                                                                           \
+		hipError_t e__ = (expr);                                                   \
+		if (e__ != hipSuccess)                                                     \
+			return syz::hip_fail(e__, #expr, __FILE__, __LINE__);                  \
+	} while (0)
+
+#define SYZ_TRY(expr)                                                              \
+	do {                                                                           \
+		int r__ = (expr);                                                          \
+		if (r__ != SYZSIG_OK)                                                      \
+			return r__;                                                            \
+	} while (0)
+
+// ---------------------------------------------------------------------------
+// host-side objects
+// ---------------------------------------------------------------------------
+namespace syz {
+
+// Device counters live in one small array per context (zeroed per operation).
+enum Counter : int {
+	kCntInserted = 0,   // new keys inserted into the destination table
+	kCntOverflow,       // probe limit hit (capacity too small) -> retry bigger
+	kCntError,          // malformed input detected on device
+	kCntCandidates,     // triage: records that passed the prio filter
+	kCntTouched,        // triage: distinct elements with a candidate this run
+	kCntChanged,        // triage: slots committed (prio raised or inserted)
+	kCntAux,            // misc (serialize cursor, minimize winners...)
+	kCntAux2,
+	kNumCounters = 16,
+};
+
+struct Workspace {
+	void* ptr = nullptr;
+	size_t size = 0;
+};
+
+}  // namespace syz
+
+struct syzsig_ctx {
+	int device = 0;
+	hipStream_t own_stream = nullptr;
+	hipStream_t stream = nullptr;
+	unsigned long long* d_cnt = nullptr;  // kNumCounters
+	unsigned long long* h_cnt = nullptr;  // pinned mirror
+	syz::Workspace ws[16];                // grow-only scratch buffers (index = role, see kWs*)
+	bool timing = false;                  // HIP events around triage kernels
+	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+struct syzsig_set {
+	syzsig_ctx* ctx = nullptr;
+	uint64_t* slots = nullptr;   // nbuckets * 8
+	uint64_t nbuckets = 0;       // power of two
+	uint64_t len = 0;            // live entries (host mirror of device truth)
+	// triage side state, allocated on first batch
+	uint32_t* firsts = nullptr;  // 4 per slot: epoch_rev << 24 | serial, per prio level
+	uint32_t* touched = nullptr; // 1 bit per slot
+	uint32_t epoch = 0;          // current epoch_rev (counts down 254..1)
+	uint64_t nslots() const { return nbuckets * syz::kBucketSlots; }
+};
+
+namespace syz {
+
+// scratch buffer `i` of the context, grown to at least `bytes`
+int ws_get(syzsig_ctx* ctx, int i, size_t bytes, void** out);
+int counters_reset(syzsig_ctx* ctx);
+int counters_fetch(syzsig_ctx* ctx);  // sync + copy to ctx->h_cnt
+
+// table lifecycle (table.hip)
+uint64_t buckets_for(uint64_t n_entries);
+int set_alloc(syzsig_ctx* ctx, uint64_t nbuckets, syzsig_set** out);
+int set_reserve(syzsig_set* s, uint64_t extra);  // ensure room for len+extra
+int set_rehash(syzsig_set* s, uint64_t nbuckets, bool drop_absent);
+int set_ensure_triage_state(syzsig_set* s);
+int merge_pairs_dev(syzsig_ctx* ctx, syzsig_set* dst, const uint64_t* d_pairs, uint64_t n);
+
+// Prio levels of one triage run: DiffRaw compares prios as int8
+// (signal.go:93), so levels follow signed order.
+struct LevelMap {
+	uint8_t lvl[256];  // prio (as u8) -> level, 0xff = not in this run
+	int8_t val[4];     // level -> prio
+	uint32_t n;
+};
+constexpr uint32_t kSerialMask = 0xFFFFFF;  // 24-bit serial index inside a run
+int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm);
+
+// the default load-factor policy: a table is grown when live/slots exceeds this
+constexpr double kMaxLoad = 0.75;
+constexpr double kTargetLoad = 0.5;
+constexpr uint32_t kMaxProbeBuckets = 1024;
+
+inline int grid_for(uint64_t n, int block, int max_blocks = 2048)
+{
+	uint64_t g = (n + block - 1) / block;
+	if (g < 1)
+		g = 1;
+	if (g > (uint64_t)max_blocks)
+		g = max_blocks;
+	return (int)g;
+}
+
+}  // namespace syz
+
+// ---------------------------------------------------------------------------
+// device primitives
+// ---------------------------------------------------------------------------
+#if defined(__HIPCC__)
+namespace syz {
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// number of set bits of `mask` below this lane
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask)
+{
+	return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
+{
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1)
+		v += __shfl_xor(v, o, 64);
+	return v;
+}
+
+// Block-wide sum of v added to *counter by one thread.  Every thread of the
+// block must call it (uniform control flow).
+__device__ __forceinline__ void block_count(unsigned long long* counter, uint64_t v)
+{
+	__shared__ unsigned long long part;
+	if (threadIdx.x == 0)
+		part = 0;
+	__syncthreads();
+	v = wave_sum_u64(v);
+	if (lane_id() == 0 && v)
+		atomicAdd(&part, (unsigned long long)v);
+	__syncthreads();
+	if (threadIdx.x == 0 && part)
+		atomicAdd(counter, part);
+}
+
+struct Bucket {
+	uint64_t s[kBucketSlots];
+};
+
+__device__ __forceinline__ Bucket load_bucket(const uint64_t* p)
+{
+	const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p);
+	ulonglong2 a = q[0], b = q[1], c = q[2], d = q[3];
+	Bucket B;
+	B.s[0] = a.x; B.s[1] = a.y; B.s[2] = b.x; B.s[3] = b.y;
+	B.s[4] = c.x; B.s[5] = c.y; B.s[6] = d.x; B.s[7] = d.y;
+	return B;
+}
+
+__device__ __forceinline__ uint64_t home_bucket(uint32_t key, uint64_t bmask) { return fmix32(key) & bmask; }
+
+// Lookup.  Returns the slot index, or -1 if absent (first empty slot reached:
+// slots only ever go EMPTY -> key, so occupied slots form a prefix of every
+// probe sequence).
+__device__ __forceinline__ int64_t tbl_lookup(const uint64_t* __restrict__ slots, uint64_t bmask, uint32_t key,
+                                              uint64_t& val)
+{
+	uint64_t b = home_bucket(key, bmask);
+	for (uint64_t n = 0; n <= bmask; n++) {
+		Bucket B = load_bucket(slots + (b << 3));
+#pragma unroll
+		for (int i = 0; i < (int)kBucketSlots; i++) {
+			if (B.s[i] == kSlotEmpty)
+				return -1;
+			if (slot_key(B.s[i]) == key) {
+				val = B.s[i];
+				return (int64_t)((b << 3) + i);
+			}
+		}
+		b = (b + 1) & bmask;
+	}
+	return -1;
+}
+
+// Find `key`, inserting `ins` (a slot word for `key`) at the first empty slot
+// if absent.  old = previous word (0 when this call inserted).  Returns -1
+// when max_probe buckets were scanned without success (overflow).
+__device__ __forceinline__ int64_t tbl_find_or_insert(uint64_t* slots, uint64_t bmask, uint32_t key, uint64_t ins,
+                                                      uint64_t& old, uint64_t max_probe)
+{
+	uint64_t b = home_bucket(key, bmask);
+	for (uint64_t n = 0; n < max_probe; n++) {
+		uint64_t* bp = slots + (b << 3);
+		Bucket B = load_bucket(bp);
+#pragma unroll
+		for (int i = 0; i < (int)kBucketSlots; i++) {
+			uint64_t s = B.s[i];
+			if (s == kSlotEmpty) {
+				s = atomicCAS(reinterpret_cast<unsigned long long*>(bp + i), 0ull, (unsigned long long)ins);
+				if (s == kSlotEmpty) {
+					old = 0;
+					return (int64_t)((b << 3) + i);
+				}
+			}
+			if (slot_key(s) == key) {
+				old = s;
+				return (int64_t)((b << 3) + i);
+			}
+		}
+		b = (b + 1) & bmask;
+	}
+	return -1;
+}
+
+__device__ __forceinline__ uint64_t max_probe_for(uint64_t bmask)
+{
+	uint64_t nb = bmask + 1;
+	return nb < kMaxProbeBuckets ? nb : kMaxProbeBuckets;
+}
+
+// Insert-or-max (Merge rule).  Returns 1 if inserted, 0 otherwise; -1 overflow.
+__device__ __forceinline__ int tbl_merge(uint64_t* slots, uint64_t bmask, uint32_t key, int8_t prio)
+{
+	uint64_t v = make_slot(key, prio), old;
+	int64_t idx = tbl_find_or_insert(slots, bmask, key, v, old, max_probe_for(bmask));
+	if (idx < 0)
+		return -1;
+	if (old == 0)
+		return 1;
+	if (old < v)
+		atomicMax(reinterpret_cast<unsigned long long*>(slots + idx), (unsigned long long)v);
+	return 0;
+}
+
+}  // namespace syz
+#endif

@@ -1,0 +1,135 @@
+// runtime.hip -- context, stream, scratch and error plumbing of libsyzsig.
+#include <cstdio>
+
+#include "internal.h"
+
+namespace syz {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const std::string& msg)
+{
+	set_error(msg);
+	return code;
+}
+
+int hip_fail(hipError_t e, const char* what, const char* file, int line)
+{
+	char buf[512];
+	snprintf(buf, sizeof(buf), "%s failed: %s (%s:%d)", what, hipGetErrorString(e), file, line);
+	set_error(buf);
+	return e == hipErrorOutOfMemory ? SYZSIG_ENOMEM : SYZSIG_EIO;
+}
+
+int ws_get(syzsig_ctx* ctx, int i, size_t bytes, void** out)
+{
+	Workspace& w = ctx->ws[i];
+	if (w.size < bytes) {
+		if (w.ptr) {
+			SYZ_HIP(hipStreamSynchronize(ctx->stream));
+			SYZ_HIP(hipFree(w.ptr));
+			w.ptr = nullptr;
+			w.size = 0;
+		}
+		size_t want = bytes + bytes / 4 + 4096;
+		SYZ_HIP(hipMalloc(&w.ptr, want));
+		w.size = want;
+	}
+	*out = w.ptr;
+	return SYZSIG_OK;
+}
+
+int counters_reset(syzsig_ctx* ctx)
+{
+	SYZ_HIP(hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * kNumCounters, ctx->stream));
+	return SYZSIG_OK;
+}
+
+int counters_fetch(syzsig_ctx* ctx)
+{
+	SYZ_HIP(hipMemcpyAsync(ctx->h_cnt, ctx->d_cnt, sizeof(unsigned long long) * kNumCounters,
+	                       hipMemcpyDeviceToHost, ctx->stream));
+	SYZ_HIP(hipStreamSynchronize(ctx->stream));
+	return SYZSIG_OK;
+}
+
+}  // namespace syz
+
+extern "C" {
+
+int syzsig_abi_version(void) { return SYZSIG_ABI_VERSION; }
+
+const char* syzsig_last_error(void) { return syz::g_last_error.c_str(); }
+
+int syzsig_ctx_create(int device, syzsig_ctx** out)
+{
+	if (!out)
+		return syz::fail(SYZSIG_EINVAL, "ctx_create: out is NULL");
+	*out = nullptr;
+	int ndev = 0;
+	SYZ_HIP(hipGetDeviceCount(&ndev));
+	if (device < 0 || device >= ndev)
+		return syz::fail(SYZSIG_EINVAL, "ctx_create: no such HIP device");
+	SYZ_HIP(hipSetDevice(device));
+	syzsig_ctx* c = new syzsig_ctx();
+	c->device = device;
+	hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+	if (e == hipSuccess)
+		e = hipMalloc(&c->d_cnt, sizeof(unsigned long long) * syz::kNumCounters);
+	if (e == hipSuccess)
+		e = hipHostMalloc(&c->h_cnt, sizeof(unsigned long long) * syz::kNumCounters, hipHostMallocDefault);
+	if (e != hipSuccess) {
+		syzsig_ctx_destroy(c);
+		return syz::hip_fail(e, "ctx_create", __FILE__, __LINE__);
+	}
+	c->stream = c->own_stream;
+	*out = c;
+	return SYZSIG_OK;
+}
+
+void syzsig_ctx_destroy(syzsig_ctx* c)
+{
+	if (!c)
+		return;
+	(void)hipSetDevice(c->device);
+	if (c->stream)
+		(void)hipStreamSynchronize(c->stream);
+	for (auto& w : c->ws)
+		if (w.ptr)
+			(void)hipFree(w.ptr);
+	if (c->d_cnt)
+		(void)hipFree(c->d_cnt);
+	if (c->h_cnt)
+		(void)hipHostFree(c->h_cnt);
+	for (auto& e : c->ev)
+		if (e)
+			(void)hipEventDestroy(e);
+	if (c->own_stream)
+		(void)hipStreamDestroy(c->own_stream);
+	delete c;
+}
+
+int syzsig_ctx_set_stream(syzsig_ctx* ctx, void* stream)
+{
+	if (!ctx)
+		return syz::fail(SYZSIG_EINVAL, "ctx_set_stream: ctx is NULL");
+	ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+	return SYZSIG_OK;
+}
+
+void* syzsig_ctx_stream(syzsig_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable)
+{
+	if (!ctx)
+		return syz::fail(SYZSIG_EINVAL, "ctx_set_timing: ctx is NULL");
+	if (enable && !ctx->ev[0])
+		for (auto& e : ctx->ev)
+			SYZ_HIP(hipEventCreate(&e));
+	ctx->timing = enable != 0;
+	return SYZSIG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,597 @@
+// triage.hip -- K3: batched checkNewSignal (DiffRaw + Merge) against a
+// device-resident maxSignal, bit-exact with the reference's sequential order.
+//
+// Reference: syz-fuzzer/fuzzer.go:494-511 checkNewSignal, pkg/signal/signal.go
+// :90-102 DiffRaw and :117-131 Merge.  Over a batch in serial order
+// (program-major, call-minor; call k has raw signal sig_k and prio p_k), with
+// M0 = maxSignal before the batch:
+//
+//   e in new_k  <=>  e in sig_k  and  p_k > M0[e]  and  no j < k has e in sig_j with p_j >= p_k
+//   M_final[e]  =  max(M0[e], max_k p_k)               (absent < every prio)
+//   newSignal   +=  { e : M_final[e] != M0[e] } with prio M_final[e]
+//
+// Parallel restatement (per run of calls with <= 4 distinct prios, each prio
+// mapped to a level by signed order): for every slot and level keep
+//   first[slot][l] = min serial k over records of level l  (epoch-tagged u32)
+// Phase 1 (probe): each record finds/inserts its element, drops itself if
+//   p_k <= M0[e] or if an already-recorded first at a level >= l is < k
+//   (firsts only decrease, so a stale read never drops a record wrongly),
+//   else atomicMin's its level and is kept as a candidate.  The thread that
+//   first marks a slot "touched" becomes its committer.
+// Phase 2 (decide): a candidate is new iff min_{l' >= l} first[l'] == k; the
+//   committer writes M_final (top set level) and merges it into newSignal.
+// One wave per call; candidates are compacted in place inside the call's own
+// record range, so the phases need no global atomics besides the per-block
+// counters.
+#include <algorithm>
+#include <vector>
+
+#include "internal.h"
+
+namespace syz {
+
+
+__device__ __forceinline__ uint32_t min_from_level(uint4 f, uint32_t l)
+{
+	uint32_t m = f.w;
+	if (l <= 2)
+		m = min(m, f.z);
+	if (l <= 1)
+		m = min(m, f.y);
+	if (l == 0)
+		m = min(m, f.x);
+	return m;
+}
+
+__device__ __forceinline__ uint32_t first_at(uint4 f, uint32_t l)
+{
+	return l == 0 ? f.x : l == 1 ? f.y : l == 2 ? f.z : f.w;
+}
+
+// ---------------------------------------------------------------- inputs
+// A batch is processed as segments, one wave each; candidates are compacted in
+// place inside the segment's own record range.
+//  - CallsIn: segment = one call (local batch); prio and serial uniform per call.
+//  - RecsIn:  segment = 4096 packed records (owner side of a sharded batch).
+struct Seg {
+	uint64_t start;  // first record
+	uint32_t len;    // records
+	uint32_t level;  // CallsIn: the call's level
+	uint32_t serial; // CallsIn: the call's serial index in the run
+	bool ok;
+};
+
+struct CallsIn {
+	const uint32_t* sigs;
+	const uint64_t* call_start;
+	const uint32_t* call_len;
+	const uint8_t* call_prio;
+	uint64_t c0, c1, nrec;
+	uint32_t* new_bits;
+	uint8_t* call_new;
+
+	__device__ uint64_t nseg() const { return c1 - c0; }
+	__device__ Seg seg(uint64_t s, const LevelMap& lm) const
+	{
+		Seg g;
+		const uint64_t c = c0 + s;
+		g.start = call_start[c];
+		g.len = call_len[c];
+		g.ok = g.start <= nrec && g.len <= nrec - g.start && g.len <= kSerialMask;
+		g.level = lm.lvl[call_prio[c]];
+		g.ok = g.ok && g.level < lm.n;
+		g.serial = (uint32_t)s;
+		return g;
+	}
+	// element, level, serial of record j of segment g
+	__device__ void rec(const Seg& g, uint32_t j, uint32_t& e, uint32_t& l, uint32_t& k) const
+	{
+		e = sigs[g.start + j];
+		l = g.level;
+		k = g.serial;
+	}
+	__device__ void mark_new(const Seg& g, uint32_t j) const
+	{
+		const uint64_t r = g.start + j;
+		atomicOr(&new_bits[r >> 5], 1u << (r & 31));
+	}
+	__device__ void seg_has_new(uint64_t s) const { call_new[c0 + s] = 1; }
+};
+
+constexpr uint32_t kSegRecs = 4096;
+
+struct RecsIn {
+	const uint64_t* recs;
+	uint64_t nrec;
+	uint8_t* new_flags;
+
+	__device__ uint64_t nseg() const { return (nrec + kSegRecs - 1) / kSegRecs; }
+	__device__ Seg seg(uint64_t s, const LevelMap&) const
+	{
+		Seg g;
+		g.start = s * kSegRecs;
+		g.len = (uint32_t)min<uint64_t>(kSegRecs, nrec - g.start);
+		g.ok = true;
+		g.level = 0;
+		g.serial = 0;
+		return g;
+	}
+	__device__ void rec(const Seg& g, uint32_t j, uint32_t& e, uint32_t& l, uint32_t& k) const
+	{
+		const uint64_t r = recs[g.start + j];
+		e = (uint32_t)(r >> 32);
+		l = (uint32_t)(r >> 24) & 0xff;
+		k = (uint32_t)r & kSerialMask;
+	}
+	__device__ void mark_new(const Seg& g, uint32_t j) const { new_flags[g.start + j] = 1; }
+	__device__ void seg_has_new(uint64_t) const {}
+};
+
+// ---------------------------------------------------------------- phase 1
+template <typename In>
+__global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, uint32_t* firsts, uint32_t* touched,
+                                               In in, LevelMap lm, uint32_t epoch, uint32_t* cand_slot,
+                                               uint32_t* cand_meta, uint32_t* cand_cnt, unsigned long long* cnt)
+{
+	const uint32_t lane = lane_id();
+	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	const uint64_t max_probe = max_probe_for(bmask);
+	const uint64_t nseg = in.nseg();
+	uint64_t ncand = 0, ntouch = 0, ovf = 0, err = 0;
+	for (uint64_t s = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); s < nseg; s += nwaves) {
+		const Seg g = in.seg(s, lm);
+		if (!g.ok) {
+			err += lane == 0;
+			if (lane == 0)
+				cand_cnt[s] = 0;
+			continue;
+		}
+		uint32_t nc = 0;
+		for (uint32_t base = 0; base < g.len; base += 64) {
+			const uint32_t j = base + lane;
+			bool cand = false, toucher = false;
+			uint32_t sidx = 0, l = 0;
+			if (j < g.len) {
+				uint32_t e, k;
+				in.rec(g, j, e, l, k);
+				if (l >= lm.n) {
+					err++;
+				} else {
+					// live slot low word of (e, p_k): p_k > M0[e]  <=>  old low word < want
+					const uint32_t want = (uint32_t)make_slot(0, lm.val[l]);
+					const uint32_t tag = (epoch << 24) | k;
+					uint64_t old;
+					const int64_t idx = tbl_find_or_insert(slots, bmask, e, make_absent(e), old, max_probe);
+					if (idx < 0) {
+						ovf++;
+					} else if (!slot_live(old) || (uint32_t)old < want) {
+						sidx = (uint32_t)idx;
+						const uint4 f = reinterpret_cast<const uint4*>(firsts)[sidx];
+						if (min_from_level(f, l) >= tag) {
+							const uint32_t prev = atomicMin(&firsts[4 * (uint64_t)sidx + l], tag);
+							if (prev > ((epoch << 24) | kSerialMask)) {
+								const uint32_t bit = 1u << (sidx & 31);
+								toucher = !(atomicOr(&touched[sidx >> 5], bit) & bit);
+							}
+							cand = true;
+						}
+					}
+				}
+			}
+			const uint64_t m = __ballot(cand);
+			if (cand) {
+				const uint64_t pos = g.start + nc + lane_rank(m);
+				cand_slot[pos] = sidx;
+				cand_meta[pos] = ((uint32_t)toucher << 31) | (l << 24) | j;
+			}
+			nc += (uint32_t)__popcll(m);
+			ntouch += toucher;
+		}
+		if (lane == 0) {
+			cand_cnt[s] = nc;
+			ncand += nc;
+		}
+	}
+	block_count(&cnt[kCntCandidates], ncand);
+	block_count(&cnt[kCntTouched], ntouch);
+	block_count(&cnt[kCntOverflow], ovf);
+	block_count(&cnt[kCntError], err);
+}
+
+// ---------------------------------------------------------------- phase 2
+template <typename In>
+__global__ __launch_bounds__(256) void k_decide(uint64_t* slots, const uint32_t* __restrict__ firsts,
+                                                uint64_t* ns_slots, uint64_t ns_bmask, In in, LevelMap lm,
+                                                uint32_t epoch, const uint32_t* __restrict__ cand_slot,
+                                                const uint32_t* __restrict__ cand_meta,
+                                                const uint32_t* __restrict__ cand_cnt, unsigned long long* cnt)
+{
+	const uint32_t lane = lane_id();
+	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	const uint32_t cur_hi = (epoch << 24) | kSerialMask;
+	const uint64_t nseg = in.nseg();
+	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0;
+	for (uint64_t s = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); s < nseg; s += nwaves) {
+		const uint32_t nc = cand_cnt[s];
+		if (nc == 0)
+			continue;
+		const Seg g = in.seg(s, lm);
+		bool any_new = false;
+		for (uint32_t base = 0; base < nc; base += 64) {
+			const uint32_t i = base + lane;
+			if (i >= nc)
+				continue;
+			const uint32_t sidx = cand_slot[g.start + i];
+			const uint32_t meta = cand_meta[g.start + i];
+			const uint32_t l = (meta >> 24) & 3, j = meta & kSerialMask;
+			uint32_t e, l2, k;
+			in.rec(g, j, e, l2, k);
+			const uint4 f = reinterpret_cast<const uint4*>(firsts)[sidx];
+			if (min_from_level(f, l) == ((epoch << 24) | k)) {
+				in.mark_new(g, j);
+				any_new = true;
+			}
+			if (meta >> 31) {
+				// committer: M_final = prio of the highest level recorded this epoch
+				uint32_t top = 0;
+#pragma unroll
+				for (uint32_t t = 0; t < 4; t++)
+					if (t < lm.n && first_at(f, t) <= cur_hi)
+						top = t;
+				const int8_t P = lm.val[top];
+				const uint64_t old = slots[sidx];
+				slots[sidx] = make_slot(e, P);
+				inserted += !slot_live(old);
+				changed++;
+				const int r = tbl_merge(ns_slots, ns_bmask, e, P);
+				ns_ins += r == 1;
+				ovf += r < 0;
+			}
+		}
+		if (__ballot(any_new) && lane == 0)
+			in.seg_has_new(s);
+	}
+	block_count(&cnt[kCntInserted], inserted);
+	block_count(&cnt[kCntChanged], changed);
+	block_count(&cnt[kCntAux], ns_ins);
+	block_count(&cnt[kCntOverflow], ovf);
+}
+
+// prio presence over calls -> 256-bit mask (block-local, one atomic per word per block)
+__global__ void k_prio_presence(const uint8_t* __restrict__ prio, uint64_t n, uint32_t* mask)
+{
+	__shared__ uint32_t m[8];
+	if (threadIdx.x < 8)
+		m[threadIdx.x] = 0;
+	__syncthreads();
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+		uint8_t p = prio[i];
+		atomicOr(&m[p >> 5], 1u << (p & 31));
+	}
+	__syncthreads();
+	if (threadIdx.x < 8 && m[threadIdx.x])
+		atomicOr(&mask[threadIdx.x], m[threadIdx.x]);
+}
+
+// ---------------------------------------------------------------- host
+
+struct Run {
+	uint64_t c0, c1;
+	LevelMap lm;
+};
+
+static void level_map_from(const bool present[256], LevelMap* lm)
+{
+	memset(lm, 0xff, sizeof(*lm));
+	// levels in signed int8 order of the prio (DiffRaw compares prioType(prio))
+	uint32_t n = 0;
+	for (int v = -128; v <= 127; v++) {
+		uint8_t u = (uint8_t)(int8_t)v;
+		if (present[u]) {
+			lm->lvl[u] = (uint8_t)n;
+			lm->val[n] = (int8_t)v;
+			n++;
+		}
+	}
+	lm->n = n;
+}
+
+static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* runs)
+{
+	void* dmask;
+	SYZ_TRY(ws_get(ctx, 6, 64, &dmask));
+	SYZ_HIP(hipMemsetAsync(dmask, 0, 32, ctx->stream));
+	k_prio_presence<<<grid_for(b->ncalls, 256, 256), 256, 0, ctx->stream>>>(b->call_prio, b->ncalls,
+	                                                                        (uint32_t*)dmask);
+	SYZ_HIP(hipGetLastError());
+	uint32_t hmask[8];
+	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 32, hipMemcpyDeviceToHost, ctx->stream));
+	SYZ_HIP(hipStreamSynchronize(ctx->stream));
+	bool present[256];
+	int np = 0;
+	for (int i = 0; i < 256; i++) {
+		present[i] = (hmask[i >> 5] >> (i & 31)) & 1;
+		np += present[i];
+	}
+	if (np <= 4) {
+		LevelMap lm;
+		level_map_from(present, &lm);
+		for (uint64_t c0 = 0; c0 < b->ncalls; c0 += kSerialMask)
+			runs->push_back({c0, std::min<uint64_t>(b->ncalls, c0 + kSerialMask), lm});
+		return SYZSIG_OK;
+	}
+	// More than 4 distinct prios: split the serial order into maximal runs with
+	// <= 4 distinct prios each; runs execute one after another, so each sees
+	// the merges of all earlier calls exactly as the sequential loop does.
+	std::vector<uint8_t> hp(b->ncalls);
+	SYZ_HIP(hipMemcpy(hp.data(), b->call_prio, b->ncalls, hipMemcpyDeviceToHost));
+	uint64_t c0 = 0;
+	while (c0 < b->ncalls) {
+		bool pres[256] = {false};
+		int cnt = 0;
+		uint64_t c = c0;
+		for (; c < b->ncalls && c - c0 < kSerialMask; c++) {
+			if (!pres[hp[c]]) {
+				if (cnt == 4)
+					break;
+				pres[hp[c]] = true;
+				cnt++;
+			}
+		}
+		LevelMap lm;
+		level_map_from(pres, &lm);
+		runs->push_back({c0, c, lm});
+		c0 = c;
+	}
+	return SYZSIG_OK;
+}
+
+// One run (<= 4 prio levels): probe, then decide+commit.  On capacity
+// overflow the run's only table side effects -- absent markers -- are dropped
+// by a rehash into a bigger table and the run restarts.
+template <typename In>
+static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const In& in, uint64_t nseg,
+                      const LevelMap& lm, uint32_t* cand_slot, uint32_t* cand_meta, uint32_t* cand_cnt,
+                      syzsig_batch_stats* st)
+{
+	for (;;) {
+		if (--ms->epoch == 0) {
+			SYZ_HIP(hipMemsetAsync(ms->firsts, 0xff, ms->nslots() * 16, ctx->stream));
+			ms->epoch = 254;
+		}
+		SYZ_HIP(hipMemsetAsync(ms->touched, 0, (ms->nslots() / 32 + 1) * 4, ctx->stream));
+		SYZ_TRY(counters_reset(ctx));
+		const int grid = grid_for(nseg * 64, 256, 4096);
+		if (ctx->timing)
+			SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
+		k_probe<In><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in, lm,
+		                                           ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt);
+		SYZ_HIP(hipGetLastError());
+		if (ctx->timing)
+			SYZ_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
+		SYZ_TRY(counters_fetch(ctx));
+		if (ctx->timing) {
+			float ms = 0;
+			SYZ_HIP(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
+			st->probe_ms += ms;
+		}
+		if (ctx->h_cnt[kCntError])
+			return fail(SYZSIG_EINVAL, "triage: a call range lies outside [0, nrec), a call has >= 2^24 "
+			                           "records, or a record's prio level is out of range");
+		if (ctx->h_cnt[kCntOverflow]) {
+			SYZ_TRY(set_rehash(ms, ms->nbuckets * 8, true));
+			st->retries++;
+			continue;
+		}
+		const uint64_t touched = ctx->h_cnt[kCntTouched];
+		st->candidates += ctx->h_cnt[kCntCandidates];
+		if (touched && !*ns)
+			SYZ_TRY(syzsig_set_make(ctx, touched, ns));  // newSignal.Merge allocates (signal.go:121-125)
+		if (touched)
+			SYZ_TRY(set_reserve(*ns, touched));
+		SYZ_TRY(counters_reset(ctx));
+		syzsig_set* nsp = *ns;
+		if (ctx->timing)
+			SYZ_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
+		k_decide<In><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->firsts, nsp ? nsp->slots : nullptr,
+		                                            nsp ? nsp->nbuckets - 1 : 0, in, lm, ms->epoch, cand_slot,
+		                                            cand_meta, cand_cnt, ctx->d_cnt);
+		SYZ_HIP(hipGetLastError());
+		if (ctx->timing)
+			SYZ_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
+		SYZ_TRY(counters_fetch(ctx));
+		if (ctx->timing) {
+			float ms = 0;
+			SYZ_HIP(hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]));
+			st->decide_ms += ms;
+		}
+		if (ctx->h_cnt[kCntOverflow])
+			return fail(SYZSIG_EIO, "newSignal overflow (internal error)");
+		ms->len += ctx->h_cnt[kCntInserted];
+		st->inserted += ctx->h_cnt[kCntInserted];
+		st->changed += ctx->h_cnt[kCntChanged];
+		if (nsp)
+			nsp->len += ctx->h_cnt[kCntAux];
+		st->runs++;
+		return SYZSIG_OK;
+	}
+}
+
+int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b,
+                      syzsig_batch_stats* st)
+{
+	SYZ_HIP(hipMemsetAsync(b->new_bits, 0, ((b->nrec + 31) / 32) * 4, ctx->stream));
+	if (b->ncalls)
+		SYZ_HIP(hipMemsetAsync(b->call_new, 0, b->ncalls, ctx->stream));
+	st->records = b->nrec;
+	if (b->ncalls == 0 || b->nrec == 0) {
+		SYZ_HIP(hipStreamSynchronize(ctx->stream));
+		return SYZSIG_OK;
+	}
+	SYZ_TRY(set_ensure_triage_state(ms));
+	std::vector<Run> runs;
+	SYZ_TRY(plan_runs(ctx, b, &runs));
+	uint64_t maxrun = 0;
+	for (auto& r : runs)
+		maxrun = std::max(maxrun, r.c1 - r.c0);
+	void *cs, *cm, *cc;
+	SYZ_TRY(ws_get(ctx, 3, b->nrec * 4, &cs));
+	SYZ_TRY(ws_get(ctx, 4, b->nrec * 4, &cm));
+	SYZ_TRY(ws_get(ctx, 5, maxrun * 4, &cc));
+	for (auto& r : runs) {
+		CallsIn in;
+		in.sigs = b->sigs;
+		in.call_start = b->call_start;
+		in.call_len = b->call_len;
+		in.call_prio = b->call_prio;
+		in.c0 = r.c0;
+		in.c1 = r.c1;
+		in.nrec = b->nrec;
+		in.new_bits = b->new_bits;
+		in.call_new = b->call_new;
+		SYZ_TRY(triage_run(ctx, ms, ns, in, r.c1 - r.c0, r.lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
+	}
+	if ((double)ms->len > kMaxLoad * (double)ms->nslots())
+		SYZ_TRY(set_rehash(ms, buckets_for(ms->len), false));
+	st->new_signal_len = syzsig_len(*ns);
+	return SYZSIG_OK;
+}
+
+// levels[] (ascending int8, <= 4) -> LevelMap
+int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm)
+{
+	if (!levels || nlevels == 0 || nlevels > 4)
+		return fail(SYZSIG_EINVAL, "levels: need 1..4 prio levels");
+	bool present[256] = {false};
+	for (uint32_t i = 0; i < nlevels; i++) {
+		if (i && levels[i] <= levels[i - 1])
+			return fail(SYZSIG_EINVAL, "levels: must be strictly ascending");
+		present[(uint8_t)levels[i]] = true;
+	}
+	level_map_from(present, lm);
+	return SYZSIG_OK;
+}
+
+int triage_records_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t nrec,
+                        const int8_t* levels, uint32_t nlevels, uint8_t* new_flags, syzsig_batch_stats* st)
+{
+	LevelMap lm;
+	SYZ_TRY(level_map_from_levels(levels, nlevels, &lm));
+	st->records = nrec;
+	if (nrec == 0)
+		return SYZSIG_OK;
+	SYZ_HIP(hipMemsetAsync(new_flags, 0, nrec, ctx->stream));
+	SYZ_TRY(set_ensure_triage_state(ms));
+	const uint64_t nseg = (nrec + kSegRecs - 1) / kSegRecs;
+	void *cs, *cm, *cc;
+	SYZ_TRY(ws_get(ctx, 3, nrec * 4, &cs));
+	SYZ_TRY(ws_get(ctx, 4, nrec * 4, &cm));
+	SYZ_TRY(ws_get(ctx, 5, nseg * 4, &cc));
+	RecsIn in;
+	in.recs = recs;
+	in.nrec = nrec;
+	in.new_flags = new_flags;
+	SYZ_TRY(triage_run(ctx, ms, ns, in, nseg, lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
+	if ((double)ms->len > kMaxLoad * (double)ms->nslots())
+		SYZ_TRY(set_rehash(ms, buckets_for(ms->len), false));
+	st->new_signal_len = syzsig_len(*ns);
+	return SYZSIG_OK;
+}
+
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" {
+
+int syzsig_triage_batch(syzsig_ctx* ctx, syzsig_set* max_signal, syzsig_set** new_signal, const syzsig_batch* b,
+                        syzsig_batch_stats* stats)
+{
+	if (!ctx || !max_signal || !new_signal || !b)
+		return fail(SYZSIG_EINVAL, "triage_batch: NULL argument");
+	if (*new_signal == max_signal)
+		return fail(SYZSIG_EINVAL, "triage_batch: new_signal aliases max_signal");
+	if (b->nrec && (!b->sigs || !b->new_bits))
+		return fail(SYZSIG_EINVAL, "triage_batch: NULL record arrays");
+	if (b->ncalls && (!b->call_start || !b->call_len || !b->call_prio || !b->call_new))
+		return fail(SYZSIG_EINVAL, "triage_batch: NULL call arrays");
+	syzsig_batch_stats st;
+	memset(&st, 0, sizeof(st));
+	int rc = triage_batch_impl(ctx, max_signal, new_signal, b, &st);
+	if (stats)
+		*stats = st;
+	return rc;
+}
+
+int syzsig_check_new_signal(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_signal, const uint32_t* sigs,
+                            uint64_t nrec, const uint64_t* call_start, const uint32_t* call_len,
+                            const uint8_t* call_prio, uint32_t ncalls, uint32_t* out_calls, uint32_t* n_out,
+                            uint32_t* new_bits)
+{
+	if (!ctx || !max_signal || !new_signal || !n_out || (ncalls && (!call_start || !call_len || !call_prio)) ||
+	    (nrec && !sigs) || (ncalls && !out_calls))
+		return fail(SYZSIG_EINVAL, "check_new_signal: NULL argument");
+	*n_out = 0;
+	for (uint32_t i = 0; i < ncalls; i++)
+		if (call_start[i] > nrec || call_len[i] > nrec - call_start[i])
+			return fail(SYZSIG_EINVAL, "check_new_signal: call range outside sigs");
+	if (!*max_signal)
+		SYZ_TRY(syzsig_set_make(ctx, 0, max_signal));
+	const uint64_t nwords = (nrec + 31) / 32;
+	void *ds, *dcs, *dcl, *dcp, *dbits, *dnew;
+	SYZ_TRY(ws_get(ctx, 7, nrec * 4 + 4, &ds));
+	SYZ_TRY(ws_get(ctx, 8, ncalls * 8 + 8, &dcs));
+	SYZ_TRY(ws_get(ctx, 9, ncalls * 4 + 4, &dcl));
+	SYZ_TRY(ws_get(ctx, 10, ncalls + 1, &dcp));
+	SYZ_TRY(ws_get(ctx, 11, nwords * 4 + 4, &dbits));
+	SYZ_TRY(ws_get(ctx, 12, ncalls + 1, &dnew));
+	if (nrec)
+		SYZ_HIP(hipMemcpyAsync(ds, sigs, nrec * 4, hipMemcpyHostToDevice, ctx->stream));
+	if (ncalls) {
+		SYZ_HIP(hipMemcpyAsync(dcs, call_start, ncalls * 8, hipMemcpyHostToDevice, ctx->stream));
+		SYZ_HIP(hipMemcpyAsync(dcl, call_len, ncalls * 4, hipMemcpyHostToDevice, ctx->stream));
+		SYZ_HIP(hipMemcpyAsync(dcp, call_prio, ncalls, hipMemcpyHostToDevice, ctx->stream));
+	}
+	syzsig_batch b;
+	b.sigs = (const uint32_t*)ds;
+	b.call_start = (const uint64_t*)dcs;
+	b.call_len = (const uint32_t*)dcl;
+	b.call_prio = (const uint8_t*)dcp;
+	b.ncalls = ncalls;
+	b.nrec = nrec;
+	b.new_bits = (uint32_t*)dbits;
+	b.call_new = (uint8_t*)dnew;
+	syzsig_batch_stats st;
+	memset(&st, 0, sizeof(st));
+	SYZ_TRY(triage_batch_impl(ctx, *max_signal, new_signal, &b, &st));
+	std::vector<uint8_t> cn(ncalls);
+	if (ncalls)
+		SYZ_HIP(hipMemcpyAsync(cn.data(), dnew, ncalls, hipMemcpyDeviceToHost, ctx->stream));
+	if (new_bits && nwords)
+		SYZ_HIP(hipMemcpyAsync(new_bits, dbits, nwords * 4, hipMemcpyDeviceToHost, ctx->stream));
+	SYZ_HIP(hipStreamSynchronize(ctx->stream));
+	uint32_t n = 0;
+	for (uint32_t i = 0; i < ncalls; i++)
+		if (cn[i])
+			out_calls[n++] = i;
+	*n_out = n;
+	return SYZSIG_OK;
+}
+
+int syzsig_triage_records_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set** new_signal, const uint64_t* d_recs,
+                              uint64_t nrec, const int8_t* levels, uint32_t nlevels, uint8_t* d_new_flags,
+                              syzsig_batch_stats* stats)
+{
+	if (!ctx || !shard || !new_signal || (nrec && (!d_recs || !d_new_flags)))
+		return fail(SYZSIG_EINVAL, "triage_records: NULL argument");
+	if (*new_signal == shard)
+		return fail(SYZSIG_EINVAL, "triage_records: new_signal aliases the shard");
+	syzsig_batch_stats st;
+	memset(&st, 0, sizeof(st));
+	int rc = triage_records_impl(ctx, shard, new_signal, d_recs, nrec, levels, nlevels, d_new_flags, &st);
+	if (stats)
+		*stats = st;
+	return rc;
+}
+
+}  // extern "C"

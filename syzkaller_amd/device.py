@@ -1,0 +1,155 @@
+"""Batch (device-resident) API of the engine over torch tensors.
+
+torch is plumbing here: it owns HBM buffers and the stream; every computation
+runs in libsyzsig's HIP kernels.  All tensors must live on this Device's GPU.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import Batch, BatchStats, check
+from .signal import Signal, engine
+
+__all__ = ["Device", "call_layout"]
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr() if (t is not None and t.numel()) else 0)
+
+
+def call_layout(call_len, device=None):
+    """Exclusive prefix sum of per-call lengths -> call_start (u64 as int64)."""
+    call_len = torch.as_tensor(call_len, device=device)
+    start = torch.zeros(call_len.numel(), dtype=torch.int64, device=call_len.device)
+    if call_len.numel() > 1:
+        start[1:] = torch.cumsum(call_len[:-1].to(torch.int64), 0)
+    return start
+
+
+class Device:
+    def __init__(self, device=0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("syzkaller_amd.device needs a ROCm GPU (no CPU fallback)")
+        self.index = int(device)
+        self.dev = torch.device("cuda", self.index)
+        self.eng = engine(self.index)
+        self.sync_stream()
+
+    def sync_stream(self):
+        """Run library work on torch's current stream of this device."""
+        self.eng.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    @property
+    def L(self):
+        return self.eng.L
+
+    def _check_dev(self, *ts):
+        for t in ts:
+            if t is not None and t.device != self.dev:
+                raise ValueError(f"tensor on {t.device}, expected {self.dev}")
+            if t is not None and not t.is_contiguous():
+                raise ValueError("tensors must be contiguous")
+
+    # ---------------------------------------------------------------- sets
+    def new_set(self, hint=0):
+        return Signal.make(hint, self.eng)
+
+    def deserialize(self, elems, prios):
+        self._check_dev(elems, prios)
+        assert elems.dtype == torch.int32 or elems.dtype == torch.uint32
+        h = ctypes.c_void_p()
+        check(self.L.syzsig_deserialize_dev(self.eng.h, _p(elems), _p(prios), elems.numel(), ctypes.byref(h)))
+        return Signal(h, self.eng)
+
+    # ---------------------------------------------------------------- K3
+    def batch(self, sigs, call_start, call_len, call_prio, new_bits=None, call_new=None):
+        self._check_dev(sigs, call_start, call_len, call_prio, new_bits, call_new)
+        nrec, ncalls = sigs.numel(), call_len.numel()
+        if new_bits is None:
+            new_bits = torch.empty((nrec + 31) // 32, dtype=torch.int32, device=self.dev)
+        if call_new is None:
+            call_new = torch.empty(ncalls, dtype=torch.uint8, device=self.dev)
+        b = Batch(sigs=_p(sigs).value, call_start=_p(call_start).value, call_len=_p(call_len).value,
+                  call_prio=_p(call_prio).value, ncalls=ncalls, nrec=nrec, new_bits=_p(new_bits).value,
+                  call_new=_p(call_new).value)
+        return b, new_bits, call_new
+
+    def triage(self, max_signal, new_signal, sigs, call_start, call_len, call_prio, new_bits=None, call_new=None):
+        """checkNewSignal over a whole batch (syz-fuzzer/fuzzer.go:494-511).
+        Returns (new_bits int32[ceil(nrec/32)], call_new uint8[ncalls], stats)."""
+        b, new_bits, call_new = self.batch(sigs, call_start, call_len, call_prio, new_bits, call_new)
+        st = BatchStats()
+        nh = ctypes.c_void_p(new_signal.handle.value or 0)
+        check(self.L.syzsig_triage_batch(self.eng.h, max_signal.handle, ctypes.byref(nh), ctypes.byref(b),
+                                         ctypes.byref(st)))
+        if nh.value and new_signal.is_nil():
+            new_signal._h = nh
+        return new_bits, call_new, st.as_dict()
+
+    # ---------------------------------------------------------------- K1+K2
+    def edge_derive(self, pcs, call_start, call_len, prog_call, sigs=None, sig_cnt=None, completed=None):
+        """executor write_coverage_signal for every program of a batch."""
+        self._check_dev(pcs, call_start, call_len, prog_call, sigs, sig_cnt, completed)
+        nprog = prog_call.numel() - 1
+        if sigs is None:
+            sigs = torch.empty(pcs.numel(), dtype=torch.int32, device=self.dev)
+        if sig_cnt is None:
+            sig_cnt = torch.empty(call_len.numel(), dtype=torch.int32, device=self.dev)
+        if completed is None:
+            completed = torch.empty(max(nprog, 0), dtype=torch.int32, device=self.dev)
+        check(self.L.syzsig_edge_derive_dev(self.eng.h, _p(pcs), pcs.numel(), _p(call_start), _p(call_len),
+                                            call_len.numel(), _p(prog_call), max(nprog, 0), _p(sigs), _p(sig_cnt),
+                                            _p(completed)))
+        return sigs, sig_cnt, completed
+
+    # ---------------------------------------------------------------- K5
+    def minimize(self, ctx_off, elems, prios, hint_distinct=0):
+        self._check_dev(ctx_off, elems, prios)
+        n = ctx_off.numel() - 1
+        keep = torch.empty(max(n, 0), dtype=torch.uint8, device=self.dev)
+        cnt = ctypes.c_uint64()
+        check(self.L.syzsig_minimize_dev(self.eng.h, _p(ctx_off), _p(elems), _p(prios), max(n, 0),
+                                         int(hint_distinct), _p(keep), ctypes.byref(cnt)))
+        return keep, int(cnt.value)
+
+    # ---------------------------------------------------------------- sharding
+    def shard_partition(self, b, serial_base, levels, nshards, send, send_pos):
+        lv = (ctypes.c_int8 * len(levels))(*levels)
+        counts = (ctypes.c_uint64 * nshards)()
+        check(self.L.syzsig_shard_partition_dev(self.eng.h, ctypes.byref(b), int(serial_base), lv, len(levels),
+                                                int(nshards), _p(send), _p(send_pos), counts))
+        return [int(c) for c in counts]
+
+    def triage_records(self, shard, new_signal, recs, levels, new_flags):
+        self._check_dev(recs, new_flags)
+        lv = (ctypes.c_int8 * len(levels))(*levels)
+        st = BatchStats()
+        nh = ctypes.c_void_p(new_signal.handle.value or 0)
+        check(self.L.syzsig_triage_records_dev(self.eng.h, shard.handle, ctypes.byref(nh), _p(recs), recs.numel(),
+                                               lv, len(levels), _p(new_flags), ctypes.byref(st)))
+        if nh.value and new_signal.is_nil():
+            new_signal._h = nh
+        return st.as_dict()
+
+    def shard_unpartition(self, b, send_pos, back_flags):
+        check(self.L.syzsig_shard_unpartition_dev(self.eng.h, ctypes.byref(b), _p(send_pos), _p(back_flags)))
+
+    # ---------------------------------------------------------------- synthetic data
+    def synth_traces(self, cfg, prog_base, nprog, calls_per_prog, call_len):
+        """-> (pcs int64[sum], call_start int64[n], call_prio uint8[n]) for nprog programs."""
+        call_len = call_len.to(self.dev, torch.int32).contiguous()
+        call_start = call_layout(call_len)
+        total = int(call_len.to(torch.int64).sum().item())
+        pcs = torch.empty(total, dtype=torch.int64, device=self.dev)
+        prio = torch.empty(call_len.numel(), dtype=torch.uint8, device=self.dev)
+        check(self.L.syzsig_synth_traces_dev(self.eng.h, ctypes.byref(cfg), int(prog_base), int(nprog),
+                                             int(calls_per_prog), _p(call_start), _p(call_len), _p(pcs), _p(prio)))
+        return pcs, call_start, call_len, prio
+
+    def synth_m0(self, cfg, known_sys, n):
+        elems = torch.empty(n, dtype=torch.int32, device=self.dev)
+        prios = torch.empty(n, dtype=torch.int8, device=self.dev)
+        check(self.L.syzsig_synth_m0_dev(self.eng.h, ctypes.byref(cfg), int(known_sys), int(n), _p(elems),
+                                         _p(prios)))
+        return elems, prios

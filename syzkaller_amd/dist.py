@@ -1,0 +1,110 @@
+"""Hash-sharded maxSignal across GPUs: one process per GPU, torch.distributed
+(RCCL over xGMI on MI355X; gloo in CPU tests).
+
+A batch is split by program range: rank r triages programs
+[r*P, (r+1)*P), so the global serial order is rank-major (the order a single
+fuzzer would see them).  maxSignal is partitioned by element:
+shard(e) = owner_of(e, world) (csrc/common.h).  One step:
+
+  1. levels  = union of every rank's call prios          (all_reduce, 256 ints)
+  2. partition records by owner                          (shard.hip)
+  3. exchange counts, then records                       (all_to_all_single)
+  4. owner triages the records it received               (triage.hip, records mode)
+  5. new-flags travel back to the sources                (all_to_all_single)
+  6. sources scatter flags to record bits / call flags   (shard.hip)
+
+Only step 3/5 move data between GPUs; each element's whole history in the
+batch lands on one owner, which applies the exact serial semantics via the
+serial index carried in every record (see triage.hip).
+"""
+import torch
+import torch.distributed as dist
+
+__all__ = ["owner_of_torch", "ShardedTriage", "GpuShardOps"]
+
+_M32 = 0xFFFFFFFF
+
+
+def _fmix32(h):
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _M32
+    h = h ^ (h >> 16)
+    return h
+
+
+def owner_of_torch(elems, nshards):
+    """syz::owner_of over an int32/int64 tensor of elements (as u32)."""
+    e = elems.to(torch.int64) & _M32
+    h = _fmix32((e * 0x9E3779B1 + 0x7F4A7C15) & _M32)
+    return (h * nshards) >> 32
+
+
+class GpuShardOps:
+    """The device half of a sharded step, on libsyzsig."""
+
+    def __init__(self, dev):
+        self.dev = dev
+
+    def partition(self, batch, serial_base, levels, nshards):
+        b, new_bits, call_new = batch
+        n = b.nrec
+        send = torch.empty(n, dtype=torch.int64, device=self.dev.dev)
+        send_pos = torch.empty(n, dtype=torch.int32, device=self.dev.dev)
+        counts = self.dev.shard_partition(b, serial_base, levels, nshards, send, send_pos)
+        return send, send_pos, counts
+
+    def triage_records(self, shard, new_signal, recs, levels):
+        flags = torch.empty(recs.numel(), dtype=torch.uint8, device=self.dev.dev)
+        st = self.dev.triage_records(shard, new_signal, recs, levels, flags)
+        return flags, st
+
+    def unpartition(self, batch, send_pos, back):
+        b, new_bits, call_new = batch
+        self.dev.shard_unpartition(b, send_pos, back)
+        return new_bits, call_new
+
+
+class ShardedTriage:
+    def __init__(self, ops, shard, new_signal, group=None, device=None):
+        self.ops = ops
+        self.shard = shard            # this rank's maxSignal shard
+        self.new_signal = new_signal  # this rank's newSignal shard
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = device
+
+    def levels(self, call_prio):
+        """Union of the prios of all ranks' calls, ascending as int8."""
+        present = torch.zeros(256, dtype=torch.int32, device=call_prio.device)
+        if call_prio.numel():
+            present[call_prio.to(torch.int64)] = 1
+        dist.all_reduce(present, op=dist.ReduceOp.MAX, group=self.group)
+        vals = [v if v < 128 else v - 256 for v in torch.nonzero(present).flatten().tolist()]
+        return sorted(vals)
+
+    def step(self, batch, call_prio, serial_base):
+        """batch = (Batch, new_bits, call_new) for this rank's calls."""
+        levels = self.levels(call_prio)
+        if len(levels) > 4:
+            raise ValueError("sharded triage supports <= 4 distinct prios per batch (signalPrio gives 0..3)")
+        if not levels:
+            levels = [0]
+        send, send_pos, counts = self.ops.partition(batch, serial_base, levels, self.world)
+        dev = send.device
+        cnt_out = torch.tensor(counts, dtype=torch.int64, device=dev)
+        cnt_in = torch.empty_like(cnt_out)
+        dist.all_to_all_single(cnt_in, cnt_out, group=self.group)
+        recv_counts = cnt_in.tolist()
+        recv = torch.empty(sum(recv_counts), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv, send, recv_counts, counts, group=self.group)
+        flags, st = self.ops.triage_records(self.shard, self.new_signal, recv, levels)
+        back = torch.empty(send.numel(), dtype=torch.uint8, device=dev)
+        dist.all_to_all_single(back, flags, counts, recv_counts, group=self.group)
+        new_bits, call_new = self.ops.unpartition(batch, send_pos, back)
+        st = dict(st)
+        st["sent"] = int(send.numel())
+        st["received"] = int(recv.numel())
+        return new_bits, call_new, st

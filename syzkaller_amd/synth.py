@@ -1,0 +1,48 @@
+"""Host-side synthetic KCOV workload (numpy), produced by libsyzsig's host
+generator -- the same code the device generator runs (csrc/common.h), so host
+checkers and GPU kernels see identical traces.  Needs no GPU."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, synth_default
+
+__all__ = ["synth_default", "call_lengths", "traces", "m0", "prog_call_index"]
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data) if a.size else ctypes.c_void_p(0)
+
+
+def call_lengths(nprog, calls_per_prog, length, ragged=None, seed=0):
+    """Per-call PC counts: fixed `length`, or uniform in [ragged[0], ragged[1]]."""
+    n = nprog * calls_per_prog
+    if ragged is None:
+        return np.full(n, length, dtype=np.uint32)
+    rng = np.random.default_rng(seed)
+    return rng.integers(ragged[0], ragged[1] + 1, size=n).astype(np.uint32)
+
+
+def prog_call_index(nprog, calls_per_prog):
+    return (np.arange(nprog + 1, dtype=np.uint32) * calls_per_prog).astype(np.uint32)
+
+
+def traces(cfg, prog_base, nprog, calls_per_prog, call_len):
+    """-> pcs u64[sum(call_len)], call_start u64[n], call_prio u8[n]"""
+    call_len = np.ascontiguousarray(call_len, dtype=np.uint32)
+    call_start = np.zeros(call_len.size, dtype=np.uint64)
+    if call_len.size > 1:
+        np.cumsum(call_len[:-1], out=call_start[1:])
+    pcs = np.empty(int(call_len.sum()), dtype=np.uint64)
+    prio = np.empty(call_len.size, dtype=np.uint8)
+    check(_lib.lib().syzsig_synth_traces_host(ctypes.byref(cfg), prog_base, nprog, calls_per_prog, _p(call_start),
+                                              _p(call_len), _p(pcs), _p(prio)))
+    return pcs, call_start, prio
+
+
+def m0(cfg, known_sys, n):
+    elems = np.empty(n, dtype=np.uint32)
+    prios = np.empty(n, dtype=np.int8)
+    check(_lib.lib().syzsig_synth_m0_host(ctypes.byref(cfg), known_sys, n, _p(elems), _p(prios)))
+    return elems, prios

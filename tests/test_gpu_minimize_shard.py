@@ -1,0 +1,106 @@
+"""GPU: K5 Minimize (minimize.hip) vs the oracle, and the shard routing
+(shard.hip + records-mode triage) vs unsharded triage on one GPU."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def corpus(rng, n, mean, universe, distinct_len=False):
+    if distinct_len:
+        lens = rng.permutation(np.arange(1, n * 3))[:n]
+    else:
+        lens = rng.geometric(1.0 / mean, size=n)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    elems = np.concatenate([rng.choice(universe, size=int(L), replace=False) for L in lens]).astype(np.uint32)
+    prios = rng.integers(0, 4, size=elems.size).astype(np.int8)
+    return off, elems, prios
+
+
+@pytest.mark.parametrize("seed,n,mean,U,distinct", [(0, 300, 50, 4000, True), (1, 2000, 200, 100000, False),
+                                                     (2, 5000, 30, 500, False)])
+def test_minimize_vs_oracle(gpu, seed, n, mean, U, distinct):
+    rng = np.random.default_rng(seed)
+    off, e, p = corpus(rng, n, mean, U, distinct)
+    exp = O.minimize(off, e, p)
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).to(gpu.dev)  # noqa: E731
+    keep, cnt = gpu.minimize(t(off, np.int64), t(e, np.int32), t(p, np.int8))
+    got = np.nonzero(keep.cpu().numpy())[0].tolist()
+    assert got == exp and cnt == len(exp)
+
+
+def test_minimize_host_api(gpu):
+    from syzkaller_amd import signal as S
+
+    rng = np.random.default_rng(4)
+    off, e, p = corpus(rng, 500, 40, 3000)
+    ctxs = [S.Context(S.Serial(e[off[i]:off[i + 1]], p[off[i]:off[i + 1]]).Deserialize(gpu.eng) if off[i + 1] > off[i]
+                      else S.Signal.make(0, gpu.eng), i) for i in range(500)]
+    got = sorted(S.Minimize(ctxs, gpu.eng))
+    assert got == O.minimize(off, e, p)
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_shard_routing_equals_unsharded(gpu, nshards):
+    """Hash-partition maxSignal into G tables on one GPU, route records with
+    partition -> triage_records (per shard) -> unpartition, and compare with
+    plain triage of the whole batch against the unsharded maxSignal."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+    from syzkaller_amd._lib import Batch  # noqa: F401
+    from tests.test_gpu_triage import dev_batch
+
+    cfg = synth.synth_default(skew=1)
+    nprog, cpp = 48, 32
+    cl = synth.call_lengths(nprog, cpp, 0, ragged=(0, 3000), seed=nshards)
+    ds, dcs, dcnt, dprio = dev_batch(gpu, cfg, nprog, cpp, cl)
+    m0e, m0p = synth.m0(cfg, 1024, 80000)
+    # unsharded reference run
+    ms = S.Serial(m0e, m0p).Deserialize(gpu.eng)
+    ns = S.Signal(None, gpu.eng)
+    bits, cnew, _ = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
+    # sharded: shard g holds the M0 elements it owns
+    owner = np.array([_owner(int(x), nshards) for x in m0e], np.uint32)
+    shards = [S.Serial(m0e[owner == g], m0p[owner == g]).Deserialize(gpu.eng) for g in range(nshards)]
+    news = [S.Signal(None, gpu.eng) for _ in range(nshards)]
+    levels = sorted(set(int(x) for x in dprio.cpu().numpy().astype(np.int8)))
+    b, sbits, scnew = gpu.batch(ds, dcs, dcnt, dprio)
+    send = torch.empty(ds.numel(), dtype=torch.int64, device=gpu.dev)
+    send_pos = torch.empty(ds.numel(), dtype=torch.int32, device=gpu.dev)
+    counts = gpu.shard_partition(b, 0, levels, nshards, send, send_pos)
+    flags = torch.zeros(ds.numel(), dtype=torch.uint8, device=gpu.dev)
+    off = 0
+    for g in range(nshards):
+        seg = send[off: off + counts[g]]
+        f = flags[off: off + counts[g]]
+        gpu.triage_records(shards[g], news[g], seg, levels, f)
+        off += counts[g]
+    gpu.shard_unpartition(b, send_pos, flags)
+    torch.cuda.synchronize()
+    assert torch.equal(scnew, cnew)
+    assert torch.equal(sbits, bits)
+    merged = {}
+    for g in range(nshards):
+        merged.update(shards[g].to_dict())
+    assert merged == ms.to_dict()
+    nmerged = {}
+    for g in range(nshards):
+        nmerged.update(news[g].to_dict() if not news[g].is_nil() else {})
+    assert nmerged == ns.to_dict()
+
+
+def _owner(e, n):
+    """syz::owner_of (csrc/common.h) restated for the test."""
+    def fmix(h):
+        h ^= h >> 16
+        h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+        h ^= h >> 13
+        h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+        h ^= h >> 16
+        return h
+    h = fmix((e * 0x9E3779B1 + 0x7F4A7C15) & 0xFFFFFFFF)
+    return (h * n) >> 32

@@ -1,0 +1,161 @@
+"""GPU: K3 batch triage (triage.hip) bit-exact against the sequential oracle
+(checkNewSignal over every call of the batch in serial order), plus
+size-independent properties at the BASELINE config-2 size."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _u(t, dt):
+    return t.cpu().numpy().view(dt)
+
+
+def host_batch(cfg, nprog, cpp, call_len, prog_base=0):
+    """host traces -> oracle executor -> per-call raw signal (sparse layout)"""
+    from syzkaller_amd import synth
+
+    pcs, cs, prio = synth.traces(cfg, prog_base, nprog, cpp, call_len)
+    sigs, cnt, comp = O.exec_batch(pcs, cs, call_len, synth.prog_call_index(nprog, cpp))
+    return sigs, cs, cnt, prio
+
+
+def dev_batch(gpu, cfg, nprog, cpp, call_len, prog_base=0):
+    """device traces -> K1+K2 -> per-call raw signal, all resident in HBM"""
+    from syzkaller_amd import synth
+
+    cl = torch.from_numpy(np.ascontiguousarray(call_len).view(np.int32))
+    pcs, cs, cl, prio = gpu.synth_traces(cfg, prog_base, nprog, cpp, cl)
+    pidx = torch.from_numpy(synth.prog_call_index(nprog, cpp).view(np.int32)).to(gpu.dev)
+    sigs, cnt, comp = gpu.edge_derive(pcs, cs, cl, pidx)
+    del pcs
+    return sigs, cs, cnt, prio
+
+
+def compare(gpu, m0, hb, db, new0=None, ms_hint=None):
+    from syzkaller_amd import signal as S
+
+    hs, hcs, hcnt, hprio = hb
+    ds, dcs, dcnt, dprio = db
+    np.testing.assert_array_equal(_u(dcnt, np.uint32), hcnt)
+    np.testing.assert_array_equal(_u(dprio, np.uint8), hprio)
+    ms = S.Serial(*m0).Deserialize(gpu.eng) if m0[0].size else S.Signal.make(ms_hint or 0, gpu.eng)
+    ns = S.Serial(*new0).Deserialize(gpu.eng) if new0 is not None else S.Signal(None, gpu.eng)
+    bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
+    oms, ons, obits, ocnew = O.triage_batch(m0[0], m0[1], hs, hcs, hcnt, hprio, new0)
+    np.testing.assert_array_equal(_u(cnew, np.uint8), ocnew)
+    np.testing.assert_array_equal(_u(bits, np.uint32), obits)
+    assert ms.Len() == oms.Len()
+    assert ms.to_dict() == oms.to_dict()
+    assert (ns.to_dict() if not ns.is_nil() else {}) == ons.to_dict()
+    assert ns.is_nil() == ons.is_nil()
+    return st
+
+
+@pytest.mark.parametrize("over,known,nm0", [({}, 2048, 200000), ({"skew": 1}, 1024, 100000),
+                                             ({"region_log2": 11}, 4096, 300000), ({}, 0, 0)])
+def test_triage_c1_vs_oracle(gpu, over, known, nm0):
+    """Config 1: 64 programs x 32 calls x 2k PCs, through K1+K2+K3."""
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default(**over)
+    nprog, cpp = 64, 32
+    cl = synth.call_lengths(nprog, cpp, 2048)
+    m0 = synth.m0(cfg, known, nm0)
+    st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl))
+    assert st["candidates"] > 0 and st["runs"] == 1
+
+
+def test_triage_overflow_retry(gpu):
+    """maxSignal starts as make(Signal) with 16 slots: phase 1 overflows and the
+    run restarts on bigger tables; results must not change."""
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default()
+    cl = synth.call_lengths(32, 16, 0, ragged=(0, 3000), seed=3)
+    m0 = (np.empty(0, np.uint32), np.empty(0, np.int8))
+    st = compare(gpu, m0, host_batch(cfg, 32, 16, cl), dev_batch(gpu, cfg, 32, 16, cl), ms_hint=0)
+    assert st["retries"] > 0
+
+
+def test_triage_many_prios_and_existing_new_signal(gpu):
+    """Arbitrary uint8 prios (int8 order, > 4 distinct -> several runs) and a
+    non-empty newSignal before the batch."""
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default(region_log2=10)
+    nprog, cpp = 16, 16
+    cl = synth.call_lengths(nprog, cpp, 0, ragged=(0, 2500), seed=8)
+    hs, hcs, hcnt, _ = host_batch(cfg, nprog, cpp, cl)
+    ds, dcs, dcnt, _ = dev_batch(gpu, cfg, nprog, cpp, cl)
+    rng = np.random.default_rng(1)
+    prio = rng.choice(np.array([0, 1, 2, 3, 7, 127, 128, 200, 255], np.uint8), size=nprog * cpp)
+    m0 = synth.m0(cfg, 512, 50000)
+    new0 = synth.m0(cfg, 0, 1000)
+    st = compare(gpu, m0, (hs, hcs, hcnt, prio), (ds, dcs, dcnt, torch.from_numpy(prio).to(gpu.dev)), new0=new0)
+    assert st["runs"] > 1
+
+
+def test_triage_empty_and_degenerate(gpu):
+    from syzkaller_amd import signal as S
+
+    ms = S.Signal.make(0, gpu.eng)
+    ns = S.Signal(None, gpu.eng)
+    z = lambda n, dt: torch.zeros(n, dtype=dt, device=gpu.dev)  # noqa: E731
+    bits, cnew, st = gpu.triage(ms, ns, z(0, torch.int32), z(0, torch.int64), z(0, torch.int32), z(0, torch.uint8))
+    assert ns.is_nil() and ms.Len() == 0
+    # calls that are all empty
+    bits, cnew, st = gpu.triage(ms, ns, z(4, torch.int32), z(3, torch.int64), z(3, torch.int32), z(3, torch.uint8))
+    assert int(cnew.sum()) == 0 and ns.is_nil()
+
+
+def test_triage_rejects_out_of_range_calls(gpu):
+    from syzkaller_amd import signal as S
+    from syzkaller_amd._lib import SyzsigError
+
+    ms = S.Signal.make(0, gpu.eng)
+    ns = S.Signal(None, gpu.eng)
+    sigs = torch.arange(100, dtype=torch.int32, device=gpu.dev)
+    cs = torch.tensor([0, 90], dtype=torch.int64, device=gpu.dev)
+    cl = torch.tensor([10, 20], dtype=torch.int32, device=gpu.dev)
+    with pytest.raises(SyzsigError):
+        gpu.triage(ms, ns, sigs, cs, cl, torch.zeros(2, dtype=torch.uint8, device=gpu.dev))
+
+
+def test_triage_c2_properties(gpu):
+    """Config 2 size (4096 programs x 64 calls x 4k PCs vs a 10M maxSignal):
+    the whole batch in one launch equals the same batch as two sequential halves
+    (bit-exact bits, flags, maxSignal); replaying the batch finds nothing new;
+    every changed element is in newSignal."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default()
+    nprog, cpp = 4096, 64
+    cl = synth.call_lengths(nprog, cpp, 4096)
+    ds, dcs, dcnt, dprio = dev_batch(gpu, cfg, nprog, cpp, cl)
+    e0, p0 = gpu.synth_m0(cfg, 2048, 10_000_000)
+    ms = gpu.deserialize(e0, p0)
+    ms2 = ms.clone()
+    ns = S.Signal(None, gpu.eng)
+    bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
+    assert st["changed"] == ns.Len() and st["records"] == ds.numel()
+    h = nprog * cpp // 2
+    ns2 = S.Signal(None, gpu.eng)
+    b1, c1, _ = gpu.triage(ms2, ns2, ds, dcs[:h].contiguous(), dcnt[:h].contiguous(), dprio[:h].contiguous())
+    b2, c2, _ = gpu.triage(ms2, ns2, ds, dcs[h:].contiguous(), dcnt[h:].contiguous(), dprio[h:].contiguous())
+    assert torch.equal(cnew, torch.cat([c1, c2]))
+    assert torch.equal(bits, b1 | b2)
+    assert ms.Len() == ms2.Len() and ns.Len() == ns2.Len()
+    ser, ser2 = ms.Serialize(), ms2.Serialize()
+    o, o2 = np.argsort(ser.Elems), np.argsort(ser2.Elems)
+    np.testing.assert_array_equal(ser.Elems[o], ser2.Elems[o2])
+    np.testing.assert_array_equal(ser.Prios[o], ser2.Prios[o2])
+    # replay: nothing is new any more, maxSignal unchanged
+    ns3 = S.Signal(None, gpu.eng)
+    n_before = ms.Len()
+    bits3, cnew3, st3 = gpu.triage(ms, ns3, ds, dcs, dcnt, dprio)
+    assert int(cnew3.sum()) == 0 and int(bits3.count_nonzero()) == 0 and ns3.is_nil() and ms.Len() == n_before
