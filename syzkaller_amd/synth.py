@@ -34,11 +34,12 @@ def traces(cfg, prog_base, nprog, calls_per_prog, call_len):
     call_start = np.zeros(call_len.size, dtype=np.uint64)
     if call_len.size > 1:
         np.cumsum(call_len[:-1], out=call_start[1:])
-    pcs = np.empty(int(call_len.sum()), dtype=np.uint64)
+    total = int(call_len.sum())
+    pcs = np.empty(max(total, 1), dtype=np.uint64)  # never NULL: empty calls are legal
     prio = np.empty(call_len.size, dtype=np.uint8)
     check(_lib.lib().syzsig_synth_traces_host(ctypes.byref(cfg), prog_base, nprog, calls_per_prog, _p(call_start),
                                               _p(call_len), _p(pcs), _p(prio)))
-    return pcs, call_start, prio
+    return pcs[:total], call_start, prio
 
 
 def m0(cfg, known_sys, n):

@@ -1,0 +1,139 @@
+"""CPU, world_size 2 over gloo: the sharded step of syzkaller_amd/dist.py
+(levels all-reduce, counts + records all-to-all, owner triage, flags back)
+equals sequential checkNewSignal over the whole batch.  The device half is
+replaced by a numpy restatement (records-mode triage in serial order), so the
+exchange logic itself is what is tested here; the device kernels are checked
+against unsharded triage in tests/test_gpu_minimize_shard.py."""
+import json
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.test_gpu_minimize_shard import _owner
+
+SER = 0xFFFFFF
+
+
+class NumpyShardOps:
+    def partition(self, batch, serial_base, levels, nshards):
+        sigs, cs, cl, prio = batch["sigs"], batch["call_start"], batch["call_len"], batch["call_prio"]
+        lvl = {(v & 0xFF): i for i, v in enumerate(levels)}
+        recs, owners, pos_of = [], [], []
+        for c in range(cl.size):
+            for j in range(int(cl[c])):
+                e = int(sigs[int(cs[c]) + j])
+                recs.append((e << 32) | (lvl[int(prio[c])] << 24) | ((serial_base + c) & SER))
+                owners.append(_owner(e, nshards))
+                pos_of.append(int(cs[c]) + j)
+        order = sorted(range(len(recs)), key=lambda i: owners[i])
+        send = np.array([recs[i] for i in order], dtype=np.uint64).view(np.int64)
+        send_pos = np.zeros(sigs.size, np.int64)
+        for k, i in enumerate(order):
+            send_pos[pos_of[i]] = k
+        counts = [owners.count(g) for g in range(nshards)]
+        return torch.from_numpy(send.copy()), send_pos, counts
+
+    def triage_records(self, shard, new_signal, recs, levels):
+        r = recs.numpy().view(np.uint64)
+        flags = np.zeros(r.size, np.uint8)
+        by_k = {}
+        for i, x in enumerate(r):
+            by_k.setdefault(int(x) & SER, []).append(i)
+        for k in sorted(by_k):
+            upd = {}
+            for i in by_k[k]:
+                e, p = int(r[i]) >> 32, levels[(int(r[i]) >> 24) & 0xFF]
+                if e not in shard or p > shard[e]:
+                    flags[i] = 1
+                    upd[e] = max(p, upd.get(e, -999))
+            for e, p in upd.items():
+                shard[e] = p
+                new_signal[e] = max(p, new_signal.get(e, -999))
+        return torch.from_numpy(flags), {"records": int(r.size)}
+
+    def unpartition(self, batch, send_pos, back):
+        b = back.numpy()
+        bits = np.array([b[send_pos[i]] for i in range(send_pos.size)], np.uint8)
+        cs, cl = batch["call_start"], batch["call_len"]
+        cnew = np.array([bits[int(cs[c]): int(cs[c]) + int(cl[c])].any() for c in range(cl.size)], np.uint8)
+        return bits, cnew
+
+
+def make_rank_batch(rank, ncalls, seed):
+    rng = np.random.default_rng(seed + rank)
+    cl = rng.integers(0, 40, size=ncalls).astype(np.uint32)
+    cs = np.zeros(ncalls, np.uint64)
+    cs[1:] = np.cumsum(cl[:-1])
+    sigs = rng.integers(0, 300, size=int(cl.sum())).astype(np.uint32)
+    prio = rng.choice(np.array([0, 1, 2, 3], np.uint8), size=ncalls)
+    return {"sigs": sigs, "call_start": cs, "call_len": cl, "call_prio": prio}
+
+
+def m0_global(seed):
+    rng = np.random.default_rng(seed)
+    e = rng.choice(300, size=150, replace=False)
+    return {int(x): int(rng.integers(0, 4)) for x in e}
+
+
+def worker(rank, world, port, outdir, ncalls, seed):
+    from syzkaller_amd.dist import ShardedTriage
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    batch = make_rank_batch(rank, ncalls, seed)
+    shard = {e: p for e, p in m0_global(seed).items() if _owner(e, world) == rank}
+    news = {}
+    st = ShardedTriage(NumpyShardOps(), shard, news)
+    bits, cnew, stats = st.step(batch, torch.from_numpy(batch["call_prio"]), rank * ncalls)
+    json.dump({"bits": bits.tolist(), "cnew": cnew.tolist(), "shard": shard, "new": news, "stats": stats},
+              open(os.path.join(outdir, f"r{rank}.json"), "w"))
+    dist.destroy_process_group()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_sharded_step_equals_sequential_checknewsignal(seed):
+    from oracle import oracle as O
+
+    world, ncalls = 2, 60
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(worker, args=(world, free_port(), d, ncalls, seed), nprocs=world, start_method="spawn")
+        res = [json.load(open(os.path.join(d, f"r{r}.json"))) for r in range(world)]
+    # sequential reference over the concatenated batch (rank-major serial order)
+    parts = [make_rank_batch(r, ncalls, seed) for r in range(world)]
+    sigs = np.concatenate([p["sigs"] for p in parts])
+    off, cs = 0, []
+    for p in parts:
+        cs.append(p["call_start"] + off)
+        off += p["sigs"].size
+    cs = np.concatenate(cs)
+    cl = np.concatenate([p["call_len"] for p in parts])
+    prio = np.concatenate([p["call_prio"] for p in parts])
+    m0 = m0_global(seed)
+    ms, ns, obits, ocnew = O.triage_batch(np.array(list(m0), np.uint32), np.array(list(m0.values()), np.int8),
+                                          sigs, cs, cl, prio)
+    got_bits = np.concatenate([np.array(r["bits"], np.uint8) for r in res])
+    exp_bits = np.array([(obits[i >> 5] >> (i & 31)) & 1 for i in range(sigs.size)], np.uint8)
+    np.testing.assert_array_equal(got_bits, exp_bits)
+    np.testing.assert_array_equal(np.concatenate([r["cnew"] for r in res]), ocnew)
+    merged = {}
+    for r in res:
+        merged.update({int(k): v for k, v in r["shard"].items()})
+    assert merged == ms.to_dict()
+    nm = {}
+    for r in res:
+        nm.update({int(k): v for k, v in r["new"].items()})
+    assert nm == ns.to_dict()
+    assert sum(r["stats"]["sent"] for r in res) == sum(r["stats"]["received"] for r in res) == sigs.size
