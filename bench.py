@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--skew", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--table-hint", type=int, default=0,
+                    help="size maxSignal's table for this many entries (default: the library's policy)")
     return ap.parse_args()
 
 
@@ -131,6 +133,10 @@ def main():
     else:
         m0e, m0p = dev.synth_m0(cfg, 2048, a.m0)
     ms = dev.deserialize(m0e, m0p)
+    if a.table_hint:
+        sized = S.Signal.make(a.table_hint, dev.eng)
+        sized.Merge(ms)
+        ms = sized
     pristine = ms.clone()
     ns = S.Signal.make(4_000_000, dev.eng)
     b, bits, cnew = dev.batch(sigs, cs, cnt, prio)
@@ -192,6 +198,7 @@ def main():
                                    + (f" shard (hash-sharded over {world} GPUs, RCCL all-to-all)" if distributed else ""),
                        "programs_per_gpu": P, "calls": C, "pcs_per_call": L, "m0_per_gpu": a.m0,
                        "records_per_gpu": nrec, "pcs_per_gpu": npc, "skew": a.skew,
+                       "table_slots": ms.capacity(),
                        "parallelism": f"shard{world}" if distributed else "single"},
             "roofline": {"bound": "hbm", "kernel": "k_probe", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -143,6 +143,8 @@ typedef struct {
 	uint64_t new_signal_len; /* Len of *new_signal after the batch */
 	uint64_t retries;        /* capacity-overflow restarts */
 	uint64_t runs;           /* sub-batches (one per <=4 distinct prios) */
+	uint64_t parts;          /* table-region partitions used (0 = per-call mode) */
+	double part_ms;          /* device time of record partitioning (0 unless timing enabled) */
 	double probe_ms;         /* device time of the probe kernel(s) (0 unless timing enabled) */
 	double decide_ms;        /* device time of the decide kernel(s) (0 unless timing enabled) */
 } syzsig_batch_stats;

@@ -1,0 +1,20 @@
+#!/bin/bash
+# rocprofv3 kernel trace + stats of a short bench run, then separate PMC passes
+# (one counter group per run, as MI355X_MICROARCH.md prescribes).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${PROF_TAG:-prof}
+mkdir -p "$OUT"
+ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu}
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- python3 bench.py $ARGS > "$OUT/trace.log" 2>&1
+echo "[trace] exit $?" | tee -a "$OUT/status.log"
+for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" ${EXTRA_PMC:-}; do
+	tag=$(echo "$grp" | tr ' ' '_')
+	timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex "${PMC_KERNELS:-k_probe|k_decide|k_edge}" -f csv \
+		-d "$OUT/pmc_$tag" -o run -- python3 bench.py $ARGS > "$OUT/pmc_$tag.log" 2>&1
+	rc=$?
+	echo "[pmc $grp] exit $rc" | tee -a "$OUT/status.log"
+	[ $rc -ne 0 ] && exit $rc
+done
+exit 0

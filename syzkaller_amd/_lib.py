@@ -43,7 +43,7 @@ class Batch(ctypes.Structure):
 class BatchStats(ctypes.Structure):
     _fields_ = [("records", c_uint64), ("candidates", c_uint64), ("changed", c_uint64),
                 ("inserted", c_uint64), ("new_signal_len", c_uint64), ("retries", c_uint64),
-                ("runs", c_uint64), ("probe_ms", ctypes.c_double), ("decide_ms", ctypes.c_double)]
+                ("runs", c_uint64), ("parts", c_uint64), ("part_ms", ctypes.c_double), ("probe_ms", ctypes.c_double), ("decide_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {f[0]: (float if f[1] is ctypes.c_double else int)(getattr(self, f[0])) for f in self._fields_}

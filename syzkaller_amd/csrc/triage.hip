@@ -49,10 +49,15 @@ __device__ __forceinline__ uint32_t first_at(uint4 f, uint32_t l)
 }
 
 // ---------------------------------------------------------------- inputs
-// A batch is processed as segments, one wave each; candidates are compacted in
-// place inside the segment's own record range.
-//  - CallsIn: segment = one call (local batch); prio and serial uniform per call.
+// A run is processed as segments of records, one wave per segment; candidates
+// are compacted in place inside the segment's own record range.
+//  - CallsIn: segment = one call (prio and serial uniform per segment).
 //  - RecsIn:  segment = 4096 packed records (owner side of a sharded batch).
+//  - PartIn:  the run's records radix-partitioned by table region (2 MB
+//             slices of maxSignal); partition p is processed by the blocks of
+//             XCD p % 8 (blockIdx % 8, round-robin dispatch), partition after
+//             partition, so the slice being probed stays in that XCD's L2.
+//             Placement only affects speed: any block may process any segment.
 struct Seg {
 	uint64_t start;  // first record
 	uint32_t len;    // records
@@ -60,6 +65,8 @@ struct Seg {
 	uint32_t serial; // CallsIn: the call's serial index in the run
 	bool ok;
 };
+
+__device__ __forceinline__ void set_bit(uint32_t* bits, uint64_t r) { atomicOr(&bits[r >> 5], 1u << (r & 31)); }
 
 struct CallsIn {
 	const uint32_t* sigs;
@@ -70,31 +77,29 @@ struct CallsIn {
 	uint32_t* new_bits;
 	uint8_t* call_new;
 
-	__device__ uint64_t nseg() const { return c1 - c0; }
-	__device__ Seg seg(uint64_t s, const LevelMap& lm) const
+	template <typename F>
+	__device__ void for_each_segment(const LevelMap& lm, F f) const
 	{
-		Seg g;
-		const uint64_t c = c0 + s;
-		g.start = call_start[c];
-		g.len = call_len[c];
-		g.ok = g.start <= nrec && g.len <= nrec - g.start && g.len <= kSerialMask;
-		g.level = lm.lvl[call_prio[c]];
-		g.ok = g.ok && g.level < lm.n;
-		g.serial = (uint32_t)s;
-		return g;
+		const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+		for (uint64_t s = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); s < c1 - c0; s += nwaves) {
+			Seg g;
+			const uint64_t c = c0 + s;
+			g.start = call_start[c];
+			g.len = call_len[c];
+			g.ok = g.start <= nrec && g.len <= nrec - g.start && g.len <= kSerialMask;
+			g.level = lm.lvl[call_prio[c]];
+			g.ok = g.ok && g.level < lm.n;
+			g.serial = (uint32_t)s;
+			f(s, g);
+		}
 	}
-	// element, level, serial of record j of segment g
 	__device__ void rec(const Seg& g, uint32_t j, uint32_t& e, uint32_t& l, uint32_t& k) const
 	{
 		e = sigs[g.start + j];
 		l = g.level;
 		k = g.serial;
 	}
-	__device__ void mark_new(const Seg& g, uint32_t j) const
-	{
-		const uint64_t r = g.start + j;
-		atomicOr(&new_bits[r >> 5], 1u << (r & 31));
-	}
+	__device__ void mark_new(const Seg& g, uint32_t j, uint32_t) const { set_bit(new_bits, g.start + j); }
 	__device__ void seg_has_new(uint64_t s) const { call_new[c0 + s] = 1; }
 };
 
@@ -105,16 +110,20 @@ struct RecsIn {
 	uint64_t nrec;
 	uint8_t* new_flags;
 
-	__device__ uint64_t nseg() const { return (nrec + kSegRecs - 1) / kSegRecs; }
-	__device__ Seg seg(uint64_t s, const LevelMap&) const
+	template <typename F>
+	__device__ void for_each_segment(const LevelMap&, F f) const
 	{
-		Seg g;
-		g.start = s * kSegRecs;
-		g.len = (uint32_t)min<uint64_t>(kSegRecs, nrec - g.start);
-		g.ok = true;
-		g.level = 0;
-		g.serial = 0;
-		return g;
+		const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+		const uint64_t nseg = (nrec + kSegRecs - 1) / kSegRecs;
+		for (uint64_t s = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); s < nseg; s += nwaves) {
+			Seg g;
+			g.start = s * kSegRecs;
+			g.len = (uint32_t)min<uint64_t>(kSegRecs, nrec - g.start);
+			g.ok = true;
+			g.level = 0;
+			g.serial = 0;
+			f(s, g);
+		}
 	}
 	__device__ void rec(const Seg& g, uint32_t j, uint32_t& e, uint32_t& l, uint32_t& k) const
 	{
@@ -123,7 +132,53 @@ struct RecsIn {
 		l = (uint32_t)(r >> 24) & 0xff;
 		k = (uint32_t)r & kSerialMask;
 	}
-	__device__ void mark_new(const Seg& g, uint32_t j) const { new_flags[g.start + j] = 1; }
+	__device__ void mark_new(const Seg& g, uint32_t j, uint32_t) const { new_flags[g.start + j] = 1; }
+	__device__ void seg_has_new(uint64_t) const {}
+};
+
+constexpr uint32_t kPartSeg = 1024;  // records per segment in partitioned mode
+
+struct PartIn {
+	const uint64_t* recs;      // packed elem << 32 | level << 24 | serial, grouped by partition
+	const uint32_t* orig;      // record index in the caller's sigs[] (for the new bit)
+	const uint64_t* rec_base;  // nparts + 1
+	const uint64_t* seg_base;  // nparts + 1
+	uint32_t nparts;           // multiple of 8
+	uint64_t c0;
+	uint32_t* new_bits;
+	uint8_t* call_new;
+
+	template <typename F>
+	__device__ void for_each_segment(const LevelMap&, F f) const
+	{
+		const uint32_t x = blockIdx.x & 7, i = blockIdx.x >> 3, nbx = gridDim.x >> 3;
+		const uint32_t w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+		for (uint32_t p = x; p < nparts; p += 8) {
+			const uint64_t base = rec_base[p], n = rec_base[p + 1] - base;
+			const uint64_t nseg = (n + kPartSeg - 1) / kPartSeg, sb = seg_base[p];
+			for (uint64_t s = (uint64_t)i * wpb + w; s < nseg; s += (uint64_t)nbx * wpb) {
+				Seg g;
+				g.start = base + s * kPartSeg;
+				g.len = (uint32_t)min<uint64_t>(kPartSeg, n - s * kPartSeg);
+				g.ok = true;
+				g.level = 0;
+				g.serial = 0;
+				f(sb + s, g);
+			}
+		}
+	}
+	__device__ void rec(const Seg& g, uint32_t j, uint32_t& e, uint32_t& l, uint32_t& k) const
+	{
+		const uint64_t r = __builtin_nontemporal_load(&recs[g.start + j]);
+		e = (uint32_t)(r >> 32);
+		l = (uint32_t)(r >> 24) & 0xff;
+		k = (uint32_t)r & kSerialMask;
+	}
+	__device__ void mark_new(const Seg& g, uint32_t j, uint32_t k) const
+	{
+		set_bit(new_bits, orig[g.start + j]);
+		call_new[c0 + k] = 1;
+	}
 	__device__ void seg_has_new(uint64_t) const {}
 };
 
@@ -134,17 +189,14 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
                                                uint32_t* cand_meta, uint32_t* cand_cnt, unsigned long long* cnt)
 {
 	const uint32_t lane = lane_id();
-	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
 	const uint64_t max_probe = max_probe_for(bmask);
-	const uint64_t nseg = in.nseg();
 	uint64_t ncand = 0, ntouch = 0, ovf = 0, err = 0;
-	for (uint64_t s = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); s < nseg; s += nwaves) {
-		const Seg g = in.seg(s, lm);
+	in.for_each_segment(lm, [&](uint64_t s, const Seg& g) {
 		if (!g.ok) {
 			err += lane == 0;
 			if (lane == 0)
 				cand_cnt[s] = 0;
-			continue;
+			return;
 		}
 		uint32_t nc = 0;
 		for (uint32_t base = 0; base < g.len; base += 64) {
@@ -191,7 +243,7 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
 			cand_cnt[s] = nc;
 			ncand += nc;
 		}
-	}
+	});
 	block_count(&cnt[kCntCandidates], ncand);
 	block_count(&cnt[kCntTouched], ntouch);
 	block_count(&cnt[kCntOverflow], ovf);
@@ -207,15 +259,12 @@ __global__ __launch_bounds__(256) void k_decide(uint64_t* slots, const uint32_t*
                                                 const uint32_t* __restrict__ cand_cnt, unsigned long long* cnt)
 {
 	const uint32_t lane = lane_id();
-	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
 	const uint32_t cur_hi = (epoch << 24) | kSerialMask;
-	const uint64_t nseg = in.nseg();
 	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0;
-	for (uint64_t s = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); s < nseg; s += nwaves) {
+	in.for_each_segment(lm, [&](uint64_t s, const Seg& g) {
 		const uint32_t nc = cand_cnt[s];
 		if (nc == 0)
-			continue;
-		const Seg g = in.seg(s, lm);
+			return;
 		bool any_new = false;
 		for (uint32_t base = 0; base < nc; base += 64) {
 			const uint32_t i = base + lane;
@@ -228,7 +277,7 @@ __global__ __launch_bounds__(256) void k_decide(uint64_t* slots, const uint32_t*
 			in.rec(g, j, e, l2, k);
 			const uint4 f = reinterpret_cast<const uint4*>(firsts)[sidx];
 			if (min_from_level(f, l) == ((epoch << 24) | k)) {
-				in.mark_new(g, j);
+				in.mark_new(g, j, k);
 				any_new = true;
 			}
 			if (meta >> 31) {
@@ -250,27 +299,127 @@ __global__ __launch_bounds__(256) void k_decide(uint64_t* slots, const uint32_t*
 		}
 		if (__ballot(any_new) && lane == 0)
 			in.seg_has_new(s);
-	}
+	});
 	block_count(&cnt[kCntInserted], inserted);
 	block_count(&cnt[kCntChanged], changed);
 	block_count(&cnt[kCntAux], ns_ins);
 	block_count(&cnt[kCntOverflow], ovf);
 }
 
-// prio presence over calls -> 256-bit mask (block-local, one atomic per word per block)
-__global__ void k_prio_presence(const uint8_t* __restrict__ prio, uint64_t n, uint32_t* mask)
+// ---------------------------------------------------------------- partitioning
+// Records of calls [c0, c1) -> packed records grouped by table region
+// (partition = home bucket >> shift).  Blocks take 32 calls at a time.
+constexpr uint32_t kPartCallsPerBlock = 32;
+constexpr uint32_t kMaxParts = 1024;
+
+__global__ __launch_bounds__(256) void k_part_count(CallsIn in, uint64_t bmask, uint32_t shift, uint32_t nparts,
+                                                    unsigned long long* counts)
+{
+	__shared__ uint32_t h[kMaxParts];
+	for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
+		h[i] = 0;
+	__syncthreads();
+	const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = lane_id();
+	const uint64_t ncalls = in.c1 - in.c0, nchunks = (ncalls + kPartCallsPerBlock - 1) / kPartCallsPerBlock;
+	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+		const uint64_t ce = min<uint64_t>(ncalls, (ch + 1) * kPartCallsPerBlock);
+		for (uint64_t s = ch * kPartCallsPerBlock + w; s < ce; s += nw) {
+			const uint64_t c = in.c0 + s, start = in.call_start[c];
+			const uint32_t len = in.call_len[c];
+			if (start > in.nrec || len > in.nrec - start)
+				continue;  // reported by the probe's range check
+			for (uint32_t j = lane; j < len; j += 64)
+				atomicAdd(&h[(fmix32(in.sigs[start + j]) & bmask) >> shift], 1u);
+		}
+	}
+	__syncthreads();
+	for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
+		if (h[i])
+			atomicAdd(&counts[i], (unsigned long long)h[i]);
+}
+
+// counts -> rec_base / seg_base (exclusive scans) and scatter cursors
+__global__ void k_part_scan(const unsigned long long* counts, uint32_t nparts, uint64_t* rec_base, uint64_t* seg_base,
+                            unsigned long long* cursor)
+{
+	if (threadIdx.x != 0 || blockIdx.x != 0)
+		return;
+	uint64_t r = 0, sg = 0;
+	for (uint32_t p = 0; p < nparts; p++) {
+		rec_base[p] = r;
+		seg_base[p] = sg;
+		cursor[p] = r;
+		r += counts[p];
+		sg += (counts[p] + kPartSeg - 1) / kPartSeg;
+	}
+	rec_base[nparts] = r;
+	seg_base[nparts] = sg;
+}
+
+__global__ __launch_bounds__(256) void k_part_scatter(CallsIn in, LevelMap lm, uint64_t bmask, uint32_t shift,
+                                                      uint32_t nparts, unsigned long long* cursor, uint64_t* recs,
+                                                      uint32_t* orig)
+{
+	__shared__ uint32_t h[kMaxParts];
+	__shared__ unsigned long long base[kMaxParts];
+	const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = lane_id();
+	const uint64_t ncalls = in.c1 - in.c0, nchunks = (ncalls + kPartCallsPerBlock - 1) / kPartCallsPerBlock;
+	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+		for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
+			h[i] = 0;
+		__syncthreads();
+		const uint64_t ce = min<uint64_t>(ncalls, (ch + 1) * kPartCallsPerBlock);
+		for (uint64_t s = ch * kPartCallsPerBlock + w; s < ce; s += nw) {
+			const uint64_t c = in.c0 + s, start = in.call_start[c];
+			const uint32_t len = in.call_len[c];
+			if (start > in.nrec || len > in.nrec - start)
+				continue;
+			for (uint32_t j = lane; j < len; j += 64)
+				atomicAdd(&h[(fmix32(in.sigs[start + j]) & bmask) >> shift], 1u);
+		}
+		__syncthreads();
+		for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) {
+			base[i] = h[i] ? atomicAdd(&cursor[i], (unsigned long long)h[i]) : 0;
+			h[i] = 0;
+		}
+		__syncthreads();
+		for (uint64_t s = ch * kPartCallsPerBlock + w; s < ce; s += nw) {
+			const uint64_t c = in.c0 + s, start = in.call_start[c];
+			const uint32_t len = in.call_len[c];
+			if (start > in.nrec || len > in.nrec - start)
+				continue;
+			const uint64_t head = ((uint64_t)lm.lvl[in.call_prio[c]] << 24) | (s & kSerialMask);
+			for (uint32_t j = lane; j < len; j += 64) {
+				const uint32_t e = in.sigs[start + j];
+				const uint32_t p = (fmix32(e) & bmask) >> shift;
+				const uint64_t pos = base[p] + atomicAdd(&h[p], 1u);
+				recs[pos] = ((uint64_t)e << 32) | head;
+				orig[pos] = (uint32_t)(start + j);
+			}
+		}
+		__syncthreads();
+	}
+}
+
+// prio presence over calls -> 256-bit mask (block-local, one atomic per word
+// per block), plus the number of records (sum of call_len)
+__global__ void k_prio_presence(const uint8_t* __restrict__ prio, const uint32_t* __restrict__ len, uint64_t n,
+                                uint32_t* mask, unsigned long long* nrec)
 {
 	__shared__ uint32_t m[8];
 	if (threadIdx.x < 8)
 		m[threadIdx.x] = 0;
 	__syncthreads();
+	uint64_t tot = 0;
 	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
 		uint8_t p = prio[i];
 		atomicOr(&m[p >> 5], 1u << (p & 31));
+		tot += len[i];
 	}
 	__syncthreads();
 	if (threadIdx.x < 8 && m[threadIdx.x])
 		atomicOr(&mask[threadIdx.x], m[threadIdx.x]);
+	block_count(nrec, tot);
 }
 
 // ---------------------------------------------------------------- host
@@ -296,17 +445,18 @@ static void level_map_from(const bool present[256], LevelMap* lm)
 	lm->n = n;
 }
 
-static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* runs)
+static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* runs, uint64_t* total_recs)
 {
 	void* dmask;
 	SYZ_TRY(ws_get(ctx, 6, 64, &dmask));
-	SYZ_HIP(hipMemsetAsync(dmask, 0, 32, ctx->stream));
-	k_prio_presence<<<grid_for(b->ncalls, 256, 256), 256, 0, ctx->stream>>>(b->call_prio, b->ncalls,
-	                                                                        (uint32_t*)dmask);
+	SYZ_HIP(hipMemsetAsync(dmask, 0, 48, ctx->stream));
+	k_prio_presence<<<grid_for(b->ncalls, 256, 256), 256, 0, ctx->stream>>>(
+	    b->call_prio, b->call_len, b->ncalls, (uint32_t*)dmask, (unsigned long long*)((char*)dmask + 32));
 	SYZ_HIP(hipGetLastError());
-	uint32_t hmask[8];
-	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 32, hipMemcpyDeviceToHost, ctx->stream));
+	uint32_t hmask[10];
+	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 40, hipMemcpyDeviceToHost, ctx->stream));
 	SYZ_HIP(hipStreamSynchronize(ctx->stream));
+	memcpy(total_recs, &hmask[8], 8);
 	bool present[256];
 	int np = 0;
 	for (int i = 0; i < 256; i++) {
@@ -349,10 +499,11 @@ static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* r
 // One run (<= 4 prio levels): probe, then decide+commit.  On capacity
 // overflow the run's only table side effects -- absent markers -- are dropped
 // by a rehash into a bigger table and the run restarts.
-template <typename In>
-static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const In& in, uint64_t nseg,
-                      const LevelMap& lm, uint32_t* cand_slot, uint32_t* cand_meta, uint32_t* cand_cnt,
-                      syzsig_batch_stats* st)
+// `prep(&in, &grid)` builds the kernels' input for the table's current
+// geometry (it runs again after a restart on a bigger table).
+template <typename In, typename Prep>
+static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, Prep prep, const LevelMap& lm,
+                      uint32_t* cand_slot, uint32_t* cand_meta, uint32_t* cand_cnt, syzsig_batch_stats* st)
 {
 	for (;;) {
 		if (--ms->epoch == 0) {
@@ -360,8 +511,10 @@ static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const In
 			ms->epoch = 254;
 		}
 		SYZ_HIP(hipMemsetAsync(ms->touched, 0, (ms->nslots() / 32 + 1) * 4, ctx->stream));
+		In in;
+		int grid = 0;
+		SYZ_TRY(prep(&in, &grid, st));
 		SYZ_TRY(counters_reset(ctx));
-		const int grid = grid_for(nseg * 64, 256, 4096);
 		if (ctx->timing)
 			SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
 		k_probe<In><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in, lm,
@@ -417,27 +570,45 @@ static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const In
 	}
 }
 
+// Partitioned mode pays off once maxSignal no longer fits the L2s and the
+// run is large; it needs record indices < 2^32.
+static uint32_t parts_for(const syzsig_set* ms, uint64_t nrecs, uint64_t nrec_space)
+{
+	const uint64_t bytes = ms->nslots() * 8;
+	if (bytes < (32ull << 20) || nrecs < (1ull << 20) || nrec_space >= (1ull << 32))
+		return 0;
+	uint32_t parts = 8;
+	while (parts < kMaxParts && bytes / parts > (2ull << 20) && parts < ms->nbuckets)
+		parts <<= 1;
+	return parts;
+}
+
+static uint32_t log2u(uint64_t x)
+{
+	uint32_t r = 0;
+	while ((1ull << r) < x)
+		r++;
+	return r;
+}
+
 int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b,
                       syzsig_batch_stats* st)
 {
 	SYZ_HIP(hipMemsetAsync(b->new_bits, 0, ((b->nrec + 31) / 32) * 4, ctx->stream));
 	if (b->ncalls)
 		SYZ_HIP(hipMemsetAsync(b->call_new, 0, b->ncalls, ctx->stream));
-	st->records = b->nrec;
 	if (b->ncalls == 0 || b->nrec == 0) {
 		SYZ_HIP(hipStreamSynchronize(ctx->stream));
 		return SYZSIG_OK;
 	}
 	SYZ_TRY(set_ensure_triage_state(ms));
 	std::vector<Run> runs;
-	SYZ_TRY(plan_runs(ctx, b, &runs));
+	uint64_t total = 0;
+	SYZ_TRY(plan_runs(ctx, b, &runs, &total));
+	st->records = total;
 	uint64_t maxrun = 0;
 	for (auto& r : runs)
 		maxrun = std::max(maxrun, r.c1 - r.c0);
-	void *cs, *cm, *cc;
-	SYZ_TRY(ws_get(ctx, 3, b->nrec * 4, &cs));
-	SYZ_TRY(ws_get(ctx, 4, b->nrec * 4, &cm));
-	SYZ_TRY(ws_get(ctx, 5, maxrun * 4, &cc));
 	for (auto& r : runs) {
 		CallsIn in;
 		in.sigs = b->sigs;
@@ -449,7 +620,68 @@ int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const sy
 		in.nrec = b->nrec;
 		in.new_bits = b->new_bits;
 		in.call_new = b->call_new;
-		SYZ_TRY(triage_run(ctx, ms, ns, in, r.c1 - r.c0, r.lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
+		const uint64_t run_recs = runs.size() == 1 ? total : b->nrec;  // bound
+		if (parts_for(ms, run_recs, b->nrec)) {
+			// ---- partitioned: records regrouped by table region, one XCD per region
+			void *cs, *cm, *cc, *pr, *po, *pm;
+			const uint64_t nseg_max = run_recs / kPartSeg + kMaxParts + 1;
+			SYZ_TRY(ws_get(ctx, 3, run_recs * 4 + 64, &cs));
+			SYZ_TRY(ws_get(ctx, 4, run_recs * 4 + 64, &cm));
+			SYZ_TRY(ws_get(ctx, 5, nseg_max * 4, &cc));
+			SYZ_TRY(ws_get(ctx, 11, run_recs * 8 + 64, &pr));
+			SYZ_TRY(ws_get(ctx, 12, run_recs * 4 + 64, &po));
+			SYZ_TRY(ws_get(ctx, 13, (kMaxParts + 1) * 8 * 4, &pm));
+			unsigned long long* counts = (unsigned long long*)pm;
+			unsigned long long* cursor = counts + kMaxParts + 1;
+			uint64_t* rec_base = (uint64_t*)(cursor + kMaxParts + 1);
+			uint64_t* seg_base = rec_base + kMaxParts + 1;
+			auto prep = [&](PartIn* pin, int* grid, syzsig_batch_stats* stp) -> int {
+				const uint32_t parts = parts_for(ms, run_recs, b->nrec);
+				if (!parts)
+					return fail(SYZSIG_EIO, "partitioned triage lost its geometry (internal error)");
+				const uint32_t shift = log2u(ms->nbuckets) - log2u(parts);
+				if (ctx->timing)
+					SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
+				SYZ_HIP(hipMemsetAsync(counts, 0, parts * 8, ctx->stream));
+				const uint64_t nchunks = (r.c1 - r.c0 + kPartCallsPerBlock - 1) / kPartCallsPerBlock;
+				const int pg = (int)std::min<uint64_t>(nchunks, 2048);
+				k_part_count<<<pg, 256, 0, ctx->stream>>>(in, ms->nbuckets - 1, shift, parts, counts);
+				k_part_scan<<<1, 64, 0, ctx->stream>>>(counts, parts, rec_base, seg_base, cursor);
+				k_part_scatter<<<pg, 256, 0, ctx->stream>>>(in, r.lm, ms->nbuckets - 1, shift, parts, cursor,
+				                                            (uint64_t*)pr, (uint32_t*)po);
+				SYZ_HIP(hipGetLastError());
+				if (ctx->timing) {
+					float t = 0;
+					SYZ_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
+					SYZ_HIP(hipEventSynchronize(ctx->ev[1]));
+					SYZ_HIP(hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]));
+					stp->part_ms += t;
+				}
+				pin->recs = (const uint64_t*)pr;
+				pin->orig = (const uint32_t*)po;
+				pin->rec_base = rec_base;
+				pin->seg_base = seg_base;
+				pin->nparts = parts;
+				stp->parts = parts;
+				pin->c0 = r.c0;
+				pin->new_bits = b->new_bits;
+				pin->call_new = b->call_new;
+				*grid = 2048;  // multiple of 8: block b works on XCD b % 8's partitions
+				return SYZSIG_OK;
+			};
+			SYZ_TRY(triage_run<PartIn>(ctx, ms, ns, prep, r.lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
+		} else {
+			void *cs, *cm, *cc;
+			SYZ_TRY(ws_get(ctx, 3, b->nrec * 4, &cs));
+			SYZ_TRY(ws_get(ctx, 4, b->nrec * 4, &cm));
+			SYZ_TRY(ws_get(ctx, 5, maxrun * 4, &cc));
+			auto prep = [&](CallsIn* cin, int* grid, syzsig_batch_stats*) -> int {
+				*cin = in;
+				*grid = grid_for((r.c1 - r.c0) * 64, 256, 4096);
+				return SYZSIG_OK;
+			};
+			SYZ_TRY(triage_run<CallsIn>(ctx, ms, ns, prep, r.lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
+		}
 	}
 	if ((double)ms->len > kMaxLoad * (double)ms->nslots())
 		SYZ_TRY(set_rehash(ms, buckets_for(ms->len), false));
@@ -487,11 +719,14 @@ int triage_records_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const 
 	SYZ_TRY(ws_get(ctx, 3, nrec * 4, &cs));
 	SYZ_TRY(ws_get(ctx, 4, nrec * 4, &cm));
 	SYZ_TRY(ws_get(ctx, 5, nseg * 4, &cc));
-	RecsIn in;
-	in.recs = recs;
-	in.nrec = nrec;
-	in.new_flags = new_flags;
-	SYZ_TRY(triage_run(ctx, ms, ns, in, nseg, lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
+	auto prep = [&](RecsIn* in, int* grid, syzsig_batch_stats*) -> int {
+		in->recs = recs;
+		in->nrec = nrec;
+		in->new_flags = new_flags;
+		*grid = grid_for(nseg * 64, 256, 4096);
+		return SYZSIG_OK;
+	};
+	SYZ_TRY(triage_run<RecsIn>(ctx, ms, ns, prep, lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
 	if ((double)ms->len > kMaxLoad * (double)ms->nslots())
 		SYZ_TRY(set_rehash(ms, buckets_for(ms->len), false));
 	st->new_signal_len = syzsig_len(*ns);

@@ -66,7 +66,21 @@ def test_triage_c1_vs_oracle(gpu, over, known, nm0):
     cl = synth.call_lengths(nprog, cpp, 2048)
     m0 = synth.m0(cfg, known, nm0)
     st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl))
-    assert st["candidates"] > 0 and st["runs"] == 1
+    assert st["candidates"] > 0 and st["runs"] == 1 and st["parts"] == 0
+
+
+@pytest.mark.parametrize("skew", [0, 1])
+def test_triage_partitioned_vs_oracle(gpu, skew):
+    """A maxSignal big enough (5M elements, 134 MB table) and a batch big enough
+    (64 x 32 x 2k) to take the partitioned (table-region per XCD) path."""
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default(skew=skew)
+    nprog, cpp = 64, 32
+    cl = synth.call_lengths(nprog, cpp, 2048)
+    m0 = synth.m0(cfg, 2048, 5_000_000)
+    st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl))
+    assert st["parts"] >= 8, st
 
 
 def test_triage_overflow_retry(gpu):
@@ -142,7 +156,7 @@ def test_triage_c2_properties(gpu):
     ms2 = ms.clone()
     ns = S.Signal(None, gpu.eng)
     bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
-    assert st["changed"] == ns.Len() and st["records"] == ds.numel()
+    assert st["changed"] == ns.Len() and st["records"] == int(dcnt.to(torch.int64).sum()) and st["parts"] > 0
     h = nprog * cpp // 2
     ns2 = S.Signal(None, gpu.eng)
     b1, c1, _ = gpu.triage(ms2, ns2, ds, dcs[:h].contiguous(), dcnt[:h].contiguous(), dprio[:h].contiguous())
