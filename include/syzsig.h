@@ -137,6 +137,7 @@ typedef struct {
 
 typedef struct {
 	uint64_t records;        /* records processed */
+	uint64_t survivors;      /* records not settled by their home bucket (full probe) */
 	uint64_t candidates;     /* records that passed the maxSignal prio filter */
 	uint64_t changed;        /* elements whose maxSignal prio changed (incl. new) */
 	uint64_t inserted;       /* elements new to maxSignal */

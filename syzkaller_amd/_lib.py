@@ -41,7 +41,7 @@ class Batch(ctypes.Structure):
 
 
 class BatchStats(ctypes.Structure):
-    _fields_ = [("records", c_uint64), ("candidates", c_uint64), ("changed", c_uint64),
+    _fields_ = [("records", c_uint64), ("survivors", c_uint64), ("candidates", c_uint64), ("changed", c_uint64),
                 ("inserted", c_uint64), ("new_signal_len", c_uint64), ("retries", c_uint64),
                 ("runs", c_uint64), ("parts", c_uint64), ("part_ms", ctypes.c_double), ("probe_ms", ctypes.c_double), ("decide_ms", ctypes.c_double)]
 

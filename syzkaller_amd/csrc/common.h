@@ -26,7 +26,10 @@
 
 namespace syz {
 
-constexpr uint32_t kBucketSlots = 8;        // 8 x u64 = one 64-B bucket
+// 2 x u64 = one 16-B bucket: the common lookup is ONE dwordx4 request per lane
+// (scattered-request rate, not bytes, bounds an L2-resident probe).
+constexpr uint32_t kBucketShift = 1;
+constexpr uint32_t kBucketSlots = 1u << kBucketShift;
 constexpr uint64_t kSlotEmpty = 0;
 constexpr uint32_t kStatePresent = 0x100;
 constexpr uint32_t kStateHasPrio = 0x200;

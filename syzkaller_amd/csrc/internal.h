@@ -66,6 +66,12 @@ struct syzsig_ctx {
 	unsigned long long* h_cnt = nullptr;  // pinned mirror
 	syz::Workspace ws[16];                // grow-only scratch buffers (index = role, see kWs*)
 	bool timing = false;                  // HIP events around triage kernels
+	// tuning knobs (defaults; SYZSIG_* environment overrides read at ctx creation)
+	int part_grid = 1024;                 // blocks of the partitioned probe/decide (multiple of 8)
+	uint64_t part_slice = 2ull << 20;     // bytes of maxSignal per partition
+	int part_mode = 1;                    // 0 = never partition
+	int probe_u = 4;                      // records per lane in flight in the probe filter
+	int debug_skip_b = 0;                 // timing-only diagnostics: skip the probe's pass B
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -109,7 +115,7 @@ int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm);
 // the default load-factor policy: a table is grown when live/slots exceeds this
 constexpr double kMaxLoad = 0.75;
 constexpr double kTargetLoad = 0.5;
-constexpr uint32_t kMaxProbeBuckets = 1024;
+constexpr uint32_t kMaxProbeBuckets = 4096;
 
 inline int grid_for(uint64_t n, int block, int max_blocks = 2048)
 {
@@ -168,10 +174,13 @@ struct Bucket {
 __device__ __forceinline__ Bucket load_bucket(const uint64_t* p)
 {
 	const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p);
-	ulonglong2 a = q[0], b = q[1], c = q[2], d = q[3];
 	Bucket B;
-	B.s[0] = a.x; B.s[1] = a.y; B.s[2] = b.x; B.s[3] = b.y;
-	B.s[4] = c.x; B.s[5] = c.y; B.s[6] = d.x; B.s[7] = d.y;
+#pragma unroll
+	for (uint32_t i = 0; i < kBucketSlots / 2; i++) {
+		const ulonglong2 v = q[i];
+		B.s[2 * i] = v.x;
+		B.s[2 * i + 1] = v.y;
+	}
 	return B;
 }
 
@@ -185,14 +194,14 @@ __device__ __forceinline__ int64_t tbl_lookup(const uint64_t* __restrict__ slots
 {
 	uint64_t b = home_bucket(key, bmask);
 	for (uint64_t n = 0; n <= bmask; n++) {
-		Bucket B = load_bucket(slots + (b << 3));
+		Bucket B = load_bucket(slots + (b << kBucketShift));
 #pragma unroll
 		for (int i = 0; i < (int)kBucketSlots; i++) {
 			if (B.s[i] == kSlotEmpty)
 				return -1;
 			if (slot_key(B.s[i]) == key) {
 				val = B.s[i];
-				return (int64_t)((b << 3) + i);
+				return (int64_t)((b << kBucketShift) + i);
 			}
 		}
 		b = (b + 1) & bmask;
@@ -208,7 +217,7 @@ __device__ __forceinline__ int64_t tbl_find_or_insert(uint64_t* slots, uint64_t 
 {
 	uint64_t b = home_bucket(key, bmask);
 	for (uint64_t n = 0; n < max_probe; n++) {
-		uint64_t* bp = slots + (b << 3);
+		uint64_t* bp = slots + (b << kBucketShift);
 		Bucket B = load_bucket(bp);
 #pragma unroll
 		for (int i = 0; i < (int)kBucketSlots; i++) {
@@ -217,12 +226,12 @@ __device__ __forceinline__ int64_t tbl_find_or_insert(uint64_t* slots, uint64_t 
 				s = atomicCAS(reinterpret_cast<unsigned long long*>(bp + i), 0ull, (unsigned long long)ins);
 				if (s == kSlotEmpty) {
 					old = 0;
-					return (int64_t)((b << 3) + i);
+					return (int64_t)((b << kBucketShift) + i);
 				}
 			}
 			if (slot_key(s) == key) {
 				old = s;
-				return (int64_t)((b << 3) + i);
+				return (int64_t)((b << kBucketShift) + i);
 			}
 		}
 		b = (b + 1) & bmask;
@@ -233,7 +242,7 @@ __device__ __forceinline__ int64_t tbl_find_or_insert(uint64_t* slots, uint64_t 
 __device__ __forceinline__ uint64_t max_probe_for(uint64_t bmask)
 {
 	uint64_t nb = bmask + 1;
-	return nb < kMaxProbeBuckets ? nb : kMaxProbeBuckets;
+	return nb < kMaxProbeBuckets ? nb : kMaxProbeBuckets;  // (kMaxProbeBuckets * kBucketSlots slots)
 }
 
 // Insert-or-max (Merge rule).  Returns 1 if inserted, 0 otherwise; -1 overflow.

@@ -1,5 +1,7 @@
 // runtime.hip -- context, stream, scratch and error plumbing of libsyzsig.
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 #include "internal.h"
 
@@ -85,6 +87,16 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 		return syz::hip_fail(e, "ctx_create", __FILE__, __LINE__);
 	}
 	c->stream = c->own_stream;
+	if (const char* v = getenv("SYZSIG_PART_GRID"))
+		c->part_grid = std::max(8, atoi(v) / 8 * 8);
+	if (const char* v = getenv("SYZSIG_PART_SLICE_KB"))
+		c->part_slice = std::max<uint64_t>(64, strtoull(v, nullptr, 10)) << 10;
+	if (const char* v = getenv("SYZSIG_PART_MODE"))
+		c->part_mode = atoi(v);
+	if (const char* v = getenv("SYZSIG_PROBE_U"))
+		c->probe_u = atoi(v);
+	if (const char* v = getenv("SYZSIG_DEBUG_SKIP_B"))
+		c->debug_skip_b = atoi(v);
 	*out = c;
 	return SYZSIG_OK;
 }

@@ -183,14 +183,15 @@ struct PartIn {
 };
 
 // ---------------------------------------------------------------- phase 1
-template <typename In>
+template <typename In, uint32_t kProbeU>
 __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, uint32_t* firsts, uint32_t* touched,
                                                In in, LevelMap lm, uint32_t epoch, uint32_t* cand_slot,
-                                               uint32_t* cand_meta, uint32_t* cand_cnt, unsigned long long* cnt)
+                                               uint32_t* cand_meta, uint32_t* cand_cnt, unsigned long long* cnt,
+                                               int skip_b)
 {
 	const uint32_t lane = lane_id();
 	const uint64_t max_probe = max_probe_for(bmask);
-	uint64_t ncand = 0, ntouch = 0, ovf = 0, err = 0;
+	uint64_t ncand = 0, ntouch = 0, ovf = 0, err = 0, nsurv = 0;
 	in.for_each_segment(lm, [&](uint64_t s, const Seg& g) {
 		if (!g.ok) {
 			err += lane == 0;
@@ -198,35 +199,84 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
 				cand_cnt[s] = 0;
 			return;
 		}
+		// Pass A (filter): kProbeU records per lane in flight; a record whose
+		// element sits in its (16-B) home bucket with a live prio
+		// >= p_k is settled (not new, changes nothing).  The rest are compacted
+		// in place (their offsets, in cand_meta) for pass B.
+		uint32_t ns = 0;
+		for (uint32_t base = 0; base < g.len; base += 64 * kProbeU) {
+			uint32_t e[kProbeU], l[kProbeU], k[kProbeU];
+			ulonglong2 h0[kProbeU];
+#pragma unroll
+			for (uint32_t u = 0; u < kProbeU; u++) {
+				const uint32_t j = base + u * 64 + lane;
+				l[u] = 0xff;
+				if (j < g.len)
+					in.rec(g, j, e[u], l[u], k[u]);
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < kProbeU; u++) {
+				if (l[u] < lm.n) {
+					h0[u] = *reinterpret_cast<const ulonglong2*>(slots + (home_bucket(e[u], bmask) << kBucketShift));
+				}
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < kProbeU; u++) {
+				bool surv = false;
+				if (l[u] != 0xff) {
+					if (l[u] >= lm.n) {
+						err++;
+					} else {
+						const uint32_t want = (uint32_t)make_slot(0, lm.val[l[u]]);
+						const uint64_t hs[2] = {h0[u].x, h0[u].y};
+						bool settled = false, seen = false;
+#pragma unroll
+						for (int i = 0; i < 2; i++) {
+							if (!seen && (hs[i] == kSlotEmpty || slot_key(hs[i]) == e[u])) {
+								seen = true;
+								settled = hs[i] != kSlotEmpty && slot_live(hs[i]) && (uint32_t)hs[i] >= want;
+							}
+						}
+						surv = !settled;
+					}
+				}
+				const uint64_t m = __ballot(surv);
+				if (surv)
+					cand_meta[g.start + ns + lane_rank(m)] = base + u * 64 + lane;
+				ns += (uint32_t)__popcll(m);
+			}
+		}
+		nsurv += lane == 0 ? ns : 0;
+		if (skip_b)  // timing-only diagnostic build path (SYZSIG_DEBUG_SKIP_B): results are wrong
+			ns = 0;
+		// Pass B (survivors, dense): full find/insert, prio filter against M0,
+		// firsts filter and atomicMin; candidates compacted in place again
+		// (write position <= read position, so unread survivors are intact).
 		uint32_t nc = 0;
-		for (uint32_t base = 0; base < g.len; base += 64) {
-			const uint32_t j = base + lane;
+		for (uint32_t base = 0; base < ns; base += 64) {
+			const uint32_t i = base + lane;
 			bool cand = false, toucher = false;
-			uint32_t sidx = 0, l = 0;
-			if (j < g.len) {
+			uint32_t sidx = 0, l = 0, j = 0;
+			if (i < ns) {
+				j = cand_meta[g.start + i];
 				uint32_t e, k;
 				in.rec(g, j, e, l, k);
-				if (l >= lm.n) {
-					err++;
-				} else {
-					// live slot low word of (e, p_k): p_k > M0[e]  <=>  old low word < want
-					const uint32_t want = (uint32_t)make_slot(0, lm.val[l]);
-					const uint32_t tag = (epoch << 24) | k;
-					uint64_t old;
-					const int64_t idx = tbl_find_or_insert(slots, bmask, e, make_absent(e), old, max_probe);
-					if (idx < 0) {
-						ovf++;
-					} else if (!slot_live(old) || (uint32_t)old < want) {
-						sidx = (uint32_t)idx;
-						const uint4 f = reinterpret_cast<const uint4*>(firsts)[sidx];
-						if (min_from_level(f, l) >= tag) {
-							const uint32_t prev = atomicMin(&firsts[4 * (uint64_t)sidx + l], tag);
-							if (prev > ((epoch << 24) | kSerialMask)) {
-								const uint32_t bit = 1u << (sidx & 31);
-								toucher = !(atomicOr(&touched[sidx >> 5], bit) & bit);
-							}
-							cand = true;
+				const uint32_t want = (uint32_t)make_slot(0, lm.val[l]);
+				const uint32_t tag = (epoch << 24) | k;
+				uint64_t old;
+				const int64_t idx = tbl_find_or_insert(slots, bmask, e, make_absent(e), old, max_probe);
+				if (idx < 0) {
+					ovf++;
+				} else if (!slot_live(old) || (uint32_t)old < want) {
+					sidx = (uint32_t)idx;
+					const uint4 f = reinterpret_cast<const uint4*>(firsts)[sidx];
+					if (min_from_level(f, l) >= tag) {
+						const uint32_t prev = atomicMin(&firsts[4 * (uint64_t)sidx + l], tag);
+						if (prev > ((epoch << 24) | kSerialMask)) {
+							const uint32_t bit = 1u << (sidx & 31);
+							toucher = !(atomicOr(&touched[sidx >> 5], bit) & bit);
 						}
+						cand = true;
 					}
 				}
 			}
@@ -248,6 +298,7 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
 	block_count(&cnt[kCntTouched], ntouch);
 	block_count(&cnt[kCntOverflow], ovf);
 	block_count(&cnt[kCntError], err);
+	block_count(&cnt[kCntAux2], nsurv);
 }
 
 // ---------------------------------------------------------------- phase 2
@@ -308,39 +359,90 @@ __global__ __launch_bounds__(256) void k_decide(uint64_t* slots, const uint32_t*
 
 // ---------------------------------------------------------------- partitioning
 // Records of calls [c0, c1) -> packed records grouped by table region
-// (partition = home bucket >> shift).  Blocks take 32 calls at a time.
-constexpr uint32_t kPartCallsPerBlock = 32;
+// (partition = home bucket >> shift).  Block b owns the chunk of calls
+// [b*kPartCPB, (b+1)*kPartCPB); its slice of every partition is fixed by a
+// scan of the per-(chunk, partition) counts, so the scatter needs no global
+// atomics.  The scatter stages kTile records in LDS, sorts them by partition
+// (counting sort) and writes each partition's run contiguously.
+constexpr uint32_t kPartCPB = 128;
 constexpr uint32_t kMaxParts = 1024;
+constexpr uint32_t kTile = 2048;
 
-__global__ __launch_bounds__(256) void k_part_count(CallsIn in, uint64_t bmask, uint32_t shift, uint32_t nparts,
-                                                    unsigned long long* counts)
+__device__ __forceinline__ uint32_t part_of(uint32_t e, uint64_t bmask, uint32_t shift)
 {
-	__shared__ uint32_t h[kMaxParts];
-	for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
-		h[i] = 0;
-	__syncthreads();
-	const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = lane_id();
-	const uint64_t ncalls = in.c1 - in.c0, nchunks = (ncalls + kPartCallsPerBlock - 1) / kPartCallsPerBlock;
-	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-		const uint64_t ce = min<uint64_t>(ncalls, (ch + 1) * kPartCallsPerBlock);
-		for (uint64_t s = ch * kPartCallsPerBlock + w; s < ce; s += nw) {
-			const uint64_t c = in.c0 + s, start = in.call_start[c];
-			const uint32_t len = in.call_len[c];
-			if (start > in.nrec || len > in.nrec - start)
-				continue;  // reported by the probe's range check
-			for (uint32_t j = lane; j < len; j += 64)
-				atomicAdd(&h[(fmix32(in.sigs[start + j]) & bmask) >> shift], 1u);
-		}
-	}
-	__syncthreads();
-	for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
-		if (h[i])
-			atomicAdd(&counts[i], (unsigned long long)h[i]);
+	return (uint32_t)((fmix32(e) & bmask) >> shift);
 }
 
-// counts -> rec_base / seg_base (exclusive scans) and scatter cursors
-__global__ void k_part_scan(const unsigned long long* counts, uint32_t nparts, uint64_t* rec_base, uint64_t* seg_base,
-                            unsigned long long* cursor)
+__global__ __launch_bounds__(256) void k_part_count(CallsIn in, uint64_t bmask, uint32_t shift, uint32_t nparts,
+                                                    uint32_t* counts)
+{
+	__shared__ uint32_t h[kMaxParts];
+	const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = lane_id();
+	const uint64_t ncalls = in.c1 - in.c0, nchunks = (ncalls + kPartCPB - 1) / kPartCPB;
+	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+		for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
+			h[i] = 0;
+		__syncthreads();
+		const uint64_t ce = min<uint64_t>(ncalls, (ch + 1) * kPartCPB);
+		for (uint64_t s = ch * kPartCPB + w; s < ce; s += nw) {
+			const uint64_t c = in.c0 + s, start = in.call_start[c];
+			const uint32_t len = in.call_len[c];
+			for (uint32_t j = lane; j < len; j += 64)
+				atomicAdd(&h[part_of(in.sigs[start + j], bmask, shift)], 1u);
+		}
+		__syncthreads();
+		for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
+			counts[ch * nparts + i] = h[i];
+		__syncthreads();
+	}
+}
+
+// exclusive scan of v over the block (256 threads); returns the block total
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* out)
+{
+	__shared__ uint32_t wsum[4];
+	const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+	uint32_t x = v;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x, o, 64);
+		if (lane >= (uint32_t)o)
+			x += y;
+	}
+	if (lane == 63)
+		wsum[w] = x;
+	__syncthreads();
+	uint32_t pre = 0, tot = 0;
+	for (uint32_t i = 0; i < 4; i++) {
+		pre += i < w ? wsum[i] : 0;
+		tot += wsum[i];
+	}
+	__syncthreads();
+	*out = pre + x - v;
+	return tot;
+}
+
+// block p: exclusive scan over chunks of counts[.][p] -> offs[.][p]; totals[p]
+__global__ __launch_bounds__(256) void k_part_scan_chunks(const uint32_t* counts, uint64_t nchunks, uint32_t nparts,
+                                                          uint32_t* offs, uint64_t* totals)
+{
+	const uint32_t p = blockIdx.x;
+	uint64_t run = 0;
+	for (uint64_t b0 = 0; b0 < nchunks; b0 += blockDim.x) {
+		const uint64_t b = b0 + threadIdx.x;
+		const uint32_t v = b < nchunks ? counts[b * nparts + p] : 0;
+		uint32_t ex;
+		const uint32_t tot = block_excl_scan(v, &ex);
+		if (b < nchunks)
+			offs[b * nparts + p] = (uint32_t)(run + ex);
+		run += tot;
+	}
+	if (threadIdx.x == 0)
+		totals[p] = run;
+}
+
+// totals -> rec_base / seg_base
+__global__ void k_part_scan(const uint64_t* totals, uint32_t nparts, uint64_t* rec_base, uint64_t* seg_base)
 {
 	if (threadIdx.x != 0 || blockIdx.x != 0)
 		return;
@@ -348,78 +450,138 @@ __global__ void k_part_scan(const unsigned long long* counts, uint32_t nparts, u
 	for (uint32_t p = 0; p < nparts; p++) {
 		rec_base[p] = r;
 		seg_base[p] = sg;
-		cursor[p] = r;
-		r += counts[p];
-		sg += (counts[p] + kPartSeg - 1) / kPartSeg;
+		r += totals[p];
+		sg += (totals[p] + kPartSeg - 1) / kPartSeg;
 	}
 	rec_base[nparts] = r;
 	seg_base[nparts] = sg;
 }
 
 __global__ __launch_bounds__(256) void k_part_scatter(CallsIn in, LevelMap lm, uint64_t bmask, uint32_t shift,
-                                                      uint32_t nparts, unsigned long long* cursor, uint64_t* recs,
+                                                      uint32_t nparts, const uint32_t* __restrict__ offs,
+                                                      const uint64_t* __restrict__ rec_base, uint64_t* recs,
                                                       uint32_t* orig)
 {
-	__shared__ uint32_t h[kMaxParts];
-	__shared__ unsigned long long base[kMaxParts];
-	const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = lane_id();
-	const uint64_t ncalls = in.c1 - in.c0, nchunks = (ncalls + kPartCallsPerBlock - 1) / kPartCallsPerBlock;
+	__shared__ uint64_t t_rec[kTile], s_rec[kTile];
+	__shared__ uint32_t t_orig[kTile], s_orig[kTile];
+	__shared__ uint16_t t_part[kTile], s_part[kTile];
+	__shared__ uint32_t cur[kMaxParts], hist[kMaxParts], bin[kMaxParts], pos[kMaxParts];
+	__shared__ uint32_t tile_n, more;
+	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+	const uint64_t ncalls = in.c1 - in.c0, nchunks = (ncalls + kPartCPB - 1) / kPartCPB;
+	const uint32_t per_t = (nparts + blockDim.x - 1) / blockDim.x;  // bins per thread in the scan
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+		const uint64_t cb = ch * kPartCPB, ce = min<uint64_t>(ncalls, cb + kPartCPB);
 		for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
-			h[i] = 0;
-		__syncthreads();
-		const uint64_t ce = min<uint64_t>(ncalls, (ch + 1) * kPartCallsPerBlock);
-		for (uint64_t s = ch * kPartCallsPerBlock + w; s < ce; s += nw) {
-			const uint64_t c = in.c0 + s, start = in.call_start[c];
-			const uint32_t len = in.call_len[c];
-			if (start > in.nrec || len > in.nrec - start)
-				continue;
-			for (uint32_t j = lane; j < len; j += 64)
-				atomicAdd(&h[(fmix32(in.sigs[start + j]) & bmask) >> shift], 1u);
-		}
-		__syncthreads();
-		for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x) {
-			base[i] = h[i] ? atomicAdd(&cursor[i], (unsigned long long)h[i]) : 0;
-			h[i] = 0;
-		}
-		__syncthreads();
-		for (uint64_t s = ch * kPartCallsPerBlock + w; s < ce; s += nw) {
-			const uint64_t c = in.c0 + s, start = in.call_start[c];
-			const uint32_t len = in.call_len[c];
-			if (start > in.nrec || len > in.nrec - start)
-				continue;
-			const uint64_t head = ((uint64_t)lm.lvl[in.call_prio[c]] << 24) | (s & kSerialMask);
-			for (uint32_t j = lane; j < len; j += 64) {
-				const uint32_t e = in.sigs[start + j];
-				const uint32_t p = (fmix32(e) & bmask) >> shift;
-				const uint64_t pos = base[p] + atomicAdd(&h[p], 1u);
-				recs[pos] = ((uint64_t)e << 32) | head;
-				orig[pos] = (uint32_t)(start + j);
+			cur[i] = offs[ch * nparts + i];
+		// per-wave cursor: call cb + w, +4, ...; offset inside the call
+		uint64_t wc = cb + w;
+		uint32_t wo = 0;
+		for (;;) {
+			for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
+				hist[i] = 0;
+			if (threadIdx.x == 0) {
+				tile_n = 0;
+				more = 0;
 			}
+			__syncthreads();
+			// fill: each wave contributes up to kTile/4 records
+			uint32_t quota = kTile / 4;
+			while (quota && wc < ce) {
+				const uint64_t c = in.c0 + wc, start = in.call_start[c];
+				const uint32_t len = in.call_len[c];
+				const uint32_t m = min(quota, len - wo);
+				uint32_t tb = 0;
+				if (lane == 0 && m)
+					tb = atomicAdd(&tile_n, m);
+				tb = __shfl(tb, 0, 64);
+				const uint64_t head = ((uint64_t)lm.lvl[in.call_prio[c]] << 24) | (wc & kSerialMask);
+				for (uint32_t i = lane; i < m; i += 64) {
+					const uint32_t e = in.sigs[start + wo + i];
+					const uint32_t p = part_of(e, bmask, shift);
+					t_rec[tb + i] = ((uint64_t)e << 32) | head;
+					t_orig[tb + i] = (uint32_t)(start + wo + i);
+					t_part[tb + i] = (uint16_t)p;
+					atomicAdd(&hist[p], 1u);
+				}
+				quota -= m;
+				wo += m;
+				if (wo == len) {
+					wc += 4;
+					wo = 0;
+				}
+			}
+			if (lane == 0 && wc < ce)
+				atomicOr(&more, 1u);
+			__syncthreads();
+			const uint32_t n = tile_n;
+			// exclusive scan of hist -> bin (per_t consecutive bins per thread)
+			uint32_t loc = 0;
+			for (uint32_t q = 0; q < per_t; q++) {
+				const uint32_t i = threadIdx.x * per_t + q;
+				loc += i < nparts ? hist[i] : 0;
+			}
+			uint32_t ex;
+			block_excl_scan(loc, &ex);
+			for (uint32_t q = 0; q < per_t; q++) {
+				const uint32_t i = threadIdx.x * per_t + q;
+				if (i < nparts) {
+					bin[i] = ex;
+					pos[i] = ex;
+					ex += hist[i];
+				}
+			}
+			__syncthreads();
+			for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+				const uint32_t p = t_part[i];
+				const uint32_t d = atomicAdd(&pos[p], 1u);
+				s_rec[d] = t_rec[i];
+				s_orig[d] = t_orig[i];
+				s_part[d] = (uint16_t)p;
+			}
+			__syncthreads();
+			// consecutive threads write consecutive records of one partition run
+			for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+				const uint32_t p = s_part[i];
+				const uint64_t g = rec_base[p] + cur[p] + (i - bin[p]);
+				recs[g] = s_rec[i];
+				orig[g] = s_orig[i];
+			}
+			__syncthreads();
+			for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
+				cur[i] += hist[i];
+			const bool again = more != 0;
+			__syncthreads();
+			if (!again)
+				break;
 		}
-		__syncthreads();
 	}
 }
 
 // prio presence over calls -> 256-bit mask (block-local, one atomic per word
 // per block), plus the number of records (sum of call_len)
-__global__ void k_prio_presence(const uint8_t* __restrict__ prio, const uint32_t* __restrict__ len, uint64_t n,
-                                uint32_t* mask, unsigned long long* nrec)
+__global__ void k_prio_presence(const uint8_t* __restrict__ prio, const uint32_t* __restrict__ len,
+                                const uint64_t* __restrict__ start, uint64_t n, uint64_t nrec_space, uint32_t* mask,
+                                unsigned long long* nrec, unsigned long long* bad)
 {
 	__shared__ uint32_t m[8];
 	if (threadIdx.x < 8)
 		m[threadIdx.x] = 0;
 	__syncthreads();
-	uint64_t tot = 0;
+	uint64_t tot = 0, nbad = 0;
 	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
 		uint8_t p = prio[i];
 		atomicOr(&m[p >> 5], 1u << (p & 31));
-		tot += len[i];
+		const uint64_t st = start[i];
+		const uint32_t ln = len[i];
+		tot += ln;
+		nbad += st > nrec_space || ln > nrec_space - st || ln > kSerialMask;
 	}
 	__syncthreads();
 	if (threadIdx.x < 8 && m[threadIdx.x])
 		atomicOr(&mask[threadIdx.x], m[threadIdx.x]);
 	block_count(nrec, tot);
+	block_count(bad, nbad);
 }
 
 // ---------------------------------------------------------------- host
@@ -451,12 +613,17 @@ static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* r
 	SYZ_TRY(ws_get(ctx, 6, 64, &dmask));
 	SYZ_HIP(hipMemsetAsync(dmask, 0, 48, ctx->stream));
 	k_prio_presence<<<grid_for(b->ncalls, 256, 256), 256, 0, ctx->stream>>>(
-	    b->call_prio, b->call_len, b->ncalls, (uint32_t*)dmask, (unsigned long long*)((char*)dmask + 32));
+	    b->call_prio, b->call_len, b->call_start, b->ncalls, b->nrec, (uint32_t*)dmask,
+	    (unsigned long long*)((char*)dmask + 32), (unsigned long long*)((char*)dmask + 40));
 	SYZ_HIP(hipGetLastError());
-	uint32_t hmask[10];
-	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 40, hipMemcpyDeviceToHost, ctx->stream));
+	uint32_t hmask[12];
+	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 48, hipMemcpyDeviceToHost, ctx->stream));
 	SYZ_HIP(hipStreamSynchronize(ctx->stream));
 	memcpy(total_recs, &hmask[8], 8);
+	uint64_t nbad;
+	memcpy(&nbad, &hmask[10], 8);
+	if (nbad)
+		return fail(SYZSIG_EINVAL, "triage_batch: a call range lies outside [0, nrec) or has >= 2^24 records");
 	bool present[256];
 	int np = 0;
 	for (int i = 0; i < 256; i++) {
@@ -517,8 +684,15 @@ static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, Prep pre
 		SYZ_TRY(counters_reset(ctx));
 		if (ctx->timing)
 			SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
-		k_probe<In><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in, lm,
-		                                           ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt);
+		if (ctx->probe_u == 2)
+			k_probe<In, 2><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in,
+			                                              lm, ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt, ctx->debug_skip_b);
+		else if (ctx->probe_u == 1)
+			k_probe<In, 1><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in,
+			                                              lm, ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt, ctx->debug_skip_b);
+		else
+			k_probe<In, 4><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in,
+			                                              lm, ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt, ctx->debug_skip_b);
 		SYZ_HIP(hipGetLastError());
 		if (ctx->timing)
 			SYZ_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -538,6 +712,7 @@ static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, Prep pre
 		}
 		const uint64_t touched = ctx->h_cnt[kCntTouched];
 		st->candidates += ctx->h_cnt[kCntCandidates];
+		st->survivors += ctx->h_cnt[kCntAux2];
 		if (touched && !*ns)
 			SYZ_TRY(syzsig_set_make(ctx, touched, ns));  // newSignal.Merge allocates (signal.go:121-125)
 		if (touched)
@@ -574,11 +749,12 @@ static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, Prep pre
 // run is large; it needs record indices < 2^32.
 static uint32_t parts_for(const syzsig_set* ms, uint64_t nrecs, uint64_t nrec_space)
 {
+	const syzsig_ctx* ctx = ms->ctx;
 	const uint64_t bytes = ms->nslots() * 8;
-	if (bytes < (32ull << 20) || nrecs < (1ull << 20) || nrec_space >= (1ull << 32))
+	if (!ctx->part_mode || bytes < (32ull << 20) || nrecs < (1ull << 20) || nrec_space >= (1ull << 32))
 		return 0;
 	uint32_t parts = 8;
-	while (parts < kMaxParts && bytes / parts > (2ull << 20) && parts < ms->nbuckets)
+	while (parts < kMaxParts && bytes / parts > ctx->part_slice && parts < ms->nbuckets)
 		parts <<= 1;
 	return parts;
 }
@@ -623,31 +799,33 @@ int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const sy
 		const uint64_t run_recs = runs.size() == 1 ? total : b->nrec;  // bound
 		if (parts_for(ms, run_recs, b->nrec)) {
 			// ---- partitioned: records regrouped by table region, one XCD per region
-			void *cs, *cm, *cc, *pr, *po, *pm;
+			void *cs, *cm, *cc, *pr, *po, *pm, *pc;
 			const uint64_t nseg_max = run_recs / kPartSeg + kMaxParts + 1;
+			const uint64_t nchunks = (r.c1 - r.c0 + kPartCPB - 1) / kPartCPB;
 			SYZ_TRY(ws_get(ctx, 3, run_recs * 4 + 64, &cs));
 			SYZ_TRY(ws_get(ctx, 4, run_recs * 4 + 64, &cm));
 			SYZ_TRY(ws_get(ctx, 5, nseg_max * 4, &cc));
 			SYZ_TRY(ws_get(ctx, 11, run_recs * 8 + 64, &pr));
 			SYZ_TRY(ws_get(ctx, 12, run_recs * 4 + 64, &po));
-			SYZ_TRY(ws_get(ctx, 13, (kMaxParts + 1) * 8 * 4, &pm));
-			unsigned long long* counts = (unsigned long long*)pm;
-			unsigned long long* cursor = counts + kMaxParts + 1;
-			uint64_t* rec_base = (uint64_t*)(cursor + kMaxParts + 1);
+			SYZ_TRY(ws_get(ctx, 13, (kMaxParts + 1) * 8 * 3, &pm));
+			SYZ_TRY(ws_get(ctx, 14, nchunks * kMaxParts * 4 * 2 + 64, &pc));
+			uint64_t* totals = (uint64_t*)pm;
+			uint64_t* rec_base = totals + kMaxParts + 1;
 			uint64_t* seg_base = rec_base + kMaxParts + 1;
 			auto prep = [&](PartIn* pin, int* grid, syzsig_batch_stats* stp) -> int {
 				const uint32_t parts = parts_for(ms, run_recs, b->nrec);
 				if (!parts)
 					return fail(SYZSIG_EIO, "partitioned triage lost its geometry (internal error)");
 				const uint32_t shift = log2u(ms->nbuckets) - log2u(parts);
+				uint32_t* counts = (uint32_t*)pc;
+				uint32_t* offs = counts + nchunks * parts;
 				if (ctx->timing)
 					SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
-				SYZ_HIP(hipMemsetAsync(counts, 0, parts * 8, ctx->stream));
-				const uint64_t nchunks = (r.c1 - r.c0 + kPartCallsPerBlock - 1) / kPartCallsPerBlock;
-				const int pg = (int)std::min<uint64_t>(nchunks, 2048);
+				const int pg = (int)std::min<uint64_t>(nchunks, 4096);
 				k_part_count<<<pg, 256, 0, ctx->stream>>>(in, ms->nbuckets - 1, shift, parts, counts);
-				k_part_scan<<<1, 64, 0, ctx->stream>>>(counts, parts, rec_base, seg_base, cursor);
-				k_part_scatter<<<pg, 256, 0, ctx->stream>>>(in, r.lm, ms->nbuckets - 1, shift, parts, cursor,
+				k_part_scan_chunks<<<parts, 256, 0, ctx->stream>>>(counts, nchunks, parts, offs, totals);
+				k_part_scan<<<1, 64, 0, ctx->stream>>>(totals, parts, rec_base, seg_base);
+				k_part_scatter<<<pg, 256, 0, ctx->stream>>>(in, r.lm, ms->nbuckets - 1, shift, parts, offs, rec_base,
 				                                            (uint64_t*)pr, (uint32_t*)po);
 				SYZ_HIP(hipGetLastError());
 				if (ctx->timing) {
@@ -666,7 +844,7 @@ int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const sy
 				pin->c0 = r.c0;
 				pin->new_bits = b->new_bits;
 				pin->call_new = b->call_new;
-				*grid = 2048;  // multiple of 8: block b works on XCD b % 8's partitions
+				*grid = ctx->part_grid;  // multiple of 8: block b works on XCD b % 8's partitions
 				return SYZSIG_OK;
 			};
 			SYZ_TRY(triage_run<PartIn>(ctx, ms, ns, prep, r.lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
