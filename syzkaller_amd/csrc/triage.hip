@@ -189,6 +189,8 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
                                                uint32_t* cand_meta, uint32_t* cand_cnt, unsigned long long* cnt,
                                                int skip_b)
 {
+	__shared__ uint64_t q_rec[4][128];  // per-wave survivor queue (<= 64 + 63 entries)
+	__shared__ uint32_t q_j[4][128];
 	const uint32_t lane = lane_id();
 	const uint64_t max_probe = max_probe_for(bmask);
 	uint64_t ncand = 0, ntouch = 0, ovf = 0, err = 0, nsurv = 0;
@@ -199,68 +201,22 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
 				cand_cnt[s] = 0;
 			return;
 		}
-		// Pass A (filter): kProbeU records per lane in flight; a record whose
-		// element sits in its (16-B) home bucket with a live prio
-		// >= p_k is settled (not new, changes nothing).  The rest are compacted
-		// in place (their offsets, in cand_meta) for pass B.
-		uint32_t ns = 0;
-		for (uint32_t base = 0; base < g.len; base += 64 * kProbeU) {
-			uint32_t e[kProbeU], l[kProbeU], k[kProbeU];
-			ulonglong2 h0[kProbeU];
-#pragma unroll
-			for (uint32_t u = 0; u < kProbeU; u++) {
-				const uint32_t j = base + u * 64 + lane;
-				l[u] = 0xff;
-				if (j < g.len)
-					in.rec(g, j, e[u], l[u], k[u]);
-			}
-#pragma unroll
-			for (uint32_t u = 0; u < kProbeU; u++) {
-				if (l[u] < lm.n) {
-					h0[u] = *reinterpret_cast<const ulonglong2*>(slots + (home_bucket(e[u], bmask) << kBucketShift));
-				}
-			}
-#pragma unroll
-			for (uint32_t u = 0; u < kProbeU; u++) {
-				bool surv = false;
-				if (l[u] != 0xff) {
-					if (l[u] >= lm.n) {
-						err++;
-					} else {
-						const uint32_t want = (uint32_t)make_slot(0, lm.val[l[u]]);
-						const uint64_t hs[2] = {h0[u].x, h0[u].y};
-						bool settled = false, seen = false;
-#pragma unroll
-						for (int i = 0; i < 2; i++) {
-							if (!seen && (hs[i] == kSlotEmpty || slot_key(hs[i]) == e[u])) {
-								seen = true;
-								settled = hs[i] != kSlotEmpty && slot_live(hs[i]) && (uint32_t)hs[i] >= want;
-							}
-						}
-						surv = !settled;
-					}
-				}
-				const uint64_t m = __ballot(surv);
-				if (surv)
-					cand_meta[g.start + ns + lane_rank(m)] = base + u * 64 + lane;
-				ns += (uint32_t)__popcll(m);
-			}
-		}
-		nsurv += lane == 0 ? ns : 0;
-		if (skip_b)  // timing-only diagnostic build path (SYZSIG_DEBUG_SKIP_B): results are wrong
-			ns = 0;
-		// Pass B (survivors, dense): full find/insert, prio filter against M0,
-		// firsts filter and atomicMin; candidates compacted in place again
-		// (write position <= read position, so unread survivors are intact).
-		uint32_t nc = 0;
-		for (uint32_t base = 0; base < ns; base += 64) {
-			const uint32_t i = base + lane;
+		// Filter: kProbeU records per lane in flight; a record whose element
+		// sits in its (16-B) home bucket with a live prio >= p_k is settled (not
+		// new, changes nothing).  Survivors go to this wave's LDS queue, which
+		// is drained 64 at a time by the full path, so the slow path runs dense
+		// and survivors never leave the chip.
+		uint32_t nc = 0, qn = 0;
+		uint64_t* qr = q_rec[threadIdx.x >> 6];
+		uint32_t* qj = q_j[threadIdx.x >> 6];
+		auto drain64 = [&](uint32_t n) {  // full path for queue entries [0, n), n <= 64
 			bool cand = false, toucher = false;
 			uint32_t sidx = 0, l = 0, j = 0;
-			if (i < ns) {
-				j = cand_meta[g.start + i];
-				uint32_t e, k;
-				in.rec(g, j, e, l, k);
+			if (lane < n && !skip_b) {
+				const uint64_t r = qr[lane];
+				j = qj[lane];
+				const uint32_t e = (uint32_t)(r >> 32), k = (uint32_t)r & kSerialMask;
+				l = (uint32_t)(r >> 24) & 0xff;
 				const uint32_t want = (uint32_t)make_slot(0, lm.val[l]);
 				const uint32_t tag = (epoch << 24) | k;
 				uint64_t old;
@@ -288,6 +244,70 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
 			}
 			nc += (uint32_t)__popcll(m);
 			ntouch += toucher;
+		};
+		for (uint32_t base = 0; base < g.len; base += 64 * kProbeU) {
+			uint32_t e[kProbeU], l[kProbeU], k[kProbeU];
+			ulonglong2 h0[kProbeU];
+#pragma unroll
+			for (uint32_t u = 0; u < kProbeU; u++) {
+				const uint32_t j = base + u * 64 + lane;
+				l[u] = 0xff;
+				if (j < g.len)
+					in.rec(g, j, e[u], l[u], k[u]);
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < kProbeU; u++)
+				if (l[u] < lm.n)
+					h0[u] = *reinterpret_cast<const ulonglong2*>(slots + (home_bucket(e[u], bmask) << kBucketShift));
+#pragma unroll
+			for (uint32_t u = 0; u < kProbeU; u++) {
+				bool surv = false;
+				if (l[u] != 0xff) {
+					if (l[u] >= lm.n) {
+						err++;
+					} else {
+						const uint32_t want = (uint32_t)make_slot(0, lm.val[l[u]]);
+						const uint64_t a0 = h0[u].x, a1 = h0[u].y;
+						const bool settled = (a0 != kSlotEmpty && slot_key(a0) == e[u] && slot_live(a0) &&
+						                      (uint32_t)a0 >= want) ||
+						                     (a0 != kSlotEmpty && slot_key(a0) != e[u] && a1 != kSlotEmpty &&
+						                      slot_key(a1) == e[u] && slot_live(a1) && (uint32_t)a1 >= want);
+						surv = !settled;
+					}
+				}
+				const uint64_t m = __ballot(surv);
+				if (surv) {
+					const uint32_t qp = qn + lane_rank(m);
+					qr[qp] = ((uint64_t)e[u] << 32) | ((uint64_t)l[u] << 24) | k[u];
+					qj[qp] = base + u * 64 + lane;
+				}
+				qn += (uint32_t)__popcll(m);
+				nsurv += lane == 0 ? __popcll(m) : 0;
+				if (qn >= 64) {
+					__builtin_amdgcn_wave_barrier();
+					drain64(64);
+					qn -= 64;
+					if (qn) {  // move the tail (< 64 entries) to the queue head
+						uint64_t tr = 0;
+						uint32_t tj = 0;
+						if (lane < qn) {
+							tr = qr[64 + lane];
+							tj = qj[64 + lane];
+						}
+						__builtin_amdgcn_wave_barrier();
+						if (lane < qn) {
+							qr[lane] = tr;
+							qj[lane] = tj;
+						}
+					}
+					__builtin_amdgcn_wave_barrier();
+				}
+			}
+		}
+		if (qn) {
+			__builtin_amdgcn_wave_barrier();
+			drain64(qn);
+			__builtin_amdgcn_wave_barrier();
 		}
 		if (lane == 0) {
 			cand_cnt[s] = nc;
@@ -496,13 +516,23 @@ __global__ __launch_bounds__(256) void k_part_scatter(CallsIn in, LevelMap lm, u
 					tb = atomicAdd(&tile_n, m);
 				tb = __shfl(tb, 0, 64);
 				const uint64_t head = ((uint64_t)lm.lvl[in.call_prio[c]] << 24) | (wc & kSerialMask);
-				for (uint32_t i = lane; i < m; i += 64) {
-					const uint32_t e = in.sigs[start + wo + i];
-					const uint32_t p = part_of(e, bmask, shift);
-					t_rec[tb + i] = ((uint64_t)e << 32) | head;
-					t_orig[tb + i] = (uint32_t)(start + wo + i);
-					t_part[tb + i] = (uint16_t)p;
-					atomicAdd(&hist[p], 1u);
+				// all loads of this piece first (independent, in flight together)
+				uint32_t ev[kTile / 4 / 64];
+#pragma unroll
+				for (uint32_t u = 0; u < kTile / 4 / 64; u++) {
+					const uint32_t i = u * 64 + lane;
+					ev[u] = i < m ? in.sigs[start + wo + i] : 0;
+				}
+#pragma unroll
+				for (uint32_t u = 0; u < kTile / 4 / 64; u++) {
+					const uint32_t i = u * 64 + lane;
+					if (i < m) {
+						const uint32_t p = part_of(ev[u], bmask, shift);
+						t_rec[tb + i] = ((uint64_t)ev[u] << 32) | head;
+						t_orig[tb + i] = (uint32_t)(start + wo + i);
+						t_part[tb + i] = (uint16_t)p;
+						atomicAdd(&hist[p], 1u);
+					}
 				}
 				quota -= m;
 				wo += m;
