@@ -40,6 +40,10 @@ SYZ_HD uint64_t make_slot(uint32_t key, int8_t prio)
 	return ((uint64_t)key << 32) | kStateLive | (uint32_t)((uint8_t)prio ^ 0x80u);
 }
 SYZ_HD uint64_t make_absent(uint32_t key) { return ((uint64_t)key << 32) | kStatePresent; }
+// Bits 10..28 of a slot word carry a triage-run hint (csrc/triage.hip): zero
+// outside a run, cleared by the run's committers.  slot_state() masks it off.
+constexpr uint64_t kHintMask = 0x7FFFFull << 10;
+SYZ_HD uint32_t slot_state(uint64_t s) { return (uint32_t)s & 0x3FF; }
 SYZ_HD uint32_t slot_key(uint64_t s) { return (uint32_t)(s >> 32); }
 SYZ_HD bool slot_live(uint64_t s) { return (s & kStateHasPrio) != 0; }
 SYZ_HD int8_t slot_prio(uint64_t s) { return (int8_t)((uint8_t)s ^ 0x80u); }

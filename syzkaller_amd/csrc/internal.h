@@ -64,13 +64,17 @@ struct syzsig_ctx {
 	hipStream_t stream = nullptr;
 	unsigned long long* d_cnt = nullptr;  // kNumCounters
 	unsigned long long* h_cnt = nullptr;  // pinned mirror
-	syz::Workspace ws[16];                // grow-only scratch buffers (index = role, see kWs*)
+	// grow-only scratch buffers by role: 0-2 set ops, 3-6 triage candidates and
+	// small state, 7-10 host uploads of minimize, 11-14 triage partitions and
+	// minimize internals, 16-19 triage survivors, 24-29 check_new_signal uploads
+	syz::Workspace ws[32];
 	bool timing = false;                  // HIP events around triage kernels
 	// tuning knobs (defaults; SYZSIG_* environment overrides read at ctx creation)
 	int part_grid = 1024;                 // blocks of the partitioned probe/decide (multiple of 8)
-	uint64_t part_slice = 2ull << 20;     // bytes of maxSignal per partition
+	uint64_t part_slice = 4ull << 20;     // bytes of maxSignal per partition
 	int part_mode = 1;                    // 0 = never partition
-	int probe_u = 4;                      // records per lane in flight in the probe filter
+	int probe_u = 1;                      // records per lane in flight in the probe filter (1, 2)
+	int probe_drain = 128;                // survivors drained per batch (128, 256)
 	int debug_skip_b = 0;                 // timing-only diagnostics: skip the probe's pass B
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };

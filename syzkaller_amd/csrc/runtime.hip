@@ -95,6 +95,8 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 		c->part_mode = atoi(v);
 	if (const char* v = getenv("SYZSIG_PROBE_U"))
 		c->probe_u = atoi(v);
+	if (const char* v = getenv("SYZSIG_PROBE_DRAIN"))
+		c->probe_drain = atoi(v);
 	if (const char* v = getenv("SYZSIG_DEBUG_SKIP_B"))
 		c->debug_skip_b = atoi(v);
 	*out = c;

@@ -40,7 +40,7 @@ __global__ void k_rehash(const uint64_t* __restrict__ old, uint64_t nslots, uint
 	uint64_t ins = 0, ovf = 0;
 	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nslots;
 	     i += (uint64_t)gridDim.x * blockDim.x) {
-		uint64_t s = old[i];
+		uint64_t s = old[i] & ~kHintMask;  // a restarted triage run leaves hints behind
 		if (s == kSlotEmpty || (drop_absent && !slot_live(s)))
 			continue;
 		uint64_t prev;

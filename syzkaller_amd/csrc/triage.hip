@@ -95,7 +95,7 @@ struct CallsIn {
 	}
 	__device__ void rec(const Seg& g, uint32_t j, uint32_t& e, uint32_t& l, uint32_t& k) const
 	{
-		e = sigs[g.start + j];
+		e = __builtin_nontemporal_load(&sigs[g.start + j]);  // streamed once: keep caches for the table
 		l = g.level;
 		k = g.serial;
 	}
@@ -183,17 +183,48 @@ struct PartIn {
 };
 
 // ---------------------------------------------------------------- phase 1
-template <typename In, uint32_t kProbeU>
+// Run hint stored in a slot's bits 10..28 by a candidate (l, k): H = (l+1) << 16 |
+// (0xFFFF - (k >> 8)), larger = better.  It records a fact of this run -- a
+// record with level l and serial <= ((k >> 8) << 8) | 0xFF carries the element
+// -- so any record (l', k') with l' <= l and (k' >> 8) > (k >> 8) cannot be new
+// and cannot raise M_final.  Written with a plain store: a reader that misses it
+// only loses the shortcut.  Every hinted slot has a candidate, hence a
+// committer, which rewrites the word without hint bits.
+__device__ __forceinline__ uint32_t make_hint(uint32_t l, uint32_t k) { return ((l + 1) << 16) | (0xFFFF - (k >> 8)); }
+__device__ __forceinline__ bool hint_settles(uint32_t H, uint32_t l, uint32_t k)
+{
+	return H != 0 && (H >> 16) - 1 >= l && (0xFFFF - (H & 0xFFFF)) < (k >> 8);
+}
+
+constexpr uint32_t kKnown = 0x80000000u;  // queue hint: slot index known from the home bucket
+
+// Phase 1 -- probe.  Filter: kProbeU records per lane in flight; a record
+// whose element sits in its (16-B) home bucket with a live prio >= p_k, or
+// whose run hint settles it, is done (not new, changes nothing).  Survivors go
+// to this wave's LDS queue (with the slot index and word when the home bucket
+// already told them) and are drained kDrain at a time, kDrain/64 per lane in
+// flight: find/insert if needed, prio filter against M0, firsts filter,
+// atomicMin of the record's level, and a run hint for later records of the
+// element.  The slow path thus runs dense and survivors never leave the chip;
+// the drain runs inside the segment loop so hints reach later segments.
+template <typename In, uint32_t kProbeU, uint32_t kDrain>
 __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, uint32_t* firsts, uint32_t* touched,
                                                In in, LevelMap lm, uint32_t epoch, uint32_t* cand_slot,
                                                uint32_t* cand_meta, uint32_t* cand_cnt, unsigned long long* cnt,
-                                               int skip_b)
+                                               int dbg)
 {
-	__shared__ uint64_t q_rec[4][128];  // per-wave survivor queue (<= 64 + 63 entries)
-	__shared__ uint32_t q_j[4][128];
+	constexpr uint32_t QCAP = kDrain + 64 * kProbeU;
+	__shared__ uint64_t q_rec[4][QCAP];  // per-wave survivor queue: e << 32 | level << 24 | serial
+	__shared__ uint32_t q_j[4][QCAP];    // offset in the segment
+	__shared__ uint32_t q_s[4][QCAP];    // kKnown | slot index, or 0
+	__shared__ uint32_t q_v[4][QCAP];    // low word of the slot seen by the filter (when known)
 	const uint32_t lane = lane_id();
 	const uint64_t max_probe = max_probe_for(bmask);
 	uint64_t ncand = 0, ntouch = 0, ovf = 0, err = 0, nsurv = 0;
+	uint64_t* qr = q_rec[threadIdx.x >> 6];
+	uint32_t* qj = q_j[threadIdx.x >> 6];
+	uint32_t* qs = q_s[threadIdx.x >> 6];
+	uint32_t* qv = q_v[threadIdx.x >> 6];
 	in.for_each_segment(lm, [&](uint64_t s, const Seg& g) {
 		if (!g.ok) {
 			err += lane == 0;
@@ -201,49 +232,71 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
 				cand_cnt[s] = 0;
 			return;
 		}
-		// Filter: kProbeU records per lane in flight; a record whose element
-		// sits in its (16-B) home bucket with a live prio >= p_k is settled (not
-		// new, changes nothing).  Survivors go to this wave's LDS queue, which
-		// is drained 64 at a time by the full path, so the slow path runs dense
-		// and survivors never leave the chip.
 		uint32_t nc = 0, qn = 0;
-		uint64_t* qr = q_rec[threadIdx.x >> 6];
-		uint32_t* qj = q_j[threadIdx.x >> 6];
-		auto drain64 = [&](uint32_t n) {  // full path for queue entries [0, n), n <= 64
-			bool cand = false, toucher = false;
-			uint32_t sidx = 0, l = 0, j = 0;
-			if (lane < n && !skip_b) {
-				const uint64_t r = qr[lane];
-				j = qj[lane];
-				const uint32_t e = (uint32_t)(r >> 32), k = (uint32_t)r & kSerialMask;
-				l = (uint32_t)(r >> 24) & 0xff;
-				const uint32_t want = (uint32_t)make_slot(0, lm.val[l]);
-				const uint32_t tag = (epoch << 24) | k;
-				uint64_t old;
-				const int64_t idx = tbl_find_or_insert(slots, bmask, e, make_absent(e), old, max_probe);
-				if (idx < 0) {
-					ovf++;
-				} else if (!slot_live(old) || (uint32_t)old < want) {
-					sidx = (uint32_t)idx;
-					const uint4 f = reinterpret_cast<const uint4*>(firsts)[sidx];
-					if (min_from_level(f, l) >= tag) {
-						const uint32_t prev = atomicMin(&firsts[4 * (uint64_t)sidx + l], tag);
-						if (prev > ((epoch << 24) | kSerialMask)) {
-							const uint32_t bit = 1u << (sidx & 31);
-							toucher = !(atomicOr(&touched[sidx >> 5], bit) & bit);
+		auto drain = [&](uint32_t n) {  // queue entries [0, n), n <= kDrain
+			constexpr uint32_t D = kDrain / 64;
+			uint32_t sidx[D], l[D], k[D], j[D], lw[D], e[D];
+			bool live[D];
+			uint4 f[D];
+#pragma unroll
+			for (uint32_t u = 0; u < D; u++) {
+				const uint32_t q = u * 64 + lane;
+				live[u] = q < n && !(dbg & 1);
+				if (live[u]) {
+					const uint64_t r = qr[q];
+					const uint32_t hint = qs[q];
+					e[u] = (uint32_t)(r >> 32);
+					j[u] = qj[q];
+					k[u] = (uint32_t)r & kSerialMask;
+					l[u] = (uint32_t)(r >> 24) & 0xff;
+					if (hint & kKnown) {
+						sidx[u] = hint & ~kKnown;
+						lw[u] = qv[q];
+					} else {
+						const uint32_t want = (uint32_t)make_slot(0, lm.val[l[u]]);
+						uint64_t old;
+						const int64_t idx = tbl_find_or_insert(slots, bmask, e[u], make_absent(e[u]), old, max_probe);
+						if (idx < 0) {
+							ovf++;
+							live[u] = false;
+						} else if (slot_live(old) && slot_state(old) >= want) {
+							live[u] = false;  // settled after all (element beyond its home bucket)
 						}
-						cand = true;
+						sidx[u] = (uint32_t)idx;
+						lw[u] = old ? (uint32_t)old : (uint32_t)make_absent(e[u]);
 					}
 				}
 			}
-			const uint64_t m = __ballot(cand);
-			if (cand) {
-				const uint64_t pos = g.start + nc + lane_rank(m);
-				cand_slot[pos] = sidx;
-				cand_meta[pos] = ((uint32_t)toucher << 31) | (l << 24) | j;
+#pragma unroll
+			for (uint32_t u = 0; u < D; u++)
+				if (live[u])
+					f[u] = reinterpret_cast<const uint4*>(firsts)[sidx[u]];
+#pragma unroll
+			for (uint32_t u = 0; u < D; u++) {
+				bool cand = false, toucher = false;
+				if (live[u]) {
+					const uint32_t tag = (epoch << 24) | k[u];
+					if (min_from_level(f[u], l[u]) >= tag) {
+						const uint32_t prev = atomicMin(&firsts[4 * (uint64_t)sidx[u] + l[u]], tag);
+						if (prev > ((epoch << 24) | kSerialMask)) {
+							const uint32_t bit = 1u << (sidx[u] & 31);
+							toucher = !(atomicOr(&touched[sidx[u] >> 5], bit) & bit);
+						}
+						cand = true;
+						const uint32_t Hn = make_hint(l[u], k[u]);
+						if (!(dbg & 2) && Hn > ((lw[u] & (uint32_t)kHintMask) >> 10))
+							slots[sidx[u]] = ((uint64_t)e[u] << 32) | (lw[u] & ~(uint32_t)kHintMask) | ((uint64_t)Hn << 10);
+					}
+				}
+				const uint64_t m = __ballot(cand);
+				if (cand) {
+					const uint64_t pos = g.start + nc + lane_rank(m);
+					cand_slot[pos] = sidx[u];
+					cand_meta[pos] = ((uint32_t)toucher << 31) | (l[u] << 24) | j[u];
+				}
+				nc += (uint32_t)__popcll(m);
+				ntouch += toucher;
 			}
-			nc += (uint32_t)__popcll(m);
-			ntouch += toucher;
 		};
 		for (uint32_t base = 0; base < g.len; base += 64 * kProbeU) {
 			uint32_t e[kProbeU], l[kProbeU], k[kProbeU];
@@ -262,17 +315,26 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
 #pragma unroll
 			for (uint32_t u = 0; u < kProbeU; u++) {
 				bool surv = false;
+				uint32_t hint = 0, lwv = 0;
 				if (l[u] != 0xff) {
 					if (l[u] >= lm.n) {
 						err++;
 					} else {
 						const uint32_t want = (uint32_t)make_slot(0, lm.val[l[u]]);
 						const uint64_t a0 = h0[u].x, a1 = h0[u].y;
-						const bool settled = (a0 != kSlotEmpty && slot_key(a0) == e[u] && slot_live(a0) &&
-						                      (uint32_t)a0 >= want) ||
-						                     (a0 != kSlotEmpty && slot_key(a0) != e[u] && a1 != kSlotEmpty &&
-						                      slot_key(a1) == e[u] && slot_live(a1) && (uint32_t)a1 >= want);
+						const uint64_t hb = home_bucket(e[u], bmask) << kBucketShift;
+						// position of e in its home bucket: 0, 1, or unknown (2)
+						const uint32_t at = (a0 != kSlotEmpty && slot_key(a0) == e[u]) ? 0
+						                    : (a0 != kSlotEmpty && a1 != kSlotEmpty && slot_key(a1) == e[u]) ? 1 : 2;
+						const uint64_t sv = at == 0 ? a0 : a1;
+						const uint32_t H = (uint32_t)((sv & kHintMask) >> 10);
+						const bool settled = at < 2 && ((slot_live(sv) && slot_state(sv) >= want) ||
+						                                hint_settles(H, l[u], k[u]));
 						surv = !settled;
+						if (surv && at < 2 && hb + at < kKnown) {
+							hint = kKnown | (uint32_t)(hb + at);
+							lwv = (uint32_t)sv;
+						}
 					}
 				}
 				const uint64_t m = __ballot(surv);
@@ -280,33 +342,40 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* slots, uint64_t bmask, 
 					const uint32_t qp = qn + lane_rank(m);
 					qr[qp] = ((uint64_t)e[u] << 32) | ((uint64_t)l[u] << 24) | k[u];
 					qj[qp] = base + u * 64 + lane;
+					qs[qp] = hint;
+					qv[qp] = lwv;
 				}
 				qn += (uint32_t)__popcll(m);
 				nsurv += lane == 0 ? __popcll(m) : 0;
-				if (qn >= 64) {
-					__builtin_amdgcn_wave_barrier();
-					drain64(64);
-					qn -= 64;
-					if (qn) {  // move the tail (< 64 entries) to the queue head
-						uint64_t tr = 0;
-						uint32_t tj = 0;
-						if (lane < qn) {
-							tr = qr[64 + lane];
-							tj = qj[64 + lane];
-						}
-						__builtin_amdgcn_wave_barrier();
-						if (lane < qn) {
-							qr[lane] = tr;
-							qj[lane] = tj;
-						}
+			}
+			if (qn >= kDrain) {
+				__builtin_amdgcn_wave_barrier();
+				drain(kDrain);
+				qn -= kDrain;
+				// move the tail (< 64 * kProbeU entries) to the queue head
+				for (uint32_t t = 0; t < qn; t += 64) {
+					uint64_t tr = 0;
+					uint32_t tj = 0, ts = 0, tv = 0;
+					if (t + lane < qn) {
+						tr = qr[kDrain + t + lane];
+						tj = qj[kDrain + t + lane];
+						ts = qs[kDrain + t + lane];
+						tv = qv[kDrain + t + lane];
 					}
 					__builtin_amdgcn_wave_barrier();
+					if (t + lane < qn) {
+						qr[t + lane] = tr;
+						qj[t + lane] = tj;
+						qs[t + lane] = ts;
+						qv[t + lane] = tv;
+					}
 				}
+				__builtin_amdgcn_wave_barrier();
 			}
 		}
 		if (qn) {
 			__builtin_amdgcn_wave_barrier();
-			drain64(qn);
+			drain(qn);
 			__builtin_amdgcn_wave_barrier();
 		}
 		if (lane == 0) {
@@ -696,6 +765,27 @@ static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* r
 // One run (<= 4 prio levels): probe, then decide+commit.  On capacity
 // overflow the run's only table side effects -- absent markers -- are dropped
 // by a rehash into a bigger table and the run restarts.
+// probe variants: records per lane in flight (probe_u) x survivors drained per batch
+template <typename In>
+static void launch_probe(syzsig_ctx* ctx, int grid, syzsig_set* ms, const In& in, const LevelMap& lm,
+                         uint32_t* cand_slot, uint32_t* cand_meta, uint32_t* cand_cnt)
+{
+#define SYZ_PROBE(U, D)                                                                                     \
+	k_probe<In, U, D><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in, lm, \
+	                                                 ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt,         \
+	                                                 ctx->debug_skip_b)
+	const bool u2 = ctx->probe_u == 2, d2 = ctx->probe_drain == 128;
+	if (u2 && d2)
+		SYZ_PROBE(2, 128);
+	else if (u2)
+		SYZ_PROBE(2, 256);
+	else if (d2)
+		SYZ_PROBE(1, 128);
+	else
+		SYZ_PROBE(1, 256);
+#undef SYZ_PROBE
+}
+
 // `prep(&in, &grid)` builds the kernels' input for the table's current
 // geometry (it runs again after a restart on a bigger table).
 template <typename In, typename Prep>
@@ -714,15 +804,7 @@ static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, Prep pre
 		SYZ_TRY(counters_reset(ctx));
 		if (ctx->timing)
 			SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
-		if (ctx->probe_u == 2)
-			k_probe<In, 2><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in,
-			                                              lm, ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt, ctx->debug_skip_b);
-		else if (ctx->probe_u == 1)
-			k_probe<In, 1><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in,
-			                                              lm, ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt, ctx->debug_skip_b);
-		else
-			k_probe<In, 4><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in,
-			                                              lm, ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt, ctx->debug_skip_b);
+		launch_probe<In>(ctx, grid, ms, in, lm, cand_slot, cand_meta, cand_cnt);
 		SYZ_HIP(hipGetLastError());
 		if (ctx->timing)
 			SYZ_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -982,12 +1064,12 @@ int syzsig_check_new_signal(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set
 		SYZ_TRY(syzsig_set_make(ctx, 0, max_signal));
 	const uint64_t nwords = (nrec + 31) / 32;
 	void *ds, *dcs, *dcl, *dcp, *dbits, *dnew;
-	SYZ_TRY(ws_get(ctx, 7, nrec * 4 + 4, &ds));
-	SYZ_TRY(ws_get(ctx, 8, ncalls * 8 + 8, &dcs));
-	SYZ_TRY(ws_get(ctx, 9, ncalls * 4 + 4, &dcl));
-	SYZ_TRY(ws_get(ctx, 10, ncalls + 1, &dcp));
-	SYZ_TRY(ws_get(ctx, 11, nwords * 4 + 4, &dbits));
-	SYZ_TRY(ws_get(ctx, 12, ncalls + 1, &dnew));
+	SYZ_TRY(ws_get(ctx, 24, nrec * 4 + 4, &ds));
+	SYZ_TRY(ws_get(ctx, 25, ncalls * 8 + 8, &dcs));
+	SYZ_TRY(ws_get(ctx, 26, ncalls * 4 + 4, &dcl));
+	SYZ_TRY(ws_get(ctx, 27, ncalls + 1, &dcp));
+	SYZ_TRY(ws_get(ctx, 28, nwords * 4 + 4, &dbits));
+	SYZ_TRY(ws_get(ctx, 29, ncalls + 1, &dnew));
 	if (nrec)
 		SYZ_HIP(hipMemcpyAsync(ds, sigs, nrec * 4, hipMemcpyHostToDevice, ctx->stream));
 	if (ncalls) {
