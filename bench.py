@@ -48,6 +48,31 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel_prefix, cfg):
+    """HBM bytes per launch of the dominant kernel from the newest committed
+    rocprofv3 PMC summary (profiles/*/summary.json, written by
+    scripts/summarize_prof.py from separate FETCH_SIZE / WRITE_SIZE passes of
+    this same bench command) whose workload matches; None if there is none."""
+    import glob
+
+    keys = ("programs_per_gpu", "calls", "pcs_per_call", "m0_per_gpu", "skew")
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        bc = d.get("bench_config") or {}
+        if any(bc.get(k) != cfg.get(k) for k in keys) or bc.get("parallelism") != cfg.get("parallelism"):
+            continue
+        for name, e in d.get("kernels", {}).items():
+            if name.startswith(kernel_prefix) and "traffic_bytes" in e:
+                t = f  # profiles/rNN_* sort by round
+                if best is None or t > best[0]:
+                    best = (t, e["traffic_bytes"], os.path.relpath(f, ROOT))
+    return (best[1], best[2]) if best else (None, None)
+
+
 def cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, calls_per_prog, target_s):
     """The oracle (single-threaded C restatement of checkNewSignal/pkg/signal,
     oracle/oracle.c) on a bounded sample: the first S programs of this batch
@@ -208,6 +233,10 @@ def main():
                        "edge_pcs_per_s": npc / (np.median(edge_ms) * 1e-3)},
             "triage": {k: v for k, v in s0.items() if k not in ("probe_ms", "decide_ms")},
         }
+    if rank == 0:
+        traffic, src = pmc_traffic("syz::k_probe", out["config"])
+        out["roofline"]["traffic"] = traffic
+        out["roofline"]["traffic_source"] = src
     if rank == 0 and world == 1 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, C, a.cpu_seconds)
     elif rank == 0:
