@@ -29,6 +29,9 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PROBE_BYTES_PER_REC = 12.0  # 4 B element read + 8 B maxSignal slot read
+# the K3 pipeline of one step on one GPU (csrc/agg.hip); roofline.avg_launch_ms is
+# their summed device time (HIP events), roofline.traffic their summed PMC bytes
+K3_KERNELS = "k_agg_count+k_agg_scan_chunks+k_agg_scan_totals+k_agg_scatter+k_agg+k_agg_finalize"
 
 
 def parse():
@@ -48,7 +51,7 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_prefix, cfg):
+def pmc_traffic(kernel_prefixes, cfg):
     """HBM bytes per launch of the dominant kernel from the newest committed
     rocprofv3 PMC summary (profiles/*/summary.json, written by
     scripts/summarize_prof.py from separate FETCH_SIZE / WRITE_SIZE passes of
@@ -65,11 +68,14 @@ def pmc_traffic(kernel_prefix, cfg):
         bc = d.get("bench_config") or {}
         if any(bc.get(k) != cfg.get(k) for k in keys) or bc.get("parallelism") != cfg.get("parallelism"):
             continue
+        tot, hit = 0.0, False
         for name, e in d.get("kernels", {}).items():
-            if name.startswith(kernel_prefix) and "traffic_bytes" in e:
-                t = f  # profiles/rNN_* sort by round
-                if best is None or t > best[0]:
-                    best = (t, e["traffic_bytes"], os.path.relpath(f, ROOT))
+            if any(name == k or name.startswith(k + "<") for k in kernel_prefixes) and "traffic_bytes" in e:
+                tot += e["traffic_bytes"]
+                hit = True
+        t = f  # profiles/rNN_* sort by round
+        if hit and (best is None or t > best[0]):
+            best = (t, tot, os.path.relpath(f, ROOT))
     return (best[1], best[2]) if best else (None, None)
 
 
@@ -164,7 +170,14 @@ def main():
         ms = sized
     pristine = ms.clone()
     ns = S.Signal.make(4_000_000, dev.eng)
-    b, bits, cnew = dev.batch(sigs, cs, cnt, prio)
+    if distributed:
+        b, bits, cnew = dev.batch(sigs, cs, cnt, prio)
+    else:
+        # checkNewSignal's outputs: the calls with new signal, every call's DiffRaw
+        # result (pairs), maxSignal and newSignal (per-record bits are not part of
+        # the reference's result and are not computed)
+        pairs = torch.empty(16 << 20, dtype=torch.int64, device=dev.dev)
+        b, bits, cnew = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
     if distributed:
         sharded = ShardedTriage(GpuShardOps(dev), ms, ns)
 
@@ -173,7 +186,7 @@ def main():
         ns.clear()
         if distributed:
             return sharded.step((b, bits, cnew), prio, rank * P * C)[2]
-        return dev.triage(ms, ns, sigs, cs, cnt, prio, new_bits=bits, call_new=cnew)[2]
+        return dev.triage_b(ms, ns, b)
 
     for _ in range(a.warmup):
         step()
@@ -201,8 +214,12 @@ def main():
     s0 = stats[-1]
     probe_ms = float(np.mean([s["probe_ms"] for s in stats]))
     decide_ms = float(np.mean([s["decide_ms"] for s in stats]))
+    part_ms = float(np.mean([s["part_ms"] for s in stats]))
+    k3_ms = part_ms + probe_ms + decide_ms
     probe_units = s0["received"] if distributed else nrec
-    achieved = PROBE_BYTES_PER_REC * probe_units / (probe_ms * 1e-3) / 1e9
+    # roofline over the whole K3 pipeline (every kernel between the records in
+    # HBM and the updated sets), not one kernel of it
+    achieved = PROBE_BYTES_PER_REC * probe_units / (k3_ms * 1e-3) / 1e9
     out = None
     if rank == 0:
         out = {
@@ -225,16 +242,18 @@ def main():
                        "records_per_gpu": nrec, "pcs_per_gpu": npc, "skew": a.skew,
                        "table_slots": ms.capacity(),
                        "parallelism": f"shard{world}" if distributed else "single"},
-            "roofline": {"bound": "hbm", "kernel": "k_probe", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": K3_KERNELS if not distributed else "k_probe+k_decide (records)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": probe_units,
-                         "avg_launch_ms": probe_ms},
-            "stages": {"edge_ms": float(np.median(edge_ms)), "probe_ms": probe_ms, "decide_ms": decide_ms,
+                         "avg_launch_ms": k3_ms},
+            "stages": {"edge_ms": float(np.median(edge_ms)), "part_ms": part_ms, "agg_ms": probe_ms,
+                       "finalize_ms": decide_ms,
                        "edge_pcs_per_s": npc / (np.median(edge_ms) * 1e-3)},
-            "triage": {k: v for k, v in s0.items() if k not in ("probe_ms", "decide_ms")},
+            "triage": {k: v for k, v in s0.items() if k not in ("probe_ms", "decide_ms", "part_ms")},
         }
     if rank == 0:
-        traffic, src = pmc_traffic("syz::k_probe", out["config"])
+        traffic, src = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], out["config"])
         out["roofline"]["traffic"] = traffic
         out["roofline"]["traffic_source"] = src
     if rank == 0 and world == 1 and not a.no_cpu:

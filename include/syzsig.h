@@ -36,7 +36,7 @@ extern "C" {
 #define SYZSIG_ERANGE (-34)    /* a size limit of this ABI exceeded */
 #define SYZSIG_ECORRUPT (-74)  /* panic("corrupted Serial"), pkg/signal/signal.go:60-62 */
 
-#define SYZSIG_ABI_VERSION 1
+#define SYZSIG_ABI_VERSION 2
 
 typedef struct syzsig_ctx syzsig_ctx;
 typedef struct syzsig_set syzsig_set;
@@ -52,6 +52,11 @@ int syzsig_ctx_set_stream(syzsig_ctx* ctx, void* stream);
 void* syzsig_ctx_stream(syzsig_ctx* ctx);
 /* Record HIP events around the triage kernels (batch stats probe_ms/decide_ms). */
 int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable);
+/* Large-batch triage path selection (tests and tuning; results never depend on it):
+ * mode 0 = per-call probe path only, 1 = aggregation path for runs of >= 2^20
+ * records (default), 2 = aggregation path always; parts = fixed partition
+ * count of the aggregation path (0 = adaptive, else 8..2048). */
+int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
 
 /* ---- pkg/signal/signal.go ---- */
 
@@ -123,7 +128,15 @@ int syzsig_check_new_signal(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set
 /* ---- batch triage (device pointers): checkNewSignal over a whole batch ----
  * Serial order = call index order (program-major, call-minor).  Call ranges
  * [call_start, call_start+call_len) must lie inside [0, nrec) and be disjoint.
- * Outputs are zeroed by the call. */
+ * Outputs:
+ *  - call_new[c] = 1 iff call c's DiffRaw is non-empty (checkNewSignal's
+ *    `calls`, syz-fuzzer/fuzzer.go:498-503);
+ *  - new_pairs (optional): every call's DiffRaw result as (call << 32 | elem),
+ *    one entry per distinct (call, elem), in unspecified order; at most
+ *    new_pairs_cap are written, stats.new_pairs = the total;
+ *  - new_bits (optional, NULL = not computed): bit r = record r's element is in
+ *    its call's DiffRaw result (every duplicate occurrence is marked).
+ * call_new / new_bits are zeroed by the call. */
 typedef struct {
 	const uint32_t* sigs;       /* nrec raw signal elements */
 	const uint64_t* call_start; /* ncalls */
@@ -131,20 +144,25 @@ typedef struct {
 	const uint8_t* call_prio;   /* ncalls, signalPrio values */
 	uint64_t ncalls;
 	uint64_t nrec;
-	uint32_t* new_bits;         /* out: ceil(nrec/32) words, bit r = record r is new */
+	uint32_t* new_bits;         /* out (optional): ceil(nrec/32) words, bit r = record r is new */
 	uint8_t* call_new;          /* out: ncalls, 1 = call has new signal */
+	uint64_t* new_pairs;        /* out (optional): call << 32 | elem per DiffRaw entry */
+	uint64_t new_pairs_cap;     /* capacity of new_pairs in entries */
 } syzsig_batch;
 
 typedef struct {
 	uint64_t records;        /* records processed */
-	uint64_t survivors;      /* records not settled by their home bucket (full probe) */
-	uint64_t candidates;     /* records that passed the maxSignal prio filter */
+	uint64_t survivors;      /* per-call path: records past the home-bucket filter; aggregation path: distinct elements */
+	uint64_t candidates;     /* per-call path: records past the prio filter; aggregation path: = changed */
 	uint64_t changed;        /* elements whose maxSignal prio changed (incl. new) */
 	uint64_t inserted;       /* elements new to maxSignal */
 	uint64_t new_signal_len; /* Len of *new_signal after the batch */
 	uint64_t retries;        /* capacity-overflow restarts */
 	uint64_t runs;           /* sub-batches (one per <=4 distinct prios) */
-	uint64_t parts;          /* table-region partitions used (0 = per-call mode) */
+	uint64_t parts;          /* aggregation partitions of the last run (0 = per-call path) */
+	uint64_t distinct;       /* distinct elements aggregated (aggregation path) */
+	uint64_t overflow_parts; /* partitions redone in the HBM table (LDS table too small) */
+	uint64_t new_pairs;      /* DiffRaw entries over all calls (see syzsig_batch.new_pairs) */
 	double part_ms;          /* device time of record partitioning (0 unless timing enabled) */
 	double probe_ms;         /* device time of the probe kernel(s) (0 unless timing enabled) */
 	double decide_ms;        /* device time of the decide kernel(s) (0 unless timing enabled) */

@@ -37,13 +37,15 @@ class SynthCfg(ctypes.Structure):
 class Batch(ctypes.Structure):
     _fields_ = [("sigs", c_void_p), ("call_start", c_void_p), ("call_len", c_void_p),
                 ("call_prio", c_void_p), ("ncalls", c_uint64), ("nrec", c_uint64),
-                ("new_bits", c_void_p), ("call_new", c_void_p)]
+                ("new_bits", c_void_p), ("call_new", c_void_p), ("new_pairs", c_void_p),
+                ("new_pairs_cap", c_uint64)]
 
 
 class BatchStats(ctypes.Structure):
     _fields_ = [("records", c_uint64), ("survivors", c_uint64), ("candidates", c_uint64), ("changed", c_uint64),
                 ("inserted", c_uint64), ("new_signal_len", c_uint64), ("retries", c_uint64),
-                ("runs", c_uint64), ("parts", c_uint64), ("part_ms", ctypes.c_double), ("probe_ms", ctypes.c_double), ("decide_ms", ctypes.c_double)]
+                ("runs", c_uint64), ("parts", c_uint64), ("distinct", c_uint64), ("overflow_parts", c_uint64),
+                ("new_pairs", c_uint64), ("part_ms", ctypes.c_double), ("probe_ms", ctypes.c_double), ("decide_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {f[0]: (float if f[1] is ctypes.c_double else int)(getattr(self, f[0])) for f in self._fields_}
@@ -61,6 +63,7 @@ SIGNATURES = {
     "syzsig_ctx_set_stream": (c_int, [_P, _P]),
     "syzsig_ctx_stream": (_P, [_P]),
     "syzsig_ctx_set_timing": (c_int, [_P, c_int]),
+    "syzsig_ctx_set_agg": (c_int, [_P, c_int, ctypes.c_uint32]),
     "syzsig_set_make": (c_int, [_P, c_uint64, _PP]),
     "syzsig_set_free": (None, [_P]),
     "syzsig_set_clone": (c_int, [_P, _P, _PP]),

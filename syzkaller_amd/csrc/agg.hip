@@ -1,0 +1,946 @@
+// agg.hip -- K3 for large batches: checkNewSignal over a whole batch by
+// aggregating the batch's records per element in LDS.
+//
+// Reference: syz-fuzzer/fuzzer.go:494-511 checkNewSignal, pkg/signal/signal.go
+// :90-102 DiffRaw and :117-131 Merge.  With the batch in serial order
+// (program-major, call-minor; call k has raw signal sig_k and prio p_k) and
+// M0 = maxSignal before the batch:
+//
+//   e in new_k  <=>  e in sig_k  and  p_k > M0[e]  and  no j < k has e in sig_j with p_j >= p_k
+//   M_final[e]  =  max(M0[e], max_k p_k)
+//   newSignal  +=  { e : M_final[e] != M0[e] } with prio M_final[e]
+//
+// Everything about an element e is a function of
+//   first[e][l] = min serial k over the records of e at prio level l   (<= 4 levels per run)
+// and M0[e]: walking the levels from the top down, a level l with
+// val[l] > M0[e] holds a new record iff first[e][l] < min_{l' > l} first[e][l'],
+// and that record is (first[e][l], e) -- the call's DiffRaw result.  So the
+// batch needs ONE maxSignal probe per distinct element, not one per record.
+//
+// Pipeline (one run of <= 4 prio levels):
+//   k_agg_count / k_part_scan_chunks / k_part_scan / k_agg_scatter
+//       records -> 8-B packed (e << 32 | level << 24 | serial), grouped into P
+//       partitions by the top of fmix32(e): partition p holds every record of
+//       about D/P distinct elements.
+//   k_agg       one 1024-thread workgroup per partition: an LDS hash table
+//       (key + 4 level firsts, 20 B/slot, kAggSlots slots = 155 KiB) absorbs
+//       the partition's records with ds_cmpst / ds_min; then the distinct
+//       elements are written out compactly.  A partition with more distinct
+//       elements than the LDS table holds is flagged and redone by
+//       k_agg_global (the same aggregation in an HBM table).
+//   k_agg_finalize  one thread per distinct element: probe/insert maxSignal,
+//       emit the new (call, elem) pairs and call flags, write M_final, merge
+//       newSignal.  maxSignal/newSignal capacity is reserved before it from
+//       the exact distinct count, so nothing is ever retried.
+//   k_pairs_mark (optional) per-record new bits from the pairs.
+#include <algorithm>
+#include <vector>
+
+#include "internal.h"
+
+namespace syz {
+
+constexpr uint32_t kAggThreads = 1024;
+constexpr uint32_t kAggSlots = 7936;              // LDS slots per workgroup (+1 special slot)
+constexpr uint32_t kAggBuckets = kAggSlots / 4;   // 4-key buckets (one ds_read_b128 per probe)
+constexpr uint32_t kAggNoSlot = 0xFFFFFFFFu;
+constexpr uint32_t kAggRegion = kAggSlots + 1;    // distinct-list region per partition
+constexpr uint32_t kAggLimit = kAggSlots * 4 / 5;  // distinct elements before a partition overflows
+constexpr uint32_t kAggEmpty = 0xFFFFFFFFu;       // empty key (element 0xFFFFFFFF uses the special slot)
+constexpr uint32_t kAggNone = 0xFFFFFFFFu;        // no record at this level
+constexpr uint32_t kAggOverflow = 0xFFFFFFFFu;    // partition count marker
+constexpr uint32_t kAggMaxParts = 2048;
+constexpr uint32_t kAggCPB = 256;   // calls per chunk of the count/scatter passes
+constexpr uint32_t kAggTile = 12288; // records per scatter tile (10 B of LDS each)
+
+__device__ __forceinline__ uint32_t agg_part(uint32_t e, uint32_t P) { return __umulhi(fmix32(e), P); }
+// LDS home bucket: a second, independent mix (the partition used fmix32's top bits)
+__device__ __forceinline__ uint32_t agg_home_bucket(uint32_t e)
+{
+	return __umulhi(fmix32(e * 0x9E3779B1u + 0x632BE5ABu), kAggBuckets);
+}
+
+// position of e in a 4-key bucket, 4 if absent
+__device__ __forceinline__ uint32_t bucket_find(uint4 B, uint32_t e)
+{
+	return B.x == e ? 0 : B.y == e ? 1 : B.z == e ? 2 : B.w == e ? 3 : 4;
+}
+
+// Find-or-insert e in the LDS key buckets, bucket-linear from its home bucket.
+// Keys only go empty -> key, so a key is always at or before the first empty
+// slot of its probe sequence.  Returns the slot, or kAggNoSlot once the table
+// is past its limit (the partition is then redone in HBM).
+__device__ uint32_t agg_find_insert(uint4* kb, uint32_t e, uint32_t b, uint32_t* s_n, uint32_t* s_ovf)
+{
+	uint32_t* keys = reinterpret_cast<uint32_t*>(kb);
+	for (uint32_t step = 0; step < kAggBuckets; step++) {
+		for (uint32_t j = 0; j < 4; j++) {
+			const uint32_t i = b * 4 + j;
+			uint32_t key = keys[i];
+			if (key == kAggEmpty) {
+				key = atomicCAS(&keys[i], kAggEmpty, e);
+				if (key == kAggEmpty) {
+					if (atomicAdd(s_n, 1u) >= kAggLimit)
+						*(volatile uint32_t*)s_ovf = 1;
+					return i;
+				}
+			}
+			if (key == e)
+				return i;
+		}
+		b = b + 1 == kAggBuckets ? 0 : b + 1;
+	}
+	*(volatile uint32_t*)s_ovf = 1;
+	return kAggNoSlot;
+}
+
+// ---------------------------------------------------------------- partitioning
+// Calls of the run [c0, c1) in chunks of kAggCPB; counts[chunk][p].
+__global__ __launch_bounds__(kAggThreads) void k_agg_count(const uint32_t* __restrict__ sigs,
+                                                           const uint64_t* __restrict__ call_start,
+                                                           const uint32_t* __restrict__ call_len, uint64_t c0,
+                                                           uint64_t c1, uint32_t P, uint32_t* counts)
+{
+	__shared__ uint32_t h[kAggMaxParts];
+	const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = lane_id();
+	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + kAggCPB - 1) / kAggCPB;
+	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
+			h[i] = 0;
+		__syncthreads();
+		const uint64_t ce = min<uint64_t>(ncalls, (ch + 1) * kAggCPB);
+		for (uint64_t s = ch * kAggCPB + w; s < ce; s += nw) {
+			const uint64_t c = c0 + s, start = call_start[c];
+			const uint32_t len = call_len[c];
+			uint32_t j = lane;
+			for (; j + 192 < len; j += 256) {
+				const uint32_t a = sigs[start + j], b = sigs[start + j + 64], d = sigs[start + j + 128],
+				               f = sigs[start + j + 192];
+				atomicAdd(&h[agg_part(a, P)], 1u);
+				atomicAdd(&h[agg_part(b, P)], 1u);
+				atomicAdd(&h[agg_part(d, P)], 1u);
+				atomicAdd(&h[agg_part(f, P)], 1u);
+			}
+			for (; j < len; j += 64)
+				atomicAdd(&h[agg_part(sigs[start + j], P)], 1u);
+		}
+		__syncthreads();
+		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
+			counts[ch * P + i] = h[i];
+		__syncthreads();
+	}
+}
+
+// exclusive scan over a 1024-thread block; returns the total
+__device__ __forceinline__ uint32_t block_excl_scan_1k(uint32_t v, uint32_t* out)
+{
+	__shared__ uint32_t wsum[16];
+	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+	uint32_t x = v;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x, o, 64);
+		if (lane >= (uint32_t)o)
+			x += y;
+	}
+	if (lane == 63)
+		wsum[w] = x;
+	__syncthreads();
+	uint32_t pre = 0, tot = 0;
+	for (uint32_t i = 0; i < nw; i++) {
+		pre += i < w ? wsum[i] : 0;
+		tot += wsum[i];
+	}
+	__syncthreads();
+	*out = pre + x - v;
+	return tot;
+}
+
+// block p: exclusive scan over chunks of counts[.][p] -> offs[.][p]; totals[p]
+__global__ __launch_bounds__(1024) void k_agg_scan_chunks(const uint32_t* counts, uint64_t nchunks, uint32_t P,
+                                                          uint32_t* offs, uint64_t* totals)
+{
+	const uint32_t p = blockIdx.x;
+	uint64_t run = 0;
+	for (uint64_t b0 = 0; b0 < nchunks; b0 += blockDim.x) {
+		const uint64_t b = b0 + threadIdx.x;
+		const uint32_t v = b < nchunks ? counts[b * P + p] : 0;
+		uint32_t ex;
+		const uint32_t tot = block_excl_scan_1k(v, &ex);
+		if (b < nchunks)
+			offs[b * P + p] = (uint32_t)(run + ex);
+		run += tot;
+	}
+	if (threadIdx.x == 0)
+		totals[p] = run;
+}
+
+// totals -> rec_base[P + 1] (one block; P <= 2048)
+__global__ __launch_bounds__(1024) void k_agg_scan_totals(const uint64_t* totals, uint32_t P, uint64_t* rec_base)
+{
+	__shared__ uint64_t s[kAggMaxParts];
+	for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
+		s[i] = totals[i];
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		uint64_t r = 0;
+		for (uint32_t p = 0; p < P; p++) {
+			const uint64_t t = s[p];
+			s[p] = r;
+			r += t;
+		}
+		rec_base[P] = r;
+	}
+	__syncthreads();
+	for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
+		rec_base[i] = s[i];
+}
+
+// Records of each chunk -> their partitions' slices (fixed by the scan, so no
+// global atomics).  A tile of kAggTile records is staged in LDS, counting-sorted
+// by partition (the partition is recomputed from the record, so the tile costs
+// 10 B/record of LDS) and written as one run per partition.
+__global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __restrict__ sigs,
+                                                             const uint64_t* __restrict__ call_start,
+                                                             const uint32_t* __restrict__ call_len,
+                                                             const uint8_t* __restrict__ call_prio, LevelMap lm,
+                                                             uint64_t c0, uint64_t c1, uint32_t P,
+                                                             const uint32_t* __restrict__ offs,
+                                                             const uint64_t* __restrict__ rec_base, uint64_t* recs)
+{
+	constexpr uint32_t kWaves = kAggThreads / 64, kQuota = kAggTile / kWaves, kPer = kQuota / 64;
+	__shared__ uint64_t t_rec[kAggTile];
+	__shared__ uint16_t s_idx[kAggTile];
+	__shared__ uint32_t cur[kAggMaxParts], hist[kAggMaxParts], pos[kAggMaxParts];
+	__shared__ uint32_t tile_n, more;
+	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + kAggCPB - 1) / kAggCPB;
+	const uint32_t per_t = (P + blockDim.x - 1) / blockDim.x;
+	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+		const uint64_t cb = ch * kAggCPB, ce = min<uint64_t>(ncalls, cb + kAggCPB);
+		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
+			cur[i] = offs[ch * P + i];
+		uint64_t wc = cb + w;  // this wave's call (serial), then +kWaves
+		uint32_t wo = 0;       // offset inside it
+		for (;;) {
+			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
+				hist[i] = 0;
+			if (threadIdx.x == 0) {
+				tile_n = 0;
+				more = 0;
+			}
+			__syncthreads();
+			uint32_t quota = kQuota;
+			while (quota && wc < ce) {
+				const uint64_t c = c0 + wc, start = call_start[c];
+				const uint32_t len = call_len[c];
+				const uint32_t m = min(quota, len - wo);
+				uint32_t tb = 0;
+				if (lane == 0 && m)
+					tb = atomicAdd(&tile_n, m);
+				tb = __shfl(tb, 0, 64);
+				const uint64_t head = ((uint64_t)lm.lvl[call_prio[c]] << 24) | (wc & kSerialMask);
+				uint32_t ev[kPer];
+#pragma unroll
+				for (uint32_t u = 0; u < kPer; u++) {
+					const uint32_t i = u * 64 + lane;
+					ev[u] = i < m ? __builtin_nontemporal_load(&sigs[start + wo + i]) : 0;
+				}
+#pragma unroll
+				for (uint32_t u = 0; u < kPer; u++) {
+					const uint32_t i = u * 64 + lane;
+					if (i < m) {
+						t_rec[tb + i] = ((uint64_t)ev[u] << 32) | head;
+						atomicAdd(&hist[agg_part(ev[u], P)], 1u);
+					}
+				}
+				quota -= m;
+				wo += m;
+				if (wo == len) {
+					wc += kWaves;
+					wo = 0;
+				}
+			}
+			if (lane == 0 && wc < ce)
+				atomicOr(&more, 1u);
+			__syncthreads();
+			const uint32_t n = tile_n;
+			// exclusive scan of hist; pos[p] = the partition's first sorted position
+			uint32_t loc = 0;
+			for (uint32_t q = 0; q < per_t; q++) {
+				const uint32_t i = threadIdx.x * per_t + q;
+				loc += i < P ? hist[i] : 0;
+			}
+			uint32_t ex;
+			block_excl_scan_1k(loc, &ex);
+			for (uint32_t q = 0; q < per_t; q++) {
+				const uint32_t i = threadIdx.x * per_t + q;
+				if (i < P) {
+					pos[i] = ex;
+					cur[i] -= ex;  // cur[p] + d = output offset of sorted position d
+					ex += hist[i];
+				}
+			}
+			__syncthreads();
+			for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+				s_idx[atomicAdd(&pos[agg_part((uint32_t)(t_rec[i] >> 32), P)], 1u)] = (uint16_t)i;
+			__syncthreads();
+			// consecutive threads write consecutive records of one partition's run
+			for (uint32_t d = threadIdx.x; d < n; d += blockDim.x) {
+				const uint64_t r = t_rec[s_idx[d]];
+				const uint32_t p = agg_part((uint32_t)(r >> 32), P);
+				recs[rec_base[p] + (uint32_t)(cur[p] + d)] = r;  // u32 wrap intended: cur[p] = old - ex
+			}
+			__syncthreads();
+			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
+				cur[i] += pos[i];  // pos[p] = old start + hist[p]: advance by the run
+			const bool again = more != 0;
+			__syncthreads();
+			if (!again)
+				break;
+		}
+	}
+}
+
+// ---------------------------------------------------------------- aggregation
+// One workgroup per partition.  Output: the partition's distinct elements and
+// their level firsts at dist_*[p * kAggRegion ...], cnt[p] = how many, or
+// kAggOverflow when they do not fit the LDS table.
+__global__ __launch_bounds__(kAggThreads) void k_agg(const uint64_t* __restrict__ recs,
+                                                     const uint64_t* __restrict__ rec_base, uint32_t P,
+                                                     uint32_t* dist_e, uint4* dist_f, uint32_t* cnt)
+{
+	constexpr uint32_t U = 8;
+	__shared__ uint4 kb[kAggBuckets];  // keys, 4-slot buckets
+	__shared__ uint32_t fl[4][kAggRegion];
+	__shared__ uint32_t s_n, s_ovf, s_out;
+	const uint32_t* keys = reinterpret_cast<const uint32_t*>(kb);
+	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
+		for (uint32_t i = threadIdx.x; i < kAggRegion; i += blockDim.x) {
+			if (i < kAggBuckets)
+				kb[i] = make_uint4(kAggEmpty, kAggEmpty, kAggEmpty, kAggEmpty);
+			fl[0][i] = fl[1][i] = fl[2][i] = fl[3][i] = kAggNone;
+		}
+		if (threadIdx.x == 0) {
+			s_n = 0;
+			s_ovf = 0;
+			s_out = 0;
+		}
+		__syncthreads();
+		const uint64_t base = rec_base[p], end = rec_base[p + 1];
+		// records stream through registers one batch ahead of the LDS work; no
+		// barrier inside the loop (a wave leaves early once overflow is flagged)
+		uint64_t nxt[U];
+#pragma unroll
+		for (uint32_t u = 0; u < U; u++) {
+			const uint64_t j = base + u * kAggThreads + threadIdx.x;
+			nxt[u] = j < end ? __builtin_nontemporal_load(&recs[j]) : ~0ull;
+		}
+		for (uint64_t r0 = base; r0 < end; r0 += (uint64_t)U * kAggThreads) {
+			uint32_t e[U], l[U], k[U], slot[U], hb[U];
+			bool need[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++) {
+				const uint64_t r = nxt[u];
+				const uint64_t j = r0 + (uint64_t)(U + u) * kAggThreads + threadIdx.x;
+				nxt[u] = j < end ? __builtin_nontemporal_load(&recs[j]) : ~0ull;
+				e[u] = (uint32_t)(r >> 32);
+				l[u] = (uint32_t)(r >> 24) & 0xff;  // 0xff: past the end (a real record has level < 4)
+				k[u] = (uint32_t)r & kSerialMask;
+				hb[u] = agg_home_bucket(e[u]);
+			}
+			// home buckets of all U records in flight together (ds_read_b128 each)
+			uint4 B[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++)
+				B[u] = kb[hb[u]];
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++) {
+				need[u] = false;
+				slot[u] = kAggNoSlot;
+				if (l[u] == 0xff)
+					continue;
+				if (e[u] == kAggEmpty) {
+					slot[u] = kAggSlots;  // special slot of element 0xFFFFFFFF
+					continue;
+				}
+				const uint32_t f = bucket_find(B[u], e[u]);
+				if (f < 4)
+					slot[u] = hb[u] * 4 + f;
+				else
+					need[u] = true;
+			}
+			// rare: insertion or a chain past the home bucket
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++)
+				if (need[u])
+					slot[u] = agg_find_insert(kb, e[u], hb[u], &s_n, &s_ovf);
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++)
+				if (slot[u] != kAggNoSlot)
+					atomicMin(&fl[l[u] & 3][slot[u]], k[u]);
+			if (*(volatile uint32_t*)&s_ovf)
+				break;
+		}
+		__syncthreads();
+		if (s_ovf) {
+			if (threadIdx.x == 0)
+				cnt[p] = kAggOverflow;
+			__syncthreads();
+			continue;
+		}
+		// compact the occupied slots
+		const uint32_t lane = lane_id();
+		for (uint32_t i0 = 0; i0 < kAggRegion; i0 += kAggThreads) {
+			const uint32_t i = i0 + threadIdx.x;
+			bool occ = false;
+			uint32_t e = 0;
+			if (i < kAggSlots) {
+				e = keys[i];
+				occ = e != kAggEmpty;
+			} else if (i == kAggSlots) {
+				e = kAggEmpty;
+				occ = (fl[0][i] & fl[1][i] & fl[2][i] & fl[3][i]) != kAggNone;
+			}
+			const uint64_t m = __ballot(occ);
+			uint32_t wb = 0;
+			if (lane == 0 && m)
+				wb = atomicAdd(&s_out, (uint32_t)__popcll(m));
+			wb = __shfl(wb, 0, 64);
+			if (occ) {
+				const uint64_t o = (uint64_t)p * kAggRegion + wb + lane_rank(m);
+				dist_e[o] = e;
+				dist_f[o] = make_uint4(fl[0][i], fl[1][i], fl[2][i], fl[3][i]);
+			}
+		}
+		__syncthreads();
+		if (threadIdx.x == 0)
+			cnt[p] = s_out;
+		__syncthreads();
+	}
+}
+
+// ---- fallback: partitions whose distinct elements overflow the LDS table are
+// aggregated in one HBM hash table (gkeys[C] + gfl[4][C + 1], C a power of two;
+// slot C is element 0xFFFFFFFF).  Partitions hold disjoint elements, so one
+// table serves all of them.
+__global__ __launch_bounds__(256) void k_agg_global(const uint64_t* __restrict__ recs,
+                                                    const uint64_t* __restrict__ rec_base,
+                                                    const uint32_t* __restrict__ ovl, uint32_t novl, uint32_t* gkeys,
+                                                    uint32_t* gfl, uint64_t C, unsigned long long* err)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+	uint64_t bad = 0;
+	for (uint32_t q = 0; q < novl; q++) {
+		const uint32_t p = ovl[q];
+		const uint64_t end = rec_base[p + 1];
+		for (uint64_t j = rec_base[p] + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < end; j += stride) {
+			const uint64_t r = recs[j];
+			const uint32_t e = (uint32_t)(r >> 32), l = (uint32_t)(r >> 24) & 3, k = (uint32_t)r & kSerialMask;
+			uint64_t i = C;
+			if (e != kAggEmpty) {
+				i = fmix32(e * 0x9E3779B1u + 0x632BE5ABu) & (C - 1);
+				for (uint64_t step = 0;; step++) {
+					uint32_t key = gkeys[i];
+					if (key == kAggEmpty) {
+						key = atomicCAS(&gkeys[i], kAggEmpty, e);
+						if (key == kAggEmpty)
+							break;
+					}
+					if (key == e)
+						break;
+					i = (i + 1) & (C - 1);
+					if (step >= C) {
+						bad++;
+						i = ~0ull;
+						break;
+					}
+				}
+			}
+			if (i != ~0ull)
+				atomicMin(&gfl[(uint64_t)l * (C + 1) + i], k);
+		}
+	}
+	block_count(err, bad);
+}
+
+__global__ __launch_bounds__(256) void k_agg_global_compact(const uint32_t* __restrict__ gkeys,
+                                                            const uint32_t* __restrict__ gfl, uint64_t C,
+                                                            uint32_t* dist_e, uint4* dist_f,
+                                                            unsigned long long* out_cnt)
+{
+	const uint32_t lane = lane_id();
+	for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 <= C; i0 += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t i = i0 + threadIdx.x;
+		bool occ = false;
+		uint32_t e = kAggEmpty;
+		uint4 f = make_uint4(kAggNone, kAggNone, kAggNone, kAggNone);
+		if (i <= C) {
+			f = make_uint4(gfl[i], gfl[(C + 1) + i], gfl[2 * (C + 1) + i], gfl[3 * (C + 1) + i]);
+			if (i < C) {
+				e = gkeys[i];
+				occ = e != kAggEmpty;
+			} else {
+				occ = (f.x & f.y & f.z & f.w) != kAggNone;
+			}
+		}
+		const uint64_t m = __ballot(occ);
+		unsigned long long wb = 0;
+		if (lane == 0 && m)
+			wb = atomicAdd(out_cnt, (unsigned long long)__popcll(m));
+		wb = __shfl(wb, 0, 64);
+		if (occ) {
+			dist_e[wb + lane_rank(m)] = e;
+			dist_f[wb + lane_rank(m)] = f;
+		}
+	}
+}
+
+// ---------------------------------------------------------------- finalize
+// Region r covers dist_*[r * kAggRegion, + cnt[r]).  Grid-stride over the
+// region slots (many independent probe chains in flight); a block gathers its
+// pairs in LDS and appends them with one global atomic per flush.
+constexpr uint32_t kFinThreads = 256, kFinBuf = 4 * kFinThreads * 2;
+
+__global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __restrict__ dist_e,
+                                                              const uint4* __restrict__ dist_f,
+                                                              const uint32_t* __restrict__ cnt, uint32_t nregions,
+                                                              LevelMap lm, uint64_t c0, uint64_t* slots,
+                                                              uint64_t bmask, uint64_t* ns_slots, uint64_t ns_bmask,
+                                                              uint8_t* call_new, uint64_t* pairs,
+                                                              unsigned long long* npairs, unsigned long long* ctr)
+{
+	__shared__ uint64_t buf[kFinBuf];
+	__shared__ uint32_t s_n;
+	__shared__ unsigned long long s_base;
+	const uint64_t max_probe = max_probe_for(bmask);
+	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0;
+	if (threadIdx.x == 0)
+		s_n = 0;
+	__syncthreads();
+	const uint64_t total = (uint64_t)nregions * kAggRegion;
+	for (uint64_t o0 = blockIdx.x * (uint64_t)blockDim.x; o0 < total; o0 += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t o = o0 + threadIdx.x;
+		const uint32_t r = (uint32_t)(o / kAggRegion), i = (uint32_t)(o % kAggRegion);
+		if (o < total && cnt[r] != kAggOverflow && i < cnt[r]) {
+			const uint32_t e = dist_e[o];
+			const uint4 f4 = dist_f[o];
+			const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
+			int top = -1;
+#pragma unroll
+			for (int l = 0; l < 4; l++)
+				if (l < (int)lm.n && f[l] != kAggNone)
+					top = l;
+			if (top >= 0) {
+				// one probe sequence: insert M_final if absent, else read M0
+				const int8_t P = lm.val[top];
+				const uint64_t word = make_slot(e, P);
+				uint64_t old = 0;
+				const int64_t idx = tbl_find_or_insert(slots, bmask, e, word, old, max_probe);
+				if (idx < 0) {
+					ovf++;
+				} else {
+					const bool present = slot_live(old);  // (old == 0: inserted just now)
+					const int p0 = present ? (int)slot_prio(old) : -1000;
+					if ((int)P > p0) {
+						if (old != 0)
+							slots[idx] = word;  // one entry per element: no other writer
+						inserted += !present;  // fresh, or an "absent" marker going live
+						changed++;
+						const int rr = tbl_merge(ns_slots, ns_bmask, e, P);
+						ns_ins += rr == 1;
+						ovf += rr < 0;
+						// the staircase: first records of strictly rising level above M0[e]
+						uint32_t mk = kAggNone;
+#pragma unroll
+						for (int l = 3; l >= 0; l--) {
+							if (l > top || f[l] == kAggNone)
+								continue;
+							if ((int)lm.val[l] <= p0)
+								break;
+							if (f[l] < mk) {
+								mk = f[l];
+								const uint64_t c = c0 + f[l];
+								call_new[c] = 1;
+								buf[atomicAdd(&s_n, 1u)] = (c << 32) | e;
+							}
+						}
+					}
+				}
+			}
+		}
+		__syncthreads();
+		const uint32_t n = s_n;
+		if (n > kFinBuf - 4 * kFinThreads || o0 + (uint64_t)gridDim.x * blockDim.x >= total) {
+			if (threadIdx.x == 0)
+				s_base = n ? atomicAdd(npairs, (unsigned long long)n) : 0;
+			__syncthreads();
+			for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
+				pairs[s_base + t] = buf[t];
+			__syncthreads();
+			if (threadIdx.x == 0)
+				s_n = 0;
+			__syncthreads();
+		}
+	}
+	block_count(&ctr[kCntInserted], inserted);
+	block_count(&ctr[kCntChanged], changed);
+	block_count(&ctr[kCntAux], ns_ins);
+	block_count(&ctr[kCntOverflow], ovf);
+}
+
+// ---------------------------------------------------------------- new bits
+__device__ __forceinline__ uint64_t pair_hash(uint64_t k)
+{
+	k ^= k >> 33;
+	k *= 0xff51afd7ed558ccdull;
+	k ^= k >> 33;
+	k *= 0xc4ceb9fe1a85ec53ull;
+	k ^= k >> 33;
+	return k;
+}
+
+// Insert pairs into a set of capacity C (power of two, empty = ~0).
+// Duplicates are dropped; `uniq` counts distinct ones.
+__global__ __launch_bounds__(256) void k_pairs_set(const uint64_t* __restrict__ pairs, uint64_t n, uint64_t* set,
+                                                   uint64_t C, unsigned long long* uniq)
+{
+	uint64_t u = 0;
+	for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t v = pairs[t];
+		uint64_t i = pair_hash(v) & (C - 1);
+		for (uint64_t step = 0; step < C; step++) {
+			uint64_t k = set[i];
+			if (k == ~0ull) {
+				k = atomicCAS((unsigned long long*)&set[i], ~0ull, (unsigned long long)v);
+				if (k == ~0ull) {
+					u++;
+					break;
+				}
+			}
+			if (k == v)
+				break;
+			i = (i + 1) & (C - 1);
+		}
+	}
+	block_count(uniq, u);
+}
+
+__device__ __forceinline__ bool pairs_has(const uint64_t* set, uint64_t C, uint64_t v)
+{
+	uint64_t i = pair_hash(v) & (C - 1);
+	for (uint64_t step = 0; step < C; step++) {
+		const uint64_t k = set[i];
+		if (k == v)
+			return true;
+		if (k == ~0ull)
+			return false;
+		i = (i + 1) & (C - 1);
+	}
+	return false;
+}
+
+// one wave per call: bit r = (call, sigs[r]) is a new pair
+__global__ __launch_bounds__(256) void k_pairs_mark(const uint32_t* __restrict__ sigs,
+                                                    const uint64_t* __restrict__ call_start,
+                                                    const uint32_t* __restrict__ call_len, uint64_t c0, uint64_t c1,
+                                                    const uint8_t* __restrict__ call_new, const uint64_t* set,
+                                                    uint64_t C, uint32_t* new_bits)
+{
+	const uint32_t lane = lane_id();
+	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	for (uint64_t c = c0 + blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); c < c1; c += nwaves) {
+		if (!call_new[c])
+			continue;
+		const uint64_t st = call_start[c];
+		const uint32_t len = call_len[c];
+		for (uint32_t j = lane; j < len; j += 64)
+			if (pairs_has(set, C, (c << 32) | sigs[st + j]))
+				atomicOr(&new_bits[(st + j) >> 5], 1u << ((st + j) & 31));
+	}
+}
+
+// dedupped pairs from the set (compaction)
+__global__ __launch_bounds__(256) void k_pairs_compact(const uint64_t* __restrict__ set, uint64_t C, uint64_t* out,
+                                                       unsigned long long* n)
+{
+	const uint32_t lane = lane_id();
+	for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < C; i0 += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t i = i0 + threadIdx.x;
+		const uint64_t v = i < C ? set[i] : ~0ull;
+		const bool occ = v != ~0ull;
+		const uint64_t m = __ballot(occ);
+		unsigned long long wb = 0;
+		if (lane == 0 && m)
+			wb = atomicAdd(n, (unsigned long long)__popcll(m));
+		wb = __shfl(wb, 0, 64);
+		if (occ)
+			out[wb + lane_rank(m)] = v;
+	}
+}
+
+// pairs from per-record bits of calls [c0, c1) (per-call path); may repeat a pair
+__global__ __launch_bounds__(256) void k_bits_to_pairs(const uint32_t* __restrict__ sigs,
+                                                       const uint64_t* __restrict__ call_start,
+                                                       const uint32_t* __restrict__ call_len, uint64_t c0, uint64_t c1,
+                                                       const uint8_t* __restrict__ call_new,
+                                                       const uint32_t* __restrict__ bits, uint64_t* pairs,
+                                                       unsigned long long* n)
+{
+	const uint32_t lane = lane_id();
+	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	for (uint64_t c = c0 + blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); c < c1; c += nwaves) {
+		if (!call_new[c])
+			continue;
+		const uint64_t st = call_start[c];
+		const uint32_t len = call_len[c];
+		for (uint32_t j0 = 0; j0 < len; j0 += 64) {
+			const uint32_t j = j0 + lane;
+			const bool on = j < len && ((bits[(st + j) >> 5] >> ((st + j) & 31)) & 1);
+			const uint64_t m = __ballot(on);
+			unsigned long long wb = 0;
+			if (lane == 0 && m)
+				wb = atomicAdd(n, (unsigned long long)__popcll(m));
+			wb = __shfl(wb, 0, 64);
+			if (on)
+				pairs[wb + lane_rank(m)] = (c << 32) | sigs[st + j];
+		}
+	}
+}
+
+// ---------------------------------------------------------------- host
+static uint64_t pow2_at_least(uint64_t x)
+{
+	uint64_t p = 1;
+	while (p < x)
+		p <<= 1;
+	return p;
+}
+
+uint32_t agg_parts_for(syzsig_ctx* ctx, uint64_t nrec)
+{
+	// expected distinct elements: the ratio seen on the previous large batch
+	// (1/32 before the first), aiming at ~70% LDS load per partition (overflow at 80%)
+	const double ratio = ctx->agg_distinct_ratio > 0 ? ctx->agg_distinct_ratio : 1.0 / 32;
+	const double d = ratio * (double)nrec;
+	uint64_t P = (uint64_t)(d / (0.7 * kAggSlots)) + 1;
+	P = (P + 7) & ~7ull;
+	if (ctx->agg_parts)
+		P = ctx->agg_parts;
+	return (uint32_t)std::max<uint64_t>(8, std::min<uint64_t>(kAggMaxParts, P));
+}
+
+// One run of calls [c0, c1) with level map lm.  Pairs are appended at
+// pairs[*npairs_host ...] (capacity cap_pairs, internal buffer).
+int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,
+                   const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs_out,
+                   uint64_t* npairs_io)
+{
+	const uint32_t P = agg_parts_for(ctx, run_recs);
+	const uint64_t nchunks = (c1 - c0 + kAggCPB - 1) / kAggCPB;
+	void *recs, *cm, *pm, *de, *df, *dc, *pr;
+	SYZ_TRY(ws_get(ctx, 16, run_recs * 8 + 64, &recs));
+	SYZ_TRY(ws_get(ctx, 17, nchunks * P * 4 * 2 + 64, &cm));
+	SYZ_TRY(ws_get(ctx, 18, (kAggMaxParts + 1) * 8 * 2, &pm));
+	uint32_t* counts = (uint32_t*)cm;
+	uint32_t* offs = counts + nchunks * P;
+	uint64_t* totals = (uint64_t*)pm;
+	uint64_t* rec_base = totals + kAggMaxParts + 1;
+	const hipStream_t s = ctx->stream;
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
+	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
+	k_agg_count<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1, P, counts);
+	k_agg_scan_chunks<<<P, 1024, 0, s>>>(counts, nchunks, P, offs, totals);
+	k_agg_scan_totals<<<1, 1024, 0, s>>>(totals, P, rec_base);
+	k_agg_scatter<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, P, offs,
+	                                         rec_base, (uint64_t*)recs);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
+	// aggregation
+	SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
+	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
+	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
+	k_agg<<<P, kAggThreads, 0, s>>>((const uint64_t*)recs, rec_base, P, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
+	std::vector<uint32_t> hc(P);
+	std::vector<uint64_t> hb(P + 1);
+	SYZ_HIP(hipMemcpyAsync(hc.data(), dc, P * 4, hipMemcpyDeviceToHost, s));
+	SYZ_HIP(hipMemcpyAsync(hb.data(), rec_base, (P + 1) * 8, hipMemcpyDeviceToHost, s));
+	SYZ_HIP(hipStreamSynchronize(s));
+	if (ctx->timing) {
+		float t0 = 0, t1 = 0;
+		SYZ_HIP(hipEventElapsedTime(&t0, ctx->ev[0], ctx->ev[1]));
+		SYZ_HIP(hipEventElapsedTime(&t1, ctx->ev[1], ctx->ev[2]));
+		st->part_ms += t0;
+		st->probe_ms += t1;
+	}
+	uint64_t D = 0, ovrec = 0;
+	std::vector<uint32_t> ovl;
+	for (uint32_t p = 0; p < P; p++) {
+		if (hc[p] == kAggOverflow) {
+			ovl.push_back(p);
+			ovrec += hb[p + 1] - hb[p];
+		} else {
+			D += hc[p];
+		}
+	}
+	uint32_t nregions = P;
+	void* dist_e = de;
+	void* dist_f = df;
+	if (!ovl.empty()) {
+		// fallback: HBM aggregation table for the overflowed partitions; their
+		// distinct list is appended as extra regions after the P LDS regions
+		const uint64_t C = pow2_at_least(std::max<uint64_t>(2 * ovrec, 1024));
+		const uint64_t extra_regions = (ovrec + kAggRegion - 1) / kAggRegion + 1;
+		void *gk, *gf, *ol;
+		SYZ_TRY(ws_get(ctx, 23, C * 4 + (C + 1) * 16 + 64, &gk));
+		gf = (char*)gk + C * 4;
+		SYZ_TRY(ws_get(ctx, 22, ovl.size() * 4 + 64, &ol));
+		// distinct lists must be contiguous with the regions: grow 19/20 keeping the LDS part
+		const uint64_t tot_e = ((uint64_t)P + extra_regions) * kAggRegion;
+		void *de2, *df2;
+		SYZ_TRY(ws_get(ctx, 30, tot_e * 4 + 64, &de2));
+		SYZ_TRY(ws_get(ctx, 31, tot_e * 16 + 64, &df2));
+		SYZ_HIP(hipMemcpyAsync(de2, de, (uint64_t)P * kAggRegion * 4, hipMemcpyDeviceToDevice, s));
+		SYZ_HIP(hipMemcpyAsync(df2, df, (uint64_t)P * kAggRegion * 16, hipMemcpyDeviceToDevice, s));
+		SYZ_HIP(hipMemsetAsync(gk, 0xff, C * 4 + (C + 1) * 16, s));
+		SYZ_HIP(hipMemcpyAsync(ol, ovl.data(), ovl.size() * 4, hipMemcpyHostToDevice, s));
+		SYZ_TRY(counters_reset(ctx));
+		k_agg_global<<<grid_for(ovrec, 256, 8192), 256, 0, s>>>((const uint64_t*)recs, rec_base, (const uint32_t*)ol,
+		                                                         (uint32_t)ovl.size(), (uint32_t*)gk, (uint32_t*)gf, C,
+		                                                         &ctx->d_cnt[kCntError]);
+		k_agg_global_compact<<<grid_for(C + 1, 256, 8192), 256, 0, s>>>(
+		    (const uint32_t*)gk, (const uint32_t*)gf, C, (uint32_t*)de2 + (uint64_t)P * kAggRegion,
+		    (uint4*)df2 + (uint64_t)P * kAggRegion, &ctx->d_cnt[kCntAux2]);
+		SYZ_HIP(hipGetLastError());
+		SYZ_TRY(counters_fetch(ctx));
+		if (ctx->h_cnt[kCntError])
+			return fail(SYZSIG_EIO, "triage: aggregation table overflow (internal error)");
+		const uint64_t gcnt = ctx->h_cnt[kCntAux2];
+		D += gcnt;
+		// region counts: LDS partitions (overflowed = 0), then the fallback list in kAggRegion pieces
+		std::vector<uint32_t> rc(hc);
+		for (uint32_t p : ovl)
+			rc[p] = 0;
+		for (uint64_t left = gcnt; left; left -= std::min<uint64_t>(left, kAggRegion))
+			rc.push_back((uint32_t)std::min<uint64_t>(left, kAggRegion));
+		nregions = (uint32_t)rc.size();
+		void* dc2;
+		SYZ_TRY(ws_get(ctx, 21, rc.size() * 4 + 64, &dc2));
+		SYZ_HIP(hipMemcpyAsync(dc2, rc.data(), rc.size() * 4, hipMemcpyHostToDevice, s));
+		SYZ_HIP(hipStreamSynchronize(s));  // rc is a host temporary
+		dc = dc2;
+		dist_e = de2;
+		dist_f = df2;
+		st->overflow_parts += ovl.size();
+	}
+	st->distinct += D;
+	st->parts = P;
+	st->survivors += D;
+	ctx->agg_distinct_ratio = run_recs ? (double)D / (double)run_recs : 0;
+	// capacity for every possible change, then finalize (never retried)
+	SYZ_TRY(set_reserve(ms, D));
+	// newSignal.Merge allocates a nil receiver (signal.go:121-125) -- but only
+	// when some DiffRaw is non-empty: a fresh set is dropped again if nothing changed
+	const bool fresh_ns = D && !*ns;
+	if (fresh_ns)
+		SYZ_TRY(syzsig_set_make(ctx, D, ns));
+	if (D)
+		SYZ_TRY(set_reserve(*ns, D));
+	const uint64_t need_pairs = *npairs_io + 4 * D;
+	SYZ_TRY(ws_grow_keep(ctx, 15, need_pairs * 8 + 64, *npairs_io * 8, &pr));
+	*pairs_out = (uint64_t*)pr;
+	SYZ_TRY(counters_reset(ctx));
+	SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], npairs_io, 8, hipMemcpyHostToDevice, s));
+	syzsig_set* nsp = *ns;
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
+	if (D)
+		k_agg_finalize<<<grid_for((uint64_t)nregions * kAggRegion, kFinThreads, 2048), kFinThreads, 0, s>>>(
+		    (const uint32_t*)dist_e, (const uint4*)dist_f, (const uint32_t*)dc, nregions, lm, c0, ms->slots,
+		    ms->nbuckets - 1, nsp ? nsp->slots : nullptr, nsp ? nsp->nbuckets - 1 : 0, b->call_new, (uint64_t*)pr,
+		    &ctx->d_cnt[kCntAux2], ctx->d_cnt);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[3], s));
+	SYZ_TRY(counters_fetch(ctx));
+	if (ctx->timing) {
+		float t = 0;
+		SYZ_HIP(hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]));
+		st->decide_ms += t;
+	}
+	if (ctx->h_cnt[kCntOverflow])
+		return fail(SYZSIG_EIO, "triage: table overflow after reserve (internal error)");
+	if (fresh_ns && ctx->h_cnt[kCntChanged] == 0) {
+		syzsig_set_free(*ns);
+		*ns = nullptr;
+		nsp = nullptr;
+	}
+	ms->len += ctx->h_cnt[kCntInserted];
+	st->inserted += ctx->h_cnt[kCntInserted];
+	st->changed += ctx->h_cnt[kCntChanged];
+	st->candidates += ctx->h_cnt[kCntChanged];
+	if (nsp)
+		nsp->len += ctx->h_cnt[kCntAux];
+	*npairs_io = ctx->h_cnt[kCntAux2];
+	st->runs++;
+	return SYZSIG_OK;
+}
+
+// Per-record bits of calls [c0, c1) from the run's pairs [p0, p1).
+int agg_mark_bits(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const uint64_t* pairs,
+                  uint64_t p0, uint64_t p1)
+{
+	if (p1 == p0 || !b->new_bits)
+		return SYZSIG_OK;
+	const uint64_t n = p1 - p0, C = pow2_at_least(2 * n + 16);
+	void* set;
+	SYZ_TRY(ws_get(ctx, 14, C * 8, &set));
+	const hipStream_t s = ctx->stream;
+	SYZ_HIP(hipMemsetAsync(set, 0xff, C * 8, s));
+	SYZ_TRY(counters_reset(ctx));
+	k_pairs_set<<<grid_for(n, 256, 8192), 256, 0, s>>>(pairs + p0, n, (uint64_t*)set, C, &ctx->d_cnt[kCntAux]);
+	k_pairs_mark<<<grid_for((c1 - c0) * 64, 256, 8192), 256, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1,
+	                                                                  b->call_new, (const uint64_t*)set, C, b->new_bits);
+	SYZ_HIP(hipGetLastError());
+	return SYZSIG_OK;
+}
+
+// Pairs of the per-call path from its bits: collect, then dedup through a set.
+int pairs_from_bits(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* bits, uint64_t c0, uint64_t c1,
+                    uint64_t bound, uint64_t** pairs_io, uint64_t* npairs_io)
+{
+	const hipStream_t s = ctx->stream;
+	void *raw, *set, *out;
+	SYZ_TRY(ws_get(ctx, 13, bound * 8 + 64, &raw));
+	SYZ_TRY(counters_reset(ctx));
+	k_bits_to_pairs<<<grid_for((c1 - c0) * 64, 256, 8192), 256, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1,
+	                                                                     b->call_new, bits, (uint64_t*)raw,
+	                                                                     &ctx->d_cnt[kCntAux]);
+	SYZ_HIP(hipGetLastError());
+	SYZ_TRY(counters_fetch(ctx));
+	const uint64_t n = ctx->h_cnt[kCntAux];
+	if (n == 0)
+		return SYZSIG_OK;
+	const uint64_t C = pow2_at_least(2 * n + 16);
+	SYZ_TRY(ws_get(ctx, 14, C * 8, &set));
+	SYZ_HIP(hipMemsetAsync(set, 0xff, C * 8, s));
+	SYZ_TRY(ws_grow_keep(ctx, 15, (*npairs_io + n) * 8 + 64, *npairs_io * 8, &out));
+	*pairs_io = (uint64_t*)out;
+	SYZ_TRY(counters_reset(ctx));
+	SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], npairs_io, 8, hipMemcpyHostToDevice, s));
+	k_pairs_set<<<grid_for(n, 256, 8192), 256, 0, s>>>((const uint64_t*)raw, n, (uint64_t*)set, C,
+	                                                   &ctx->d_cnt[kCntAux]);
+	k_pairs_compact<<<grid_for(C, 256, 8192), 256, 0, s>>>((const uint64_t*)set, C, (uint64_t*)out,
+	                                                       &ctx->d_cnt[kCntAux2]);
+	SYZ_HIP(hipGetLastError());
+	SYZ_TRY(counters_fetch(ctx));
+	*npairs_io = ctx->h_cnt[kCntAux2];
+	return SYZSIG_OK;
+}
+
+}  // namespace syz

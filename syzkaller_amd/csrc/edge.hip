@@ -6,13 +6,23 @@
 // dedup table lives in LDS for the program's lifetime, calls run in order.
 // K1 is data-parallel: sig_i = (u32)pc_i ^ hash((u32)pc_{i-1}) with the
 // previous PC's hash taken from the neighbour lane.  K2 is a sequential state
-// machine, parallelised exactly: signal i touches only its 4-slot window
-// {h, h+1, h+2, h+3} (h = sig % 8192, forced overwrite at h), so operations
-// with disjoint windows commute.  Per 64-signal chunk, lanes run in rounds; a
-// lane runs once no EARLIER pending lane shares an 8-slot bin with its window
-// (conflict stamps in LDS: atomicMax of round<<8 | (63-lane) per bin).  Every
-// conflicting pair therefore keeps its trace order, which is all the
-// sequential semantics depend on.
+// machine, parallelised exactly.  Signal i reads only its 4-slot window
+// {h, h+1, h+2, h+3} (h = sig % 8192) and writes at most one slot of it (insert
+// at the first empty slot, or the forced overwrite at h); a duplicate writes
+// nothing.  Per 64-signal chunk, lanes run in rounds:
+//   1. every pending lane evaluates dedup() against the table as it stands
+//      (read only): duplicate, or a write at some slot of its window;
+//   2. writers mark the 8-slot bins their window touches (LDS stamps keep the
+//      earliest marking lane per bin); a pending lane with an EARLIER marker in
+//      its bins is blocked -- and marks its own bins too, since its re-run may
+//      turn into a write (repeated until no new marks);
+//   3. unblocked lanes are final: writers store, everyone leaves the round.
+// A final lane has only final duplicates before it inside its window, and
+// duplicates change nothing, so it saw exactly the sequential table state;
+// a lane after it that writes into its window does so after it read.  Mostly
+// duplicates (repeated edges) therefore finish in one round.
+// Latency: the trace is read kEdgeDepth chunks ahead of the chunk being
+// deduplicated (registers), so the HBM round trip overlaps LDS work.
 #include "internal.h"
 
 namespace syz {
@@ -20,6 +30,24 @@ namespace syz {
 constexpr uint32_t kBinShift = 3;  // 8-slot bins
 constexpr uint32_t kBins = kDedupSize >> kBinShift;
 constexpr uint32_t kEpochMax = 0xFFFFFF;
+constexpr uint32_t kEdgeDepth = 8;  // chunks of 64 PCs in flight per wave
+
+// The workgroup is ONE wave, so LDS traffic between its lanes needs no s_barrier
+// -- and __syncthreads() would also drain every outstanding global load (the
+// workgroup-scope release waits for vmcnt(0)), defeating the trace prefetch.
+// A wave's DS instructions execute in order; wait for them (lgkmcnt(0) only)
+// and keep the compiler from moving LDS accesses across.
+__device__ __forceinline__ void wave_lds_sync()
+{
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+	__builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt/expcnt untouched, lgkmcnt(0)
+	__builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ bool stamp_earlier(uint32_t s, uint32_t epoch, uint32_t lane)
+{
+	return (s >> 8) == epoch && 63 - (s & 255) < lane;
+}
 
 __global__ __launch_bounds__(64) void k_edge_dedup(const uint64_t* __restrict__ pcs, uint64_t npc,
                                                    const uint64_t* __restrict__ call_start,
@@ -58,73 +86,107 @@ __global__ __launch_bounds__(64) void k_edge_dedup(const uint64_t* __restrict__ 
 				break;
 			}
 			uint32_t nsig = 0, carry = 0;
-			uint64_t next = lane < len ? pcs[start + lane] : 0;
-			for (uint32_t base = 0; base < len; base += 64) {
-				const uint32_t j = base + lane;
-				const bool valid = j < len;
-				const uint64_t pc = next;
-				next = (j + 64 < len) ? pcs[start + j + 64] : 0;  // prefetch the next chunk
-				if (__ballot(valid && !cover_check(pc))) {
-					aborted = true;  // doexit(0): this call and the rest publish nothing
-					done = c - cb;
-					break;
-				}
-				const uint32_t h = exec_hash((uint32_t)pc);
-				const uint32_t up = __shfl_up(h, 1, 64);
-				const uint32_t sig = (uint32_t)pc ^ (lane == 0 ? carry : up);
-				carry = __shfl(h, 63, 64);
-				const uint32_t home = sig & (kDedupSize - 1);
-				const uint32_t b0 = home >> kBinShift, b1 = ((home + 3) & (kDedupSize - 1)) >> kBinShift;
-				bool pending = valid, emit = false;
-				while (__ballot(pending)) {
-					if (epoch == kEpochMax) {
-						for (uint32_t i = lane; i < kBins; i += 64)
-							stamp[i] = 0;
-						epoch = 0;
-						__syncthreads();
-					}
-					epoch++;
-					const uint32_t v = (epoch << 8) | (63 - lane);
-					if (pending) {
-						atomicMax(&stamp[b0], v);
-						if (b1 != b0)
-							atomicMax(&stamp[b1], v);
-					}
-					__syncthreads();
-					bool conflict = false;
-					if (pending) {
-						const uint32_t s0 = stamp[b0], s1 = stamp[b1];
-						conflict = ((s0 >> 8) == epoch && 63 - (s0 & 255) < lane) ||
-						           ((s1 >> 8) == epoch && 63 - (s1 & 255) < lane);
-					}
-					if (pending && !conflict) {
-						// executor.h:692-706, literally
-						bool dup = false, placed = false;
+			const uint32_t nch = (len + 63) / 64;
+			if (len == 0) {  // nothing to load (pcs may even be empty)
+				if (lane == 0)
+					sig_cnt[c] = 0;
+				continue;
+			}
+			// Loads are unconditional (index clamped into the call, value masked
+			// later): a load under a branch makes the compiler drain vmcnt(0)
+			// before the first use, i.e. wait for the whole prefetch.
+			const uint64_t last = start + (len ? len - 1 : 0);
+			uint64_t buf[kEdgeDepth];
 #pragma unroll
-						for (uint32_t i = 0; i < 4; i++) {
-							const uint32_t pos = (sig + i) & (kDedupSize - 1);
-							const uint32_t t = table[pos];
-							if (t == sig) {
-								dup = true;
-								break;
-							}
-							if (t == 0) {
-								table[pos] = sig;
-								placed = true;
-								break;
-							}
-						}
-						if (!dup && !placed)
-							table[home] = sig;
-						emit = !dup;
-						pending = false;
-					}
-					__syncthreads();
+			for (uint32_t u = 0; u < kEdgeDepth; u++)
+				buf[u] = pcs[min<uint64_t>(start + u * 64 + lane, last)];
+			for (uint32_t g = 0; g < nch && !aborted; g += kEdgeDepth) {
+				uint64_t cur[kEdgeDepth];
+#pragma unroll
+				for (uint32_t u = 0; u < kEdgeDepth; u++) {
+					cur[u] = buf[u];
+					buf[u] = pcs[min<uint64_t>(start + (g + kEdgeDepth + u) * 64 + lane, last)];
 				}
-				const uint64_t m = __ballot(emit);
-				if (emit)
-					sigs[start + nsig + lane_rank(m)] = sig;  // write_output order == trace order
-				nsig += (uint32_t)__popcll(m);
+#pragma unroll
+				for (uint32_t u = 0; u < kEdgeDepth; u++) {
+					if (g + u >= nch)
+						break;
+					const uint32_t j = (g + u) * 64 + lane;
+					const bool valid = j < len;
+					const uint64_t pc = valid ? cur[u] : 0;
+					if (__ballot(valid && !cover_check(pc))) {
+						aborted = true;  // doexit(0): this call and the rest publish nothing
+						done = c - cb;
+						break;
+					}
+					const uint32_t h = exec_hash((uint32_t)pc);
+					const uint32_t up = __shfl_up(h, 1, 64);
+					const uint32_t sig = (uint32_t)pc ^ (lane == 0 ? carry : up);
+					carry = __shfl(h, 63, 64);
+					const uint32_t home = sig & (kDedupSize - 1);
+					const uint32_t b0 = home >> kBinShift, b1 = ((home + 3) & (kDedupSize - 1)) >> kBinShift;
+					bool pending = valid, emit = false;
+					while (__ballot(pending)) {
+						// 1. evaluate dedup() (executor.h:692-706, literally) on the current table
+						bool writer = false;
+						uint32_t wpos = home;
+						if (pending) {
+							uint32_t t[4];
+#pragma unroll
+							for (uint32_t i = 0; i < 4; i++)
+								t[i] = table[(sig + i) & (kDedupSize - 1)];
+							bool decided = false;
+#pragma unroll
+							for (uint32_t i = 0; i < 4; i++) {
+								if (!decided && t[i] == sig) {
+									decided = true;  // duplicate
+								} else if (!decided && t[i] == 0) {
+									decided = true;
+									writer = true;
+									wpos = (sig + i) & (kDedupSize - 1);
+								}
+							}
+							writer = writer || !decided;  // all 4 taken: forced overwrite at home
+						}
+						// 2. mark / block until stable
+						if (epoch == kEpochMax) {
+							for (uint32_t i = lane; i < kBins; i += 64)
+								stamp[i] = 0;
+							epoch = 0;
+							wave_lds_sync();
+						}
+						epoch++;
+						const uint32_t v = (epoch << 8) | (63 - lane);
+						bool marker = pending && writer, blocked = false;
+						bool mark_now = marker;
+						for (;;) {
+							if (mark_now) {
+								atomicMax(&stamp[b0], v);
+								if (b1 != b0)
+									atomicMax(&stamp[b1], v);
+							}
+							wave_lds_sync();
+							blocked = pending && (stamp_earlier(stamp[b0], epoch, lane) ||
+							                      stamp_earlier(stamp[b1], epoch, lane));
+							mark_now = blocked && !marker;
+							marker = marker || mark_now;
+							if (!__ballot(mark_now))
+								break;
+						}
+						// 3. final lanes commit
+						if (pending && !blocked) {
+							if (writer)
+								table[wpos] = sig;
+							emit = writer;
+							pending = false;
+						}
+						wave_lds_sync();
+					}
+					const uint64_t m = __ballot(emit);
+					if (emit)
+						sigs[start + nsig + lane_rank(m)] = sig;  // write_output order == trace order
+					nsig += (uint32_t)__popcll(m);
+				}
 			}
 			if (!aborted && lane == 0)
 				sig_cnt[c] = nsig;

@@ -66,16 +66,14 @@ struct syzsig_ctx {
 	unsigned long long* h_cnt = nullptr;  // pinned mirror
 	// grow-only scratch buffers by role: 0-2 set ops, 3-6 triage candidates and
 	// small state, 7-10 host uploads of minimize, 11-14 triage partitions and
-	// minimize internals, 16-19 triage survivors, 24-29 check_new_signal uploads
+	// minimize internals and triage pairs (13-15), 16-23 + 30-31 triage aggregation,
+	// 24-29 check_new_signal uploads
 	syz::Workspace ws[32];
 	bool timing = false;                  // HIP events around triage kernels
 	// tuning knobs (defaults; SYZSIG_* environment overrides read at ctx creation)
-	int part_grid = 1024;                 // blocks of the partitioned probe/decide (multiple of 8)
-	uint64_t part_slice = 4ull << 20;     // bytes of maxSignal per partition
-	int part_mode = 1;                    // 0 = never partition
-	int probe_u = 1;                      // records per lane in flight in the probe filter (1, 2)
-	int probe_drain = 128;                // survivors drained per batch (128, 256)
-	int debug_skip_b = 0;                 // timing-only diagnostics: skip the probe's pass B
+	int part_mode = 1;                    // 0 = never use the aggregation path (agg.hip)
+	uint32_t agg_parts = 0;               // fixed partition count of the aggregation path (0 = adaptive)
+	double agg_distinct_ratio = 0;        // distinct/records of the last aggregated run (sizes the next)
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -93,8 +91,10 @@ struct syzsig_set {
 
 namespace syz {
 
-// scratch buffer `i` of the context, grown to at least `bytes`
+// scratch buffer `i` of the context, grown to at least `bytes` (contents lost on growth)
 int ws_get(syzsig_ctx* ctx, int i, size_t bytes, void** out);
+// same, keeping the first `keep` bytes across a growth
+int ws_grow_keep(syzsig_ctx* ctx, int i, size_t bytes, size_t keep, void** out);
 int counters_reset(syzsig_ctx* ctx);
 int counters_fetch(syzsig_ctx* ctx);  // sync + copy to ctx->h_cnt
 
@@ -115,6 +115,16 @@ struct LevelMap {
 };
 constexpr uint32_t kSerialMask = 0xFFFFFF;  // 24-bit serial index inside a run
 int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm);
+
+// aggregation path (agg.hip)
+uint32_t agg_parts_for(syzsig_ctx* ctx, uint64_t nrec);
+int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,
+                   const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs,
+                   uint64_t* npairs);
+int agg_mark_bits(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const uint64_t* pairs,
+                  uint64_t p0, uint64_t p1);
+int pairs_from_bits(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* bits, uint64_t c0, uint64_t c1,
+                    uint64_t bound, uint64_t** pairs, uint64_t* npairs);
 
 // the default load-factor policy: a table is grown when live/slots exceeds this
 constexpr double kMaxLoad = 0.75;

@@ -43,6 +43,28 @@ int ws_get(syzsig_ctx* ctx, int i, size_t bytes, void** out)
 	return SYZSIG_OK;
 }
 
+int ws_grow_keep(syzsig_ctx* ctx, int i, size_t bytes, size_t keep, void** out)
+{
+	Workspace& w = ctx->ws[i];
+	if (w.size >= bytes) {
+		*out = w.ptr;
+		return SYZSIG_OK;
+	}
+	void* n = nullptr;
+	const size_t want = bytes + bytes / 4 + 4096;
+	SYZ_HIP(hipMalloc(&n, want));
+	if (w.ptr) {
+		if (keep)
+			SYZ_HIP(hipMemcpyAsync(n, w.ptr, std::min(keep, w.size), hipMemcpyDeviceToDevice, ctx->stream));
+		SYZ_HIP(hipStreamSynchronize(ctx->stream));
+		SYZ_HIP(hipFree(w.ptr));
+	}
+	w.ptr = n;
+	w.size = want;
+	*out = n;
+	return SYZSIG_OK;
+}
+
 int counters_reset(syzsig_ctx* ctx)
 {
 	SYZ_HIP(hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * kNumCounters, ctx->stream));
@@ -87,18 +109,10 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 		return syz::hip_fail(e, "ctx_create", __FILE__, __LINE__);
 	}
 	c->stream = c->own_stream;
-	if (const char* v = getenv("SYZSIG_PART_GRID"))
-		c->part_grid = std::max(8, atoi(v) / 8 * 8);
-	if (const char* v = getenv("SYZSIG_PART_SLICE_KB"))
-		c->part_slice = std::max<uint64_t>(64, strtoull(v, nullptr, 10)) << 10;
 	if (const char* v = getenv("SYZSIG_PART_MODE"))
 		c->part_mode = atoi(v);
-	if (const char* v = getenv("SYZSIG_PROBE_U"))
-		c->probe_u = atoi(v);
-	if (const char* v = getenv("SYZSIG_PROBE_DRAIN"))
-		c->probe_drain = atoi(v);
-	if (const char* v = getenv("SYZSIG_DEBUG_SKIP_B"))
-		c->debug_skip_b = atoi(v);
+	if (const char* v = getenv("SYZSIG_AGG_PARTS"))
+		c->agg_parts = (uint32_t)atoi(v);
 	*out = c;
 	return SYZSIG_OK;
 }
@@ -134,6 +148,17 @@ int syzsig_ctx_set_stream(syzsig_ctx* ctx, void* stream)
 }
 
 void* syzsig_ctx_stream(syzsig_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts)
+{
+	if (!ctx)
+		return syz::fail(SYZSIG_EINVAL, "ctx_set_agg: ctx is NULL");
+	if (mode < 0 || mode > 2 || (parts && (parts < 8 || parts > 2048)))
+		return syz::fail(SYZSIG_EINVAL, "ctx_set_agg: mode must be 0..2 and parts 0 or 8..2048");
+	ctx->part_mode = mode;
+	ctx->agg_parts = parts;
+	return SYZSIG_OK;
+}
 
 int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable)
 {

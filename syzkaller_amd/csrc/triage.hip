@@ -53,11 +53,7 @@ __device__ __forceinline__ uint32_t first_at(uint4 f, uint32_t l)
 // are compacted in place inside the segment's own record range.
 //  - CallsIn: segment = one call (prio and serial uniform per segment).
 //  - RecsIn:  segment = 4096 packed records (owner side of a sharded batch).
-//  - PartIn:  the run's records radix-partitioned by table region (2 MB
-//             slices of maxSignal); partition p is processed by the blocks of
-//             XCD p % 8 (blockIdx % 8, round-robin dispatch), partition after
-//             partition, so the slice being probed stays in that XCD's L2.
-//             Placement only affects speed: any block may process any segment.
+// (Large runs take the aggregation path of agg.hip instead.)
 struct Seg {
 	uint64_t start;  // first record
 	uint32_t len;    // records
@@ -133,52 +129,6 @@ struct RecsIn {
 		k = (uint32_t)r & kSerialMask;
 	}
 	__device__ void mark_new(const Seg& g, uint32_t j, uint32_t) const { new_flags[g.start + j] = 1; }
-	__device__ void seg_has_new(uint64_t) const {}
-};
-
-constexpr uint32_t kPartSeg = 1024;  // records per segment in partitioned mode
-
-struct PartIn {
-	const uint64_t* recs;      // packed elem << 32 | level << 24 | serial, grouped by partition
-	const uint32_t* orig;      // record index in the caller's sigs[] (for the new bit)
-	const uint64_t* rec_base;  // nparts + 1
-	const uint64_t* seg_base;  // nparts + 1
-	uint32_t nparts;           // multiple of 8
-	uint64_t c0;
-	uint32_t* new_bits;
-	uint8_t* call_new;
-
-	template <typename F>
-	__device__ void for_each_segment(const LevelMap&, F f) const
-	{
-		const uint32_t x = blockIdx.x & 7, i = blockIdx.x >> 3, nbx = gridDim.x >> 3;
-		const uint32_t w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
-		for (uint32_t p = x; p < nparts; p += 8) {
-			const uint64_t base = rec_base[p], n = rec_base[p + 1] - base;
-			const uint64_t nseg = (n + kPartSeg - 1) / kPartSeg, sb = seg_base[p];
-			for (uint64_t s = (uint64_t)i * wpb + w; s < nseg; s += (uint64_t)nbx * wpb) {
-				Seg g;
-				g.start = base + s * kPartSeg;
-				g.len = (uint32_t)min<uint64_t>(kPartSeg, n - s * kPartSeg);
-				g.ok = true;
-				g.level = 0;
-				g.serial = 0;
-				f(sb + s, g);
-			}
-		}
-	}
-	__device__ void rec(const Seg& g, uint32_t j, uint32_t& e, uint32_t& l, uint32_t& k) const
-	{
-		const uint64_t r = __builtin_nontemporal_load(&recs[g.start + j]);
-		e = (uint32_t)(r >> 32);
-		l = (uint32_t)(r >> 24) & 0xff;
-		k = (uint32_t)r & kSerialMask;
-	}
-	__device__ void mark_new(const Seg& g, uint32_t j, uint32_t k) const
-	{
-		set_bit(new_bits, orig[g.start + j]);
-		call_new[c0 + k] = 1;
-	}
 	__device__ void seg_has_new(uint64_t) const {}
 };
 
@@ -446,217 +396,6 @@ __global__ __launch_bounds__(256) void k_decide(uint64_t* slots, const uint32_t*
 	block_count(&cnt[kCntOverflow], ovf);
 }
 
-// ---------------------------------------------------------------- partitioning
-// Records of calls [c0, c1) -> packed records grouped by table region
-// (partition = home bucket >> shift).  Block b owns the chunk of calls
-// [b*kPartCPB, (b+1)*kPartCPB); its slice of every partition is fixed by a
-// scan of the per-(chunk, partition) counts, so the scatter needs no global
-// atomics.  The scatter stages kTile records in LDS, sorts them by partition
-// (counting sort) and writes each partition's run contiguously.
-constexpr uint32_t kPartCPB = 128;
-constexpr uint32_t kMaxParts = 1024;
-constexpr uint32_t kTile = 2048;
-
-__device__ __forceinline__ uint32_t part_of(uint32_t e, uint64_t bmask, uint32_t shift)
-{
-	return (uint32_t)((fmix32(e) & bmask) >> shift);
-}
-
-__global__ __launch_bounds__(256) void k_part_count(CallsIn in, uint64_t bmask, uint32_t shift, uint32_t nparts,
-                                                    uint32_t* counts)
-{
-	__shared__ uint32_t h[kMaxParts];
-	const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = lane_id();
-	const uint64_t ncalls = in.c1 - in.c0, nchunks = (ncalls + kPartCPB - 1) / kPartCPB;
-	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-		for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
-			h[i] = 0;
-		__syncthreads();
-		const uint64_t ce = min<uint64_t>(ncalls, (ch + 1) * kPartCPB);
-		for (uint64_t s = ch * kPartCPB + w; s < ce; s += nw) {
-			const uint64_t c = in.c0 + s, start = in.call_start[c];
-			const uint32_t len = in.call_len[c];
-			for (uint32_t j = lane; j < len; j += 64)
-				atomicAdd(&h[part_of(in.sigs[start + j], bmask, shift)], 1u);
-		}
-		__syncthreads();
-		for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
-			counts[ch * nparts + i] = h[i];
-		__syncthreads();
-	}
-}
-
-// exclusive scan of v over the block (256 threads); returns the block total
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* out)
-{
-	__shared__ uint32_t wsum[4];
-	const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
-	uint32_t x = v;
-#pragma unroll
-	for (int o = 1; o < 64; o <<= 1) {
-		const uint32_t y = __shfl_up(x, o, 64);
-		if (lane >= (uint32_t)o)
-			x += y;
-	}
-	if (lane == 63)
-		wsum[w] = x;
-	__syncthreads();
-	uint32_t pre = 0, tot = 0;
-	for (uint32_t i = 0; i < 4; i++) {
-		pre += i < w ? wsum[i] : 0;
-		tot += wsum[i];
-	}
-	__syncthreads();
-	*out = pre + x - v;
-	return tot;
-}
-
-// block p: exclusive scan over chunks of counts[.][p] -> offs[.][p]; totals[p]
-__global__ __launch_bounds__(256) void k_part_scan_chunks(const uint32_t* counts, uint64_t nchunks, uint32_t nparts,
-                                                          uint32_t* offs, uint64_t* totals)
-{
-	const uint32_t p = blockIdx.x;
-	uint64_t run = 0;
-	for (uint64_t b0 = 0; b0 < nchunks; b0 += blockDim.x) {
-		const uint64_t b = b0 + threadIdx.x;
-		const uint32_t v = b < nchunks ? counts[b * nparts + p] : 0;
-		uint32_t ex;
-		const uint32_t tot = block_excl_scan(v, &ex);
-		if (b < nchunks)
-			offs[b * nparts + p] = (uint32_t)(run + ex);
-		run += tot;
-	}
-	if (threadIdx.x == 0)
-		totals[p] = run;
-}
-
-// totals -> rec_base / seg_base
-__global__ void k_part_scan(const uint64_t* totals, uint32_t nparts, uint64_t* rec_base, uint64_t* seg_base)
-{
-	if (threadIdx.x != 0 || blockIdx.x != 0)
-		return;
-	uint64_t r = 0, sg = 0;
-	for (uint32_t p = 0; p < nparts; p++) {
-		rec_base[p] = r;
-		seg_base[p] = sg;
-		r += totals[p];
-		sg += (totals[p] + kPartSeg - 1) / kPartSeg;
-	}
-	rec_base[nparts] = r;
-	seg_base[nparts] = sg;
-}
-
-__global__ __launch_bounds__(256) void k_part_scatter(CallsIn in, LevelMap lm, uint64_t bmask, uint32_t shift,
-                                                      uint32_t nparts, const uint32_t* __restrict__ offs,
-                                                      const uint64_t* __restrict__ rec_base, uint64_t* recs,
-                                                      uint32_t* orig)
-{
-	__shared__ uint64_t t_rec[kTile], s_rec[kTile];
-	__shared__ uint32_t t_orig[kTile], s_orig[kTile];
-	__shared__ uint16_t t_part[kTile], s_part[kTile];
-	__shared__ uint32_t cur[kMaxParts], hist[kMaxParts], bin[kMaxParts], pos[kMaxParts];
-	__shared__ uint32_t tile_n, more;
-	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-	const uint64_t ncalls = in.c1 - in.c0, nchunks = (ncalls + kPartCPB - 1) / kPartCPB;
-	const uint32_t per_t = (nparts + blockDim.x - 1) / blockDim.x;  // bins per thread in the scan
-	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-		const uint64_t cb = ch * kPartCPB, ce = min<uint64_t>(ncalls, cb + kPartCPB);
-		for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
-			cur[i] = offs[ch * nparts + i];
-		// per-wave cursor: call cb + w, +4, ...; offset inside the call
-		uint64_t wc = cb + w;
-		uint32_t wo = 0;
-		for (;;) {
-			for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
-				hist[i] = 0;
-			if (threadIdx.x == 0) {
-				tile_n = 0;
-				more = 0;
-			}
-			__syncthreads();
-			// fill: each wave contributes up to kTile/4 records
-			uint32_t quota = kTile / 4;
-			while (quota && wc < ce) {
-				const uint64_t c = in.c0 + wc, start = in.call_start[c];
-				const uint32_t len = in.call_len[c];
-				const uint32_t m = min(quota, len - wo);
-				uint32_t tb = 0;
-				if (lane == 0 && m)
-					tb = atomicAdd(&tile_n, m);
-				tb = __shfl(tb, 0, 64);
-				const uint64_t head = ((uint64_t)lm.lvl[in.call_prio[c]] << 24) | (wc & kSerialMask);
-				// all loads of this piece first (independent, in flight together)
-				uint32_t ev[kTile / 4 / 64];
-#pragma unroll
-				for (uint32_t u = 0; u < kTile / 4 / 64; u++) {
-					const uint32_t i = u * 64 + lane;
-					ev[u] = i < m ? in.sigs[start + wo + i] : 0;
-				}
-#pragma unroll
-				for (uint32_t u = 0; u < kTile / 4 / 64; u++) {
-					const uint32_t i = u * 64 + lane;
-					if (i < m) {
-						const uint32_t p = part_of(ev[u], bmask, shift);
-						t_rec[tb + i] = ((uint64_t)ev[u] << 32) | head;
-						t_orig[tb + i] = (uint32_t)(start + wo + i);
-						t_part[tb + i] = (uint16_t)p;
-						atomicAdd(&hist[p], 1u);
-					}
-				}
-				quota -= m;
-				wo += m;
-				if (wo == len) {
-					wc += 4;
-					wo = 0;
-				}
-			}
-			if (lane == 0 && wc < ce)
-				atomicOr(&more, 1u);
-			__syncthreads();
-			const uint32_t n = tile_n;
-			// exclusive scan of hist -> bin (per_t consecutive bins per thread)
-			uint32_t loc = 0;
-			for (uint32_t q = 0; q < per_t; q++) {
-				const uint32_t i = threadIdx.x * per_t + q;
-				loc += i < nparts ? hist[i] : 0;
-			}
-			uint32_t ex;
-			block_excl_scan(loc, &ex);
-			for (uint32_t q = 0; q < per_t; q++) {
-				const uint32_t i = threadIdx.x * per_t + q;
-				if (i < nparts) {
-					bin[i] = ex;
-					pos[i] = ex;
-					ex += hist[i];
-				}
-			}
-			__syncthreads();
-			for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-				const uint32_t p = t_part[i];
-				const uint32_t d = atomicAdd(&pos[p], 1u);
-				s_rec[d] = t_rec[i];
-				s_orig[d] = t_orig[i];
-				s_part[d] = (uint16_t)p;
-			}
-			__syncthreads();
-			// consecutive threads write consecutive records of one partition run
-			for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-				const uint32_t p = s_part[i];
-				const uint64_t g = rec_base[p] + cur[p] + (i - bin[p]);
-				recs[g] = s_rec[i];
-				orig[g] = s_orig[i];
-			}
-			__syncthreads();
-			for (uint32_t i = threadIdx.x; i < nparts; i += blockDim.x)
-				cur[i] += hist[i];
-			const bool again = more != 0;
-			__syncthreads();
-			if (!again)
-				break;
-		}
-	}
-}
-
 // prio presence over calls -> 256-bit mask (block-local, one atomic per word
 // per block), plus the number of records (sum of call_len)
 __global__ void k_prio_presence(const uint8_t* __restrict__ prio, const uint32_t* __restrict__ len,
@@ -765,25 +504,12 @@ static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* r
 // One run (<= 4 prio levels): probe, then decide+commit.  On capacity
 // overflow the run's only table side effects -- absent markers -- are dropped
 // by a rehash into a bigger table and the run restarts.
-// probe variants: records per lane in flight (probe_u) x survivors drained per batch
 template <typename In>
 static void launch_probe(syzsig_ctx* ctx, int grid, syzsig_set* ms, const In& in, const LevelMap& lm,
                          uint32_t* cand_slot, uint32_t* cand_meta, uint32_t* cand_cnt)
 {
-#define SYZ_PROBE(U, D)                                                                                     \
-	k_probe<In, U, D><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in, lm, \
-	                                                 ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt,         \
-	                                                 ctx->debug_skip_b)
-	const bool u2 = ctx->probe_u == 2, d2 = ctx->probe_drain == 128;
-	if (u2 && d2)
-		SYZ_PROBE(2, 128);
-	else if (u2)
-		SYZ_PROBE(2, 256);
-	else if (d2)
-		SYZ_PROBE(1, 128);
-	else
-		SYZ_PROBE(1, 256);
-#undef SYZ_PROBE
+	k_probe<In, 1, 128><<<grid, 256, 0, ctx->stream>>>(ms->slots, ms->nbuckets - 1, ms->firsts, ms->touched, in, lm,
+	                                                   ms->epoch, cand_slot, cand_meta, cand_cnt, ctx->d_cnt, 0);
 }
 
 // `prep(&in, &grid)` builds the kernels' input for the table's current
@@ -857,39 +583,24 @@ static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, Prep pre
 	}
 }
 
-// Partitioned mode pays off once maxSignal no longer fits the L2s and the
-// run is large; it needs record indices < 2^32.
-static uint32_t parts_for(const syzsig_set* ms, uint64_t nrecs, uint64_t nrec_space)
+// The aggregation path (agg.hip) pays off once a run is large: one maxSignal
+// probe per distinct element instead of one per record.
+static bool use_agg(const syzsig_ctx* ctx, uint64_t run_recs, uint64_t nrec_space)
 {
-	const syzsig_ctx* ctx = ms->ctx;
-	const uint64_t bytes = ms->nslots() * 8;
-	if (!ctx->part_mode || bytes < (32ull << 20) || nrecs < (1ull << 20) || nrec_space >= (1ull << 32))
-		return 0;
-	uint32_t parts = 8;
-	while (parts < kMaxParts && bytes / parts > ctx->part_slice && parts < ms->nbuckets)
-		parts <<= 1;
-	return parts;
-}
-
-static uint32_t log2u(uint64_t x)
-{
-	uint32_t r = 0;
-	while ((1ull << r) < x)
-		r++;
-	return r;
+	return nrec_space < (1ull << 32) && (ctx->part_mode == 2 || (ctx->part_mode == 1 && run_recs >= (1ull << 20)));
 }
 
 int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b,
                       syzsig_batch_stats* st)
 {
-	SYZ_HIP(hipMemsetAsync(b->new_bits, 0, ((b->nrec + 31) / 32) * 4, ctx->stream));
+	if (b->new_bits)
+		SYZ_HIP(hipMemsetAsync(b->new_bits, 0, ((b->nrec + 31) / 32) * 4, ctx->stream));
 	if (b->ncalls)
 		SYZ_HIP(hipMemsetAsync(b->call_new, 0, b->ncalls, ctx->stream));
 	if (b->ncalls == 0 || b->nrec == 0) {
 		SYZ_HIP(hipStreamSynchronize(ctx->stream));
 		return SYZSIG_OK;
 	}
-	SYZ_TRY(set_ensure_triage_state(ms));
 	std::vector<Run> runs;
 	uint64_t total = 0;
 	SYZ_TRY(plan_runs(ctx, b, &runs, &total));
@@ -897,7 +608,25 @@ int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const sy
 	uint64_t maxrun = 0;
 	for (auto& r : runs)
 		maxrun = std::max(maxrun, r.c1 - r.c0);
+	uint64_t* pairs = nullptr;
+	uint64_t npairs = 0;
 	for (auto& r : runs) {
+		const uint64_t run_recs = runs.size() == 1 ? total : b->nrec;  // bound
+		if (use_agg(ctx, run_recs, b->nrec)) {
+			const uint64_t p0 = npairs;
+			SYZ_TRY(agg_triage_run(ctx, ms, ns, b, r.c0, r.c1, r.lm, run_recs, st, &pairs, &npairs));
+			SYZ_TRY(agg_mark_bits(ctx, b, r.c0, r.c1, pairs, p0, npairs));
+			continue;
+		}
+		// per-call path: probe + decide against maxSignal, per-record bits
+		SYZ_TRY(set_ensure_triage_state(ms));
+		uint32_t* bits = b->new_bits;
+		if (!bits) {
+			void* ib;
+			SYZ_TRY(ws_get(ctx, 12, ((b->nrec + 31) / 32) * 4 + 64, &ib));
+			bits = (uint32_t*)ib;
+			SYZ_HIP(hipMemsetAsync(bits, 0, ((b->nrec + 31) / 32) * 4, ctx->stream));
+		}
 		CallsIn in;
 		in.sigs = b->sigs;
 		in.call_start = b->call_start;
@@ -906,76 +635,28 @@ int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const sy
 		in.c0 = r.c0;
 		in.c1 = r.c1;
 		in.nrec = b->nrec;
-		in.new_bits = b->new_bits;
+		in.new_bits = bits;
 		in.call_new = b->call_new;
-		const uint64_t run_recs = runs.size() == 1 ? total : b->nrec;  // bound
-		if (parts_for(ms, run_recs, b->nrec)) {
-			// ---- partitioned: records regrouped by table region, one XCD per region
-			void *cs, *cm, *cc, *pr, *po, *pm, *pc;
-			const uint64_t nseg_max = run_recs / kPartSeg + kMaxParts + 1;
-			const uint64_t nchunks = (r.c1 - r.c0 + kPartCPB - 1) / kPartCPB;
-			SYZ_TRY(ws_get(ctx, 3, run_recs * 4 + 64, &cs));
-			SYZ_TRY(ws_get(ctx, 4, run_recs * 4 + 64, &cm));
-			SYZ_TRY(ws_get(ctx, 5, nseg_max * 4, &cc));
-			SYZ_TRY(ws_get(ctx, 11, run_recs * 8 + 64, &pr));
-			SYZ_TRY(ws_get(ctx, 12, run_recs * 4 + 64, &po));
-			SYZ_TRY(ws_get(ctx, 13, (kMaxParts + 1) * 8 * 3, &pm));
-			SYZ_TRY(ws_get(ctx, 14, nchunks * kMaxParts * 4 * 2 + 64, &pc));
-			uint64_t* totals = (uint64_t*)pm;
-			uint64_t* rec_base = totals + kMaxParts + 1;
-			uint64_t* seg_base = rec_base + kMaxParts + 1;
-			auto prep = [&](PartIn* pin, int* grid, syzsig_batch_stats* stp) -> int {
-				const uint32_t parts = parts_for(ms, run_recs, b->nrec);
-				if (!parts)
-					return fail(SYZSIG_EIO, "partitioned triage lost its geometry (internal error)");
-				const uint32_t shift = log2u(ms->nbuckets) - log2u(parts);
-				uint32_t* counts = (uint32_t*)pc;
-				uint32_t* offs = counts + nchunks * parts;
-				if (ctx->timing)
-					SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
-				const int pg = (int)std::min<uint64_t>(nchunks, 4096);
-				k_part_count<<<pg, 256, 0, ctx->stream>>>(in, ms->nbuckets - 1, shift, parts, counts);
-				k_part_scan_chunks<<<parts, 256, 0, ctx->stream>>>(counts, nchunks, parts, offs, totals);
-				k_part_scan<<<1, 64, 0, ctx->stream>>>(totals, parts, rec_base, seg_base);
-				k_part_scatter<<<pg, 256, 0, ctx->stream>>>(in, r.lm, ms->nbuckets - 1, shift, parts, offs, rec_base,
-				                                            (uint64_t*)pr, (uint32_t*)po);
-				SYZ_HIP(hipGetLastError());
-				if (ctx->timing) {
-					float t = 0;
-					SYZ_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
-					SYZ_HIP(hipEventSynchronize(ctx->ev[1]));
-					SYZ_HIP(hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]));
-					stp->part_ms += t;
-				}
-				pin->recs = (const uint64_t*)pr;
-				pin->orig = (const uint32_t*)po;
-				pin->rec_base = rec_base;
-				pin->seg_base = seg_base;
-				pin->nparts = parts;
-				stp->parts = parts;
-				pin->c0 = r.c0;
-				pin->new_bits = b->new_bits;
-				pin->call_new = b->call_new;
-				*grid = ctx->part_grid;  // multiple of 8: block b works on XCD b % 8's partitions
-				return SYZSIG_OK;
-			};
-			SYZ_TRY(triage_run<PartIn>(ctx, ms, ns, prep, r.lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
-		} else {
-			void *cs, *cm, *cc;
-			SYZ_TRY(ws_get(ctx, 3, b->nrec * 4, &cs));
-			SYZ_TRY(ws_get(ctx, 4, b->nrec * 4, &cm));
-			SYZ_TRY(ws_get(ctx, 5, maxrun * 4, &cc));
-			auto prep = [&](CallsIn* cin, int* grid, syzsig_batch_stats*) -> int {
-				*cin = in;
-				*grid = grid_for((r.c1 - r.c0) * 64, 256, 4096);
-				return SYZSIG_OK;
-			};
-			SYZ_TRY(triage_run<CallsIn>(ctx, ms, ns, prep, r.lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
-		}
+		void *cs, *cm, *cc;
+		SYZ_TRY(ws_get(ctx, 3, b->nrec * 4, &cs));
+		SYZ_TRY(ws_get(ctx, 4, b->nrec * 4, &cm));
+		SYZ_TRY(ws_get(ctx, 5, maxrun * 4, &cc));
+		auto prep = [&](CallsIn* cin, int* grid, syzsig_batch_stats*) -> int {
+			*cin = in;
+			*grid = grid_for((r.c1 - r.c0) * 64, 256, 4096);
+			return SYZSIG_OK;
+		};
+		SYZ_TRY(triage_run<CallsIn>(ctx, ms, ns, prep, r.lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
+		SYZ_TRY(pairs_from_bits(ctx, b, bits, r.c0, r.c1, run_recs, &pairs, &npairs));
 	}
 	if ((double)ms->len > kMaxLoad * (double)ms->nslots())
 		SYZ_TRY(set_rehash(ms, buckets_for(ms->len), false));
 	st->new_signal_len = syzsig_len(*ns);
+	st->new_pairs = npairs;
+	if (b->new_pairs && npairs)
+		SYZ_HIP(hipMemcpyAsync(b->new_pairs, pairs, std::min(npairs, b->new_pairs_cap) * 8, hipMemcpyDeviceToDevice,
+		                       ctx->stream));
+	SYZ_HIP(hipStreamSynchronize(ctx->stream));
 	return SYZSIG_OK;
 }
 
@@ -1036,8 +717,10 @@ int syzsig_triage_batch(syzsig_ctx* ctx, syzsig_set* max_signal, syzsig_set** ne
 		return fail(SYZSIG_EINVAL, "triage_batch: NULL argument");
 	if (*new_signal == max_signal)
 		return fail(SYZSIG_EINVAL, "triage_batch: new_signal aliases max_signal");
-	if (b->nrec && (!b->sigs || !b->new_bits))
+	if (b->nrec && !b->sigs)
 		return fail(SYZSIG_EINVAL, "triage_batch: NULL record arrays");
+	if (b->new_pairs_cap && !b->new_pairs)
+		return fail(SYZSIG_EINVAL, "triage_batch: new_pairs_cap without new_pairs");
 	if (b->ncalls && (!b->call_start || !b->call_len || !b->call_prio || !b->call_new))
 		return fail(SYZSIG_EINVAL, "triage_batch: NULL call arrays");
 	syzsig_batch_stats st;
@@ -1086,6 +769,8 @@ int syzsig_check_new_signal(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set
 	b.nrec = nrec;
 	b.new_bits = (uint32_t*)dbits;
 	b.call_new = (uint8_t*)dnew;
+	b.new_pairs = nullptr;
+	b.new_pairs_cap = 0;
 	syzsig_batch_stats st;
 	memset(&st, 0, sizeof(st));
 	SYZ_TRY(triage_batch_impl(ctx, *max_signal, new_signal, &b, &st));

@@ -63,29 +63,41 @@ class Device:
         return Signal(h, self.eng)
 
     # ---------------------------------------------------------------- K3
-    def batch(self, sigs, call_start, call_len, call_prio, new_bits=None, call_new=None):
-        self._check_dev(sigs, call_start, call_len, call_prio, new_bits, call_new)
+    def batch(self, sigs, call_start, call_len, call_prio, new_bits=None, call_new=None, new_pairs=None,
+              want_bits=True):
+        """A syzsig_batch over device tensors.  new_bits is allocated when
+        want_bits (else NULL: not computed); new_pairs (int64) is optional."""
+        self._check_dev(sigs, call_start, call_len, call_prio, new_bits, call_new, new_pairs)
         nrec, ncalls = sigs.numel(), call_len.numel()
-        if new_bits is None:
+        if new_bits is None and want_bits:
             new_bits = torch.empty((nrec + 31) // 32, dtype=torch.int32, device=self.dev)
         if call_new is None:
             call_new = torch.empty(ncalls, dtype=torch.uint8, device=self.dev)
         b = Batch(sigs=_p(sigs).value, call_start=_p(call_start).value, call_len=_p(call_len).value,
                   call_prio=_p(call_prio).value, ncalls=ncalls, nrec=nrec, new_bits=_p(new_bits).value,
-                  call_new=_p(call_new).value)
+                  call_new=_p(call_new).value, new_pairs=_p(new_pairs).value,
+                  new_pairs_cap=0 if new_pairs is None else new_pairs.numel())
         return b, new_bits, call_new
 
-    def triage(self, max_signal, new_signal, sigs, call_start, call_len, call_prio, new_bits=None, call_new=None):
+    def triage(self, max_signal, new_signal, sigs, call_start, call_len, call_prio, new_bits=None, call_new=None,
+               new_pairs=None, want_bits=True):
         """checkNewSignal over a whole batch (syz-fuzzer/fuzzer.go:494-511).
-        Returns (new_bits int32[ceil(nrec/32)], call_new uint8[ncalls], stats)."""
-        b, new_bits, call_new = self.batch(sigs, call_start, call_len, call_prio, new_bits, call_new)
+        Returns (new_bits int32[ceil(nrec/32)] or None, call_new uint8[ncalls], stats);
+        stats["new_pairs"] = number of (call << 32 | elem) DiffRaw entries, the
+        first min(that, new_pairs.numel()) of which are written to new_pairs."""
+        b, new_bits, call_new = self.batch(sigs, call_start, call_len, call_prio, new_bits, call_new, new_pairs,
+                                           want_bits)
+        return new_bits, call_new, self.triage_b(max_signal, new_signal, b)
+
+    def triage_b(self, max_signal, new_signal, b):
+        """syzsig_triage_batch on a prepared Batch; returns the stats dict."""
         st = BatchStats()
         nh = ctypes.c_void_p(new_signal.handle.value or 0)
         check(self.L.syzsig_triage_batch(self.eng.h, max_signal.handle, ctypes.byref(nh), ctypes.byref(b),
                                          ctypes.byref(st)))
         if nh.value and new_signal.is_nil():
             new_signal._h = nh
-        return new_bits, call_new, st.as_dict()
+        return st.as_dict()
 
     # ---------------------------------------------------------------- K1+K2
     def edge_derive(self, pcs, call_start, call_len, prog_call, sigs=None, sig_cnt=None, completed=None):

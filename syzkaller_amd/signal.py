@@ -37,6 +37,10 @@ class Engine:
     def set_stream(self, stream_handle):
         check(self.L.syzsig_ctx_set_stream(self.h, ctypes.c_void_p(stream_handle)))
 
+    def set_agg(self, mode=1, parts=0):
+        """Large-batch triage path: 0 per-call, 1 auto (default), 2 aggregation always."""
+        check(self.L.syzsig_ctx_set_agg(self.h, int(mode), int(parts)))
+
     def close(self):
         if self.h:
             self.L.syzsig_ctx_destroy(self.h)
@@ -77,7 +81,9 @@ class Signal:
     # -- ownership
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None
-        if h is not None:
+        # at interpreter shutdown the engine may be finalized first (cycles from
+        # tracebacks): its context -- and every set's memory with it -- is gone then
+        if h is not None and getattr(getattr(self, "_e", None), "h", None):
             try:
                 self._e.L.syzsig_set_free(h)
             except Exception:

@@ -35,7 +35,16 @@ def dev_batch(gpu, cfg, nprog, cpp, call_len, prog_base=0):
     return sigs, cs, cnt, prio
 
 
-def compare(gpu, m0, hb, db, new0=None, ms_hint=None):
+def oracle_pairs(hs, hcs, hcnt, obits):
+    """Every call's DiffRaw result as sorted unique (call << 32 | elem)."""
+    r = np.nonzero(np.unpackbits(obits.view(np.uint8), bitorder="little"))[0].astype(np.uint64)
+    ends = hcs.astype(np.uint64) + hcnt.astype(np.uint64)
+    call = np.searchsorted(ends, r, side="right").astype(np.uint64)
+    return np.unique((call << np.uint64(32)) | hs[r].astype(np.uint64))
+
+
+def compare(gpu, m0, hb, db, new0=None, ms_hint=None, agg=1, parts=0):
+    """agg: 0 = per-call path, 1 = auto, 2 = aggregation path (parts fixed if > 0)."""
     from syzkaller_amd import signal as S
 
     hs, hcs, hcnt, hprio = hb
@@ -44,10 +53,18 @@ def compare(gpu, m0, hb, db, new0=None, ms_hint=None):
     np.testing.assert_array_equal(_u(dprio, np.uint8), hprio)
     ms = S.Serial(*m0).Deserialize(gpu.eng) if m0[0].size else S.Signal.make(ms_hint or 0, gpu.eng)
     ns = S.Serial(*new0).Deserialize(gpu.eng) if new0 is not None else S.Signal(None, gpu.eng)
-    bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
+    pairs = torch.full((int(hcnt.sum()) + 1,), -1, dtype=torch.int64, device=gpu.dev)
+    gpu.eng.set_agg(agg, parts)
+    try:
+        bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio, new_pairs=pairs)
+    finally:
+        gpu.eng.set_agg(1, 0)
     oms, ons, obits, ocnew = O.triage_batch(m0[0], m0[1], hs, hcs, hcnt, hprio, new0)
     np.testing.assert_array_equal(_u(cnew, np.uint8), ocnew)
     np.testing.assert_array_equal(_u(bits, np.uint32), obits)
+    op = oracle_pairs(hs, hcs, hcnt, obits)
+    assert st["new_pairs"] == op.size
+    np.testing.assert_array_equal(np.sort(_u(pairs[: op.size], np.uint64)), op)
     assert ms.Len() == oms.Len()
     assert ms.to_dict() == oms.to_dict()
     assert (ns.to_dict() if not ns.is_nil() else {}) == ons.to_dict()
@@ -55,47 +72,78 @@ def compare(gpu, m0, hb, db, new0=None, ms_hint=None):
     return st
 
 
+@pytest.mark.parametrize("agg", [0, 2])
 @pytest.mark.parametrize("over,known,nm0", [({}, 2048, 200000), ({"skew": 1}, 1024, 100000),
                                              ({"region_log2": 11}, 4096, 300000), ({}, 0, 0)])
-def test_triage_c1_vs_oracle(gpu, over, known, nm0):
-    """Config 1: 64 programs x 32 calls x 2k PCs, through K1+K2+K3."""
+def test_triage_c1_vs_oracle(gpu, over, known, nm0, agg):
+    """Config 1: 64 programs x 32 calls x 2k PCs, through K1+K2+K3, on the
+    per-call path (agg=0) and the LDS aggregation path (agg=2)."""
     from syzkaller_amd import synth
 
     cfg = synth.synth_default(**over)
     nprog, cpp = 64, 32
     cl = synth.call_lengths(nprog, cpp, 2048)
     m0 = synth.m0(cfg, known, nm0)
-    st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl))
-    assert st["candidates"] > 0 and st["runs"] == 1 and st["parts"] == 0
+    st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl), agg=agg)
+    assert st["candidates"] > 0 and st["runs"] == 1
+    assert (st["parts"] > 0) == (agg == 2)
 
 
 @pytest.mark.parametrize("skew", [0, 1])
-def test_triage_partitioned_vs_oracle(gpu, skew):
-    """A maxSignal big enough (5M elements, 134 MB table) and a batch big enough
-    (64 x 32 x 2k) to take the partitioned (table-region per XCD) path."""
+def test_triage_agg_auto_vs_oracle(gpu, skew):
+    """A 5M-element maxSignal and a batch big enough (128 x 32 x 2k) to take
+    the aggregation path by itself."""
     from syzkaller_amd import synth
 
     cfg = synth.synth_default(skew=skew)
-    nprog, cpp = 64, 32
+    nprog, cpp = 128, 32
     cl = synth.call_lengths(nprog, cpp, 2048)
     m0 = synth.m0(cfg, 2048, 5_000_000)
     st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl))
-    assert st["parts"] >= 8, st
+    assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
 
 
-def test_triage_overflow_retry(gpu):
-    """maxSignal starts as make(Signal) with 16 slots: phase 1 overflows and the
-    run restarts on bigger tables; results must not change."""
+@pytest.mark.parametrize("frac", [0.3, 1.0, 100.0])
+def test_triage_agg_lds_overflow_fallback(gpu, frac):
+    """Partitions whose distinct elements do not fit the LDS table are redone in
+    the HBM table: none (frac 0.3 of the limit), about half (1.0), all (100)."""
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default(region_log2=11)
+    nprog, cpp = 64, 32
+    cl = synth.call_lengths(nprog, cpp, 2048)
+    hb = host_batch(cfg, nprog, cpp, cl)
+    hs, hcs, hcnt, _ = hb
+    idx = np.concatenate([np.arange(a, a + n) for a, n in zip(hcs.astype(np.int64), hcnt.astype(np.int64))])
+    distinct = np.unique(hs[idx]).size
+    parts = int(min(2048, max(8, round(distinct / (6348 * frac) / 8) * 8)))
+    m0 = synth.m0(cfg, 2048, 100000)
+    st = compare(gpu, m0, hb, dev_batch(gpu, cfg, nprog, cpp, cl), agg=2, parts=parts)
+    assert st["parts"] == parts and st["distinct"] == distinct
+    if frac < 1:
+        assert st["overflow_parts"] == 0, st
+    elif frac > 10:
+        assert st["overflow_parts"] == parts, st
+    else:
+        assert 0 < st["overflow_parts"] < parts, st
+
+
+@pytest.mark.parametrize("agg", [0, 2])
+def test_triage_overflow_retry(gpu, agg):
+    """maxSignal starts as make(Signal) with 16 slots: the per-call path
+    overflows and restarts on bigger tables, the aggregation path reserves from
+    its distinct count; results must not change."""
     from syzkaller_amd import synth
 
     cfg = synth.synth_default()
     cl = synth.call_lengths(32, 16, 0, ragged=(0, 3000), seed=3)
     m0 = (np.empty(0, np.uint32), np.empty(0, np.int8))
-    st = compare(gpu, m0, host_batch(cfg, 32, 16, cl), dev_batch(gpu, cfg, 32, 16, cl), ms_hint=0)
-    assert st["retries"] > 0
+    st = compare(gpu, m0, host_batch(cfg, 32, 16, cl), dev_batch(gpu, cfg, 32, 16, cl), ms_hint=0, agg=agg)
+    assert st["retries"] > 0 or agg == 2
 
 
-def test_triage_many_prios_and_existing_new_signal(gpu):
+@pytest.mark.parametrize("agg", [0, 2])
+def test_triage_many_prios_and_existing_new_signal(gpu, agg):
     """Arbitrary uint8 prios (int8 order, > 4 distinct -> several runs) and a
     non-empty newSignal before the batch."""
     from syzkaller_amd import synth
@@ -109,13 +157,16 @@ def test_triage_many_prios_and_existing_new_signal(gpu):
     prio = rng.choice(np.array([0, 1, 2, 3, 7, 127, 128, 200, 255], np.uint8), size=nprog * cpp)
     m0 = synth.m0(cfg, 512, 50000)
     new0 = synth.m0(cfg, 0, 1000)
-    st = compare(gpu, m0, (hs, hcs, hcnt, prio), (ds, dcs, dcnt, torch.from_numpy(prio).to(gpu.dev)), new0=new0)
+    st = compare(gpu, m0, (hs, hcs, hcnt, prio), (ds, dcs, dcnt, torch.from_numpy(prio).to(gpu.dev)), new0=new0,
+                 agg=agg)
     assert st["runs"] > 1
 
 
-def test_triage_empty_and_degenerate(gpu):
+@pytest.mark.parametrize("agg", [0, 2])
+def test_triage_empty_and_degenerate(gpu, agg):
     from syzkaller_amd import signal as S
 
+    gpu.eng.set_agg(agg, 0)
     ms = S.Signal.make(0, gpu.eng)
     ns = S.Signal(None, gpu.eng)
     z = lambda n, dt: torch.zeros(n, dtype=dt, device=gpu.dev)  # noqa: E731
@@ -124,6 +175,18 @@ def test_triage_empty_and_degenerate(gpu):
     # calls that are all empty
     bits, cnew, st = gpu.triage(ms, ns, z(4, torch.int32), z(3, torch.int64), z(3, torch.int32), z(3, torch.uint8))
     assert int(cnew.sum()) == 0 and ns.is_nil()
+    # only element 0xFFFFFFFF (the LDS table's special slot) and element 0
+    sigs = torch.tensor([-1, 0, -1, 0, 5], dtype=torch.int32, device=gpu.dev)
+    cs = torch.tensor([0, 2, 4], dtype=torch.int64, device=gpu.dev)
+    cl = torch.tensor([2, 2, 1], dtype=torch.int32, device=gpu.dev)
+    pr = torch.tensor([1, 3, 2], dtype=torch.uint8, device=gpu.dev)
+    pairs = torch.zeros(8, dtype=torch.int64, device=gpu.dev)
+    bits, cnew, st = gpu.triage(ms, ns, sigs, cs, cl, pr, new_pairs=pairs)
+    gpu.eng.set_agg(1, 0)
+    assert cnew.tolist() == [1, 1, 1] and int(bits[0]) == 0b11111 and st["new_pairs"] == 5
+    got = sorted(int(v) & ((1 << 64) - 1) for v in pairs[:5].tolist())
+    assert got == sorted([0xFFFFFFFF, 0, (1 << 32) | 0xFFFFFFFF, 1 << 32, (2 << 32) | 5])
+    assert ms.to_dict() == {0xFFFFFFFF: 3, 0: 3, 5: 2} and ns.to_dict() == ms.to_dict()
 
 
 def test_triage_rejects_out_of_range_calls(gpu):
@@ -155,8 +218,14 @@ def test_triage_c2_properties(gpu):
     ms = gpu.deserialize(e0, p0)
     ms2 = ms.clone()
     ns = S.Signal(None, gpu.eng)
-    bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
+    pairs = torch.empty(16 << 20, dtype=torch.int64, device=gpu.dev)
+    bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio, new_pairs=pairs)
     assert st["changed"] == ns.Len() and st["records"] == int(dcnt.to(torch.int64).sum()) and st["parts"] > 0
+    assert st["overflow_parts"] == 0 and st["new_pairs"] <= pairs.numel()
+    # pairs <-> bits: one pair per distinct (call, elem) among the marked records
+    npair = st["new_pairs"]
+    assert npair == int(torch.unique(pairs[:npair]).numel())
+    assert int(cnew.sum()) == int(torch.unique(pairs[:npair] >> 32).numel())
     h = nprog * cpp // 2
     ns2 = S.Signal(None, gpu.eng)
     b1, c1, _ = gpu.triage(ms2, ns2, ds, dcs[:h].contiguous(), dcnt[:h].contiguous(), dprio[:h].contiguous())
