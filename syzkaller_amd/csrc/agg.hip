@@ -17,21 +17,30 @@
 // and that record is (first[e][l], e) -- the call's DiffRaw result.  So the
 // batch needs ONE maxSignal probe per distinct element, not one per record.
 //
+// Record format.  h = fmix32(e) is a bijection of u32.  A run is cut into
+// P = 2^pbits partitions by the top pbits of h, and into chunks of 2^cbits
+// consecutive calls (cbits = pbits - 2).  Partition p stores its records chunk
+// after chunk (one "cell" per (chunk, p)), so a record only needs
+//   h's low 32 - pbits bits | level (2 bits) | serial inside its chunk (cbits bits)
+// = exactly 32 bits: the partition and the chunk are implied by where the
+// record is stored.
+//
 // Pipeline (one run of <= 4 prio levels):
-//   k_agg_count / k_part_scan_chunks / k_part_scan / k_agg_scatter
-//       records -> 8-B packed (e << 32 | level << 24 | serial), grouped into P
-//       partitions by the top of fmix32(e): partition p holds every record of
-//       about D/P distinct elements.
+//   k_agg_count / k_agg_scan_chunks / k_agg_scan_totals / k_agg_scatter
+//       records -> 4-B packed records grouped by partition, cells in chunk order.
 //   k_agg       one 1024-thread workgroup per partition: an LDS hash table
-//       (key + 4 level firsts, 20 B/slot, kAggSlots slots = 155 KiB) absorbs
-//       the partition's records with ds_cmpst / ds_min; then the distinct
+//       (residual key + 4 level firsts, 20 B/slot, kAggSlots slots = 155 KiB)
+//       absorbs the partition's records -- one ds_read_b128 of the home bucket,
+//       a ds_cmpst on first sight, one ds_min per record; then the distinct
 //       elements are written out compactly.  A partition with more distinct
-//       elements than the LDS table holds is flagged and redone by
-//       k_agg_global (the same aggregation in an HBM table).
-//   k_agg_finalize  one thread per distinct element: probe/insert maxSignal,
-//       emit the new (call, elem) pairs and call flags, write M_final, merge
-//       newSignal.  maxSignal/newSignal capacity is reserved before it from
-//       the exact distinct count, so nothing is ever retried.
+//       elements than kAggLimit is flagged and redone by k_agg_global (the same
+//       aggregation in an HBM table).
+//   k_agg_finalize  one workgroup per partition's distinct list: probe/insert
+//       maxSignal, emit the new (call, elem) pairs and call flags, write
+//       M_final, merge newSignal.  maxSignal's home bucket is the top bits of
+//       the same h (internal.h home_bucket), so one partition's probes stay in
+//       one contiguous slice of the table.  Capacity is reserved before it
+//       from the exact distinct count, so nothing is ever retried.
 //   k_pairs_mark (optional) per-record new bits from the pairs.
 #include <algorithm>
 #include <vector>
@@ -41,23 +50,54 @@
 namespace syz {
 
 constexpr uint32_t kAggThreads = 1024;
-constexpr uint32_t kAggSlots = 7936;              // LDS slots per workgroup (+1 special slot)
-constexpr uint32_t kAggBuckets = kAggSlots / 4;   // 4-key buckets (one ds_read_b128 per probe)
+constexpr uint32_t kAggSlots = 7936;               // LDS slots per workgroup
+constexpr uint32_t kAggBuckets = kAggSlots / 4;    // 4-key buckets (one ds_read_b128 per probe)
 constexpr uint32_t kAggNoSlot = 0xFFFFFFFFu;
-constexpr uint32_t kAggRegion = kAggSlots + 1;    // distinct-list region per partition
+constexpr uint32_t kAggRegion = kAggSlots;         // distinct-list region per partition
 constexpr uint32_t kAggLimit = kAggSlots * 4 / 5;  // distinct elements before a partition overflows
-constexpr uint32_t kAggEmpty = 0xFFFFFFFFu;       // empty key (element 0xFFFFFFFF uses the special slot)
-constexpr uint32_t kAggNone = 0xFFFFFFFFu;        // no record at this level
-constexpr uint32_t kAggOverflow = 0xFFFFFFFFu;    // partition count marker
-constexpr uint32_t kAggMaxParts = 2048;
-constexpr uint32_t kAggCPB = 256;   // calls per chunk of the count/scatter passes
-constexpr uint32_t kAggTile = 12288; // records per scatter tile (10 B of LDS each)
+constexpr double kAggTargetLoad = 0.4;             // partitions are sized for this LDS load
+constexpr uint32_t kAggEmpty = 0xFFFFFFFFu;        // empty key (LDS keys are residuals < 2^29)
+constexpr uint32_t kAggNone = 0xFFFFFFFFu;         // no record at this level
+constexpr uint32_t kAggOverflow = 0xFFFFFFFFu;     // partition count marker
+constexpr uint32_t kAggMinBits = 3, kAggMaxBits = 11;
+constexpr uint32_t kAggMaxParts = 1u << kAggMaxBits;
+constexpr uint32_t kAggTile = 15360;  // records per scatter tile (8 B of LDS each)
+constexpr uint32_t kAggGroup = 8;     // cells per wave work item of k_agg
 
-__device__ __forceinline__ uint32_t agg_part(uint32_t e, uint32_t P) { return __umulhi(fmix32(e), P); }
-// LDS home bucket: a second, independent mix (the partition used fmix32's top bits)
-__device__ __forceinline__ uint32_t agg_home_bucket(uint32_t e)
+static_assert(0x85ebca6bu * 0xa5cb9243u == 1u, "fmix32_inv multiplier");
+static_assert(0xc2b2ae35u * 0x7ed1b41du == 1u, "fmix32_inv multiplier");
+
+// murmur3 fmix32 (common.h) inverted: the records keep bits of h = fmix32(e)
+__host__ __device__ __forceinline__ uint32_t fmix32_inv(uint32_t h)
 {
-	return __umulhi(fmix32(e * 0x9E3779B1u + 0x632BE5ABu), kAggBuckets);
+	h ^= h >> 16;
+	h *= 0x7ed1b41du;
+	h ^= (h >> 13) ^ (h >> 26);
+	h *= 0xa5cb9243u;
+	h ^= h >> 16;
+	return h;
+}
+
+// Partition geometry of one run (see the header).
+struct AggGeom {
+	uint32_t pbits;  // P = 2^pbits partitions
+	__host__ __device__ uint32_t rbits() const { return 32 - pbits; }
+	__host__ __device__ uint32_t cbits() const { return pbits - 2; }
+	__host__ __device__ uint32_t part(uint32_t h) const { return h >> (32 - pbits); }
+	__host__ __device__ uint32_t meta(uint32_t level, uint64_t serial) const
+	{
+		return (level << cbits()) | ((uint32_t)serial & ((1u << cbits()) - 1));
+	}
+	__host__ __device__ uint32_t rec(uint32_t h, uint32_t meta) const { return (h << pbits) | meta; }
+	__host__ __device__ uint32_t resid(uint32_t r) const { return r >> pbits; }
+	__host__ __device__ uint32_t level(uint32_t r) const { return (r >> cbits()) & 3; }
+	__host__ __device__ uint32_t local(uint32_t r) const { return r & ((1u << cbits()) - 1); }
+};
+
+// LDS home bucket of a residual: its top bits (h is already mixed)
+__device__ __forceinline__ uint32_t agg_home_bucket(uint32_t key, const AggGeom& g)
+{
+	return __umulhi(key << g.pbits, kAggBuckets);
 }
 
 // position of e in a 4-key bucket, 4 if absent
@@ -66,63 +106,100 @@ __device__ __forceinline__ uint32_t bucket_find(uint4 B, uint32_t e)
 	return B.x == e ? 0 : B.y == e ? 1 : B.z == e ? 2 : B.w == e ? 3 : 4;
 }
 
-// Find-or-insert e in the LDS key buckets, bucket-linear from its home bucket.
-// Keys only go empty -> key, so a key is always at or before the first empty
-// slot of its probe sequence.  Returns the slot, or kAggNoSlot once the table
-// is past its limit (the partition is then redone in HBM).
-__device__ uint32_t agg_find_insert(uint4* kb, uint32_t e, uint32_t b, uint32_t* s_n, uint32_t* s_ovf)
+// position of the first empty key in a 4-key bucket, 4 if full
+__device__ __forceinline__ uint32_t bucket_first_empty(uint4 B)
+{
+	return B.x == kAggEmpty ? 0 : B.y == kAggEmpty ? 1 : B.z == kAggEmpty ? 2 : B.w == kAggEmpty ? 3 : 4;
+}
+
+// Find-or-insert e in the LDS key buckets, bucket-linear from its home bucket
+// b, whose snapshot B the caller already read.  Keys only go empty -> key, so
+// a key is always at or before the first empty slot of its probe sequence:
+// an insert is one ds_cmpst at the snapshot's first empty slot, re-reading the
+// bucket only when another lane took that slot first.  Returns the slot, or
+// kAggNoSlot once the table is past its limit (the partition is then redone
+// in HBM).
+__device__ uint32_t agg_find_insert(uint4* kb, uint32_t e, uint32_t b, uint4 B, uint32_t* s_n, uint32_t* s_ovf)
 {
 	uint32_t* keys = reinterpret_cast<uint32_t*>(kb);
-	for (uint32_t step = 0; step < kAggBuckets; step++) {
-		for (uint32_t j = 0; j < 4; j++) {
-			const uint32_t i = b * 4 + j;
-			uint32_t key = keys[i];
-			if (key == kAggEmpty) {
-				key = atomicCAS(&keys[i], kAggEmpty, e);
-				if (key == kAggEmpty) {
-					if (atomicAdd(s_n, 1u) >= kAggLimit)
-						*(volatile uint32_t*)s_ovf = 1;
-					return i;
-				}
-			}
-			if (key == e)
-				return i;
+	for (uint32_t step = 0; step < kAggBuckets;) {
+		const uint32_t f = bucket_find(B, e);
+		if (f < 4)
+			return b * 4 + f;
+		const uint32_t j = bucket_first_empty(B);
+		if (j == 4) {
+			b = b + 1 == kAggBuckets ? 0 : b + 1;
+			B = kb[b];
+			step++;
+			continue;
 		}
-		b = b + 1 == kAggBuckets ? 0 : b + 1;
+		const uint32_t i = b * 4 + j;
+		const uint32_t key = atomicCAS(&keys[i], kAggEmpty, e);
+		if (key == kAggEmpty) {
+			if (atomicAdd(s_n, 1u) >= kAggLimit)
+				*(volatile uint32_t*)s_ovf = 1;
+			return i;
+		}
+		if (key == e)
+			return i;
+		B = kb[b];  // another lane filled the slot first
 	}
 	*(volatile uint32_t*)s_ovf = 1;
 	return kAggNoSlot;
 }
 
+// Cell boundaries of one group of kAggGroup chunks of a partition (uniform
+// over the wave: scalar loads), and the serial of a record inside the group.
+struct CellGroup {
+	uint64_t ch0;
+	uint32_t bnd[kAggGroup + 1];
+	__device__ void load(const uint32_t* __restrict__ ot, uint64_t nchunks, uint64_t gi)
+	{
+		ch0 = gi * kAggGroup;
+#pragma unroll
+		for (uint32_t i = 0; i <= kAggGroup; i++)
+			bnd[i] = ot[min<uint64_t>(ch0 + i, nchunks)];
+	}
+	__device__ uint32_t serial(uint32_t j, uint32_t r, const AggGeom& g) const
+	{
+		uint32_t chunk = (uint32_t)ch0;
+#pragma unroll
+		for (uint32_t i = 1; i < kAggGroup; i++)
+			chunk += j >= bnd[i];
+		return (chunk << g.cbits()) | g.local(r);
+	}
+};
+
 // ---------------------------------------------------------------- partitioning
-// Calls of the run [c0, c1) in chunks of kAggCPB; counts[chunk][p].
+// Calls of the run [c0, c1) in chunks of 2^cbits; counts[chunk][p].
 __global__ __launch_bounds__(kAggThreads) void k_agg_count(const uint32_t* __restrict__ sigs,
                                                            const uint64_t* __restrict__ call_start,
                                                            const uint32_t* __restrict__ call_len, uint64_t c0,
-                                                           uint64_t c1, uint32_t P, uint32_t* counts)
+                                                           uint64_t c1, AggGeom g, uint32_t* counts)
 {
 	__shared__ uint32_t h[kAggMaxParts];
+	const uint32_t P = 1u << g.pbits, cb = g.cbits();
 	const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = lane_id();
-	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + kAggCPB - 1) / kAggCPB;
+	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << cb) - 1) >> cb;
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
 			h[i] = 0;
 		__syncthreads();
-		const uint64_t ce = min<uint64_t>(ncalls, (ch + 1) * kAggCPB);
-		for (uint64_t s = ch * kAggCPB + w; s < ce; s += nw) {
+		const uint64_t ce = min<uint64_t>(ncalls, (ch + 1) << cb);
+		for (uint64_t s = (ch << cb) + w; s < ce; s += nw) {
 			const uint64_t c = c0 + s, start = call_start[c];
 			const uint32_t len = call_len[c];
 			uint32_t j = lane;
 			for (; j + 192 < len; j += 256) {
 				const uint32_t a = sigs[start + j], b = sigs[start + j + 64], d = sigs[start + j + 128],
 				               f = sigs[start + j + 192];
-				atomicAdd(&h[agg_part(a, P)], 1u);
-				atomicAdd(&h[agg_part(b, P)], 1u);
-				atomicAdd(&h[agg_part(d, P)], 1u);
-				atomicAdd(&h[agg_part(f, P)], 1u);
+				atomicAdd(&h[g.part(fmix32(a))], 1u);
+				atomicAdd(&h[g.part(fmix32(b))], 1u);
+				atomicAdd(&h[g.part(fmix32(d))], 1u);
+				atomicAdd(&h[g.part(fmix32(f))], 1u);
 			}
 			for (; j < len; j += 64)
-				atomicAdd(&h[agg_part(sigs[start + j], P)], 1u);
+				atomicAdd(&h[g.part(fmix32(sigs[start + j]))], 1u);
 		}
 		__syncthreads();
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
@@ -156,23 +233,30 @@ __device__ __forceinline__ uint32_t block_excl_scan_1k(uint32_t v, uint32_t* out
 	return tot;
 }
 
-// block p: exclusive scan over chunks of counts[.][p] -> offs[.][p]; totals[p]
+// block p: exclusive scan over chunks of counts[.][p] -> offs[.][p]
+// (chunk-major, for the scatter) and offsT[p][.] (partition-major, the
+// partition's total at [nchunks], for k_agg); totals[p]
 __global__ __launch_bounds__(1024) void k_agg_scan_chunks(const uint32_t* counts, uint64_t nchunks, uint32_t P,
-                                                          uint32_t* offs, uint64_t* totals)
+                                                          uint32_t* offs, uint32_t* offsT, uint64_t* totals)
 {
 	const uint32_t p = blockIdx.x;
+	uint32_t* ot = offsT + (uint64_t)p * (nchunks + 1);
 	uint64_t run = 0;
 	for (uint64_t b0 = 0; b0 < nchunks; b0 += blockDim.x) {
 		const uint64_t b = b0 + threadIdx.x;
 		const uint32_t v = b < nchunks ? counts[b * P + p] : 0;
 		uint32_t ex;
 		const uint32_t tot = block_excl_scan_1k(v, &ex);
-		if (b < nchunks)
+		if (b < nchunks) {
 			offs[b * P + p] = (uint32_t)(run + ex);
+			ot[b] = (uint32_t)(run + ex);
+		}
 		run += tot;
 	}
-	if (threadIdx.x == 0)
+	if (threadIdx.x == 0) {
 		totals[p] = run;
+		ot[nchunks] = (uint32_t)run;
+	}
 }
 
 // totals -> rec_base[P + 1] (one block; P <= 2048)
@@ -196,32 +280,36 @@ __global__ __launch_bounds__(1024) void k_agg_scan_totals(const uint64_t* totals
 		rec_base[i] = s[i];
 }
 
-// Records of each chunk -> their partitions' slices (fixed by the scan, so no
-// global atomics).  A tile of kAggTile records is staged in LDS, counting-sorted
-// by partition (the partition is recomputed from the record, so the tile costs
-// 10 B/record of LDS) and written as one run per partition.
+// Records of each chunk -> their cells (fixed by the scan, so no global
+// atomics).  A tile of kAggTile records is staged in LDS as (h, meta),
+// counting-sorted by partition and written as one run per partition; the
+// runs of one chunk's consecutive tiles continue each other.
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __restrict__ sigs,
                                                              const uint64_t* __restrict__ call_start,
                                                              const uint32_t* __restrict__ call_len,
                                                              const uint8_t* __restrict__ call_prio, LevelMap lm,
-                                                             uint64_t c0, uint64_t c1, uint32_t P,
+                                                             uint64_t c0, uint64_t c1, AggGeom g,
                                                              const uint32_t* __restrict__ offs,
-                                                             const uint64_t* __restrict__ rec_base, uint64_t* recs)
+                                                             const uint64_t* __restrict__ rec_base, uint32_t* recs)
 {
 	constexpr uint32_t kWaves = kAggThreads / 64, kQuota = kAggTile / kWaves, kPer = kQuota / 64;
-	__shared__ uint64_t t_rec[kAggTile];
-	__shared__ uint16_t s_idx[kAggTile];
-	__shared__ uint32_t cur[kAggMaxParts], hist[kAggMaxParts], pos[kAggMaxParts];
+	static_assert(kQuota % 64 == 0, "tile quota per wave");
+	__shared__ uint32_t t_h[kAggTile];    // fmix32(e)
+	__shared__ uint16_t t_m[kAggTile];    // level << cbits | serial in chunk
+	__shared__ uint16_t s_idx[kAggTile];  // sorted position -> staged record
+	__shared__ uint64_t cur[kAggMaxParts];
+	__shared__ uint32_t hist[kAggMaxParts], pos[kAggMaxParts];
 	__shared__ uint32_t tile_n, more;
+	const uint32_t P = 1u << g.pbits, cb = g.cbits();
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + kAggCPB - 1) / kAggCPB;
+	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << cb) - 1) >> cb;
 	const uint32_t per_t = (P + blockDim.x - 1) / blockDim.x;
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-		const uint64_t cb = ch * kAggCPB, ce = min<uint64_t>(ncalls, cb + kAggCPB);
+		const uint64_t cbeg = ch << cb, ce = min<uint64_t>(ncalls, cbeg + (1ull << cb));
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
-			cur[i] = offs[ch * P + i];
-		uint64_t wc = cb + w;  // this wave's call (serial), then +kWaves
-		uint32_t wo = 0;       // offset inside it
+			cur[i] = rec_base[i] + offs[ch * P + i];
+		uint64_t wc = cbeg + w;  // this wave's call (serial), then +kWaves
+		uint32_t wo = 0;         // offset inside it
 		for (;;) {
 			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
 				hist[i] = 0;
@@ -239,7 +327,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 				if (lane == 0 && m)
 					tb = atomicAdd(&tile_n, m);
 				tb = __shfl(tb, 0, 64);
-				const uint64_t head = ((uint64_t)lm.lvl[call_prio[c]] << 24) | (wc & kSerialMask);
+				const uint32_t meta = g.meta(lm.lvl[call_prio[c]], wc);
 				uint32_t ev[kPer];
 #pragma unroll
 				for (uint32_t u = 0; u < kPer; u++) {
@@ -250,8 +338,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 				for (uint32_t u = 0; u < kPer; u++) {
 					const uint32_t i = u * 64 + lane;
 					if (i < m) {
-						t_rec[tb + i] = ((uint64_t)ev[u] << 32) | head;
-						atomicAdd(&hist[agg_part(ev[u], P)], 1u);
+						const uint32_t h = fmix32(ev[u]);
+						t_h[tb + i] = h;
+						t_m[tb + i] = (uint16_t)meta;
+						atomicAdd(&hist[g.part(h)], 1u);
 					}
 				}
 				quota -= m;
@@ -277,19 +367,18 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 				const uint32_t i = threadIdx.x * per_t + q;
 				if (i < P) {
 					pos[i] = ex;
-					cur[i] -= ex;  // cur[p] + d = output offset of sorted position d
+					cur[i] -= ex;  // cur[p] + d = output index of sorted position d (u64 wrap intended)
 					ex += hist[i];
 				}
 			}
 			__syncthreads();
 			for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
-				s_idx[atomicAdd(&pos[agg_part((uint32_t)(t_rec[i] >> 32), P)], 1u)] = (uint16_t)i;
+				s_idx[atomicAdd(&pos[g.part(t_h[i])], 1u)] = (uint16_t)i;
 			__syncthreads();
 			// consecutive threads write consecutive records of one partition's run
 			for (uint32_t d = threadIdx.x; d < n; d += blockDim.x) {
-				const uint64_t r = t_rec[s_idx[d]];
-				const uint32_t p = agg_part((uint32_t)(r >> 32), P);
-				recs[rec_base[p] + (uint32_t)(cur[p] + d)] = r;  // u32 wrap intended: cur[p] = old - ex
+				const uint32_t i = s_idx[d], h = t_h[i];
+				recs[cur[g.part(h)] + d] = g.rec(h, t_m[i]);
 			}
 			__syncthreads();
 			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
@@ -303,20 +392,24 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 }
 
 // ---------------------------------------------------------------- aggregation
-// One workgroup per partition.  Output: the partition's distinct elements and
-// their level firsts at dist_*[p * kAggRegion ...], cnt[p] = how many, or
-// kAggOverflow when they do not fit the LDS table.
-__global__ __launch_bounds__(kAggThreads) void k_agg(const uint64_t* __restrict__ recs,
-                                                     const uint64_t* __restrict__ rec_base, uint32_t P,
+// One workgroup per partition.  Waves take groups of kAggGroup cells from an
+// LDS counter.  Output: the partition's distinct elements and their level
+// firsts at dist_*[p * kAggRegion ...], cnt[p] = how many, or kAggOverflow
+// when they do not fit the LDS table.
+__global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict__ recs,
+                                                     const uint64_t* __restrict__ rec_base,
+                                                     const uint32_t* __restrict__ offsT, uint64_t nchunks, AggGeom g,
                                                      uint32_t* dist_e, uint4* dist_f, uint32_t* cnt)
 {
 	constexpr uint32_t U = 8;
-	__shared__ uint4 kb[kAggBuckets];  // keys, 4-slot buckets
-	__shared__ uint32_t fl[4][kAggRegion];
-	__shared__ uint32_t s_n, s_ovf, s_out;
+	__shared__ uint4 kb[kAggBuckets];  // keys (residuals), 4-slot buckets
+	__shared__ uint32_t fl[4][kAggSlots];
+	__shared__ uint32_t s_n, s_ovf, s_out, s_next;
 	const uint32_t* keys = reinterpret_cast<const uint32_t*>(kb);
+	const uint32_t P = 1u << g.pbits, lane = lane_id();
+	const uint64_t ngroups = (nchunks + kAggGroup - 1) / kAggGroup;
 	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
-		for (uint32_t i = threadIdx.x; i < kAggRegion; i += blockDim.x) {
+		for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
 			if (i < kAggBuckets)
 				kb[i] = make_uint4(kAggEmpty, kAggEmpty, kAggEmpty, kAggEmpty);
 			fl[0][i] = fl[1][i] = fl[2][i] = fl[3][i] = kAggNone;
@@ -325,62 +418,72 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint64_t* __restrict_
 			s_n = 0;
 			s_ovf = 0;
 			s_out = 0;
+			s_next = 0;
 		}
 		__syncthreads();
-		const uint64_t base = rec_base[p], end = rec_base[p + 1];
-		// records stream through registers one batch ahead of the LDS work; no
-		// barrier inside the loop (a wave leaves early once overflow is flagged)
-		uint64_t nxt[U];
-#pragma unroll
-		for (uint32_t u = 0; u < U; u++) {
-			const uint64_t j = base + u * kAggThreads + threadIdx.x;
-			nxt[u] = j < end ? __builtin_nontemporal_load(&recs[j]) : ~0ull;
-		}
-		for (uint64_t r0 = base; r0 < end; r0 += (uint64_t)U * kAggThreads) {
-			uint32_t e[U], l[U], k[U], slot[U], hb[U];
-			bool need[U];
-#pragma unroll
-			for (uint32_t u = 0; u < U; u++) {
-				const uint64_t r = nxt[u];
-				const uint64_t j = r0 + (uint64_t)(U + u) * kAggThreads + threadIdx.x;
-				nxt[u] = j < end ? __builtin_nontemporal_load(&recs[j]) : ~0ull;
-				e[u] = (uint32_t)(r >> 32);
-				l[u] = (uint32_t)(r >> 24) & 0xff;  // 0xff: past the end (a real record has level < 4)
-				k[u] = (uint32_t)r & kSerialMask;
-				hb[u] = agg_home_bucket(e[u]);
-			}
-			// home buckets of all U records in flight together (ds_read_b128 each)
-			uint4 B[U];
-#pragma unroll
-			for (uint32_t u = 0; u < U; u++)
-				B[u] = kb[hb[u]];
-#pragma unroll
-			for (uint32_t u = 0; u < U; u++) {
-				need[u] = false;
-				slot[u] = kAggNoSlot;
-				if (l[u] == 0xff)
-					continue;
-				if (e[u] == kAggEmpty) {
-					slot[u] = kAggSlots;  // special slot of element 0xFFFFFFFF
-					continue;
-				}
-				const uint32_t f = bucket_find(B[u], e[u]);
-				if (f < 4)
-					slot[u] = hb[u] * 4 + f;
-				else
-					need[u] = true;
-			}
-			// rare: insertion or a chain past the home bucket
-#pragma unroll
-			for (uint32_t u = 0; u < U; u++)
-				if (need[u])
-					slot[u] = agg_find_insert(kb, e[u], hb[u], &s_n, &s_ovf);
-#pragma unroll
-			for (uint32_t u = 0; u < U; u++)
-				if (slot[u] != kAggNoSlot)
-					atomicMin(&fl[l[u] & 3][slot[u]], k[u]);
-			if (*(volatile uint32_t*)&s_ovf)
+		const uint32_t* pr = recs + rec_base[p];
+		const uint32_t* ot = offsT + (uint64_t)p * (nchunks + 1);
+		// no barrier inside: a wave leaves early once overflow is flagged
+		for (;;) {
+			uint32_t gi = 0;
+			if (lane == 0)
+				gi = atomicAdd(&s_next, 1u);
+			gi = __builtin_amdgcn_readfirstlane(__shfl(gi, 0, 64));
+			if (gi >= ngroups || *(volatile uint32_t*)&s_ovf)
 				break;
+			CellGroup cg;
+			cg.load(ot, nchunks, gi);
+			const uint32_t je = cg.bnd[kAggGroup];
+			// records stream through registers one batch ahead of the LDS work
+			uint32_t nxt[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++) {
+				const uint32_t j = cg.bnd[0] + u * 64 + lane;
+				nxt[u] = j < je ? __builtin_nontemporal_load(&pr[j]) : 0;
+			}
+			for (uint32_t j0 = cg.bnd[0]; j0 < je; j0 += U * 64) {
+				uint32_t key[U], lv[U], k[U], hb[U], slot[U];
+				bool ok[U], need[U];
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++) {
+					const uint32_t j = j0 + u * 64 + lane, r = nxt[u];
+					const uint32_t jn = j + U * 64;
+					nxt[u] = jn < je ? __builtin_nontemporal_load(&pr[jn]) : 0;
+					ok[u] = j < je;
+					k[u] = cg.serial(j, r, g);
+					key[u] = g.resid(r);
+					lv[u] = g.level(r);
+					hb[u] = agg_home_bucket(key[u], g);
+				}
+				// home buckets of all U records in flight together (ds_read_b128 each)
+				uint4 B[U];
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					B[u] = kb[hb[u]];
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++) {
+					need[u] = false;
+					slot[u] = kAggNoSlot;
+					if (!ok[u])
+						continue;
+					const uint32_t f = bucket_find(B[u], key[u]);
+					if (f < 4)
+						slot[u] = hb[u] * 4 + f;
+					else
+						need[u] = true;
+				}
+				// first sight of an element, or a chain past its home bucket
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					if (need[u])
+						slot[u] = agg_find_insert(kb, key[u], hb[u], B[u], &s_n, &s_ovf);
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					if (slot[u] != kAggNoSlot)
+						atomicMin(&fl[lv[u]][slot[u]], k[u]);
+				if (*(volatile uint32_t*)&s_ovf)
+					break;
+			}
 		}
 		__syncthreads();
 		if (s_ovf) {
@@ -389,19 +492,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint64_t* __restrict_
 			__syncthreads();
 			continue;
 		}
-		// compact the occupied slots
-		const uint32_t lane = lane_id();
-		for (uint32_t i0 = 0; i0 < kAggRegion; i0 += kAggThreads) {
+		// compact the occupied slots, elements restored from (p, residual)
+		const uint32_t hp = p << g.rbits();
+		for (uint32_t i0 = 0; i0 < kAggSlots; i0 += kAggThreads) {
 			const uint32_t i = i0 + threadIdx.x;
-			bool occ = false;
-			uint32_t e = 0;
-			if (i < kAggSlots) {
-				e = keys[i];
-				occ = e != kAggEmpty;
-			} else if (i == kAggSlots) {
-				e = kAggEmpty;
-				occ = (fl[0][i] & fl[1][i] & fl[2][i] & fl[3][i]) != kAggNone;
-			}
+			const uint32_t key = i < kAggSlots ? keys[i] : kAggEmpty;
+			const bool occ = key != kAggEmpty;
 			const uint64_t m = __ballot(occ);
 			uint32_t wb = 0;
 			if (lane == 0 && m)
@@ -409,7 +505,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint64_t* __restrict_
 			wb = __shfl(wb, 0, 64);
 			if (occ) {
 				const uint64_t o = (uint64_t)p * kAggRegion + wb + lane_rank(m);
-				dist_e[o] = e;
+				dist_e[o] = fmix32_inv(hp | key);
 				dist_f[o] = make_uint4(fl[0][i], fl[1][i], fl[2][i], fl[3][i]);
 			}
 		}
@@ -421,33 +517,40 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint64_t* __restrict_
 }
 
 // ---- fallback: partitions whose distinct elements overflow the LDS table are
-// aggregated in one HBM hash table (gkeys[C] + gfl[4][C + 1], C a power of two;
-// slot C is element 0xFFFFFFFF).  Partitions hold disjoint elements, so one
-// table serves all of them.
-__global__ __launch_bounds__(256) void k_agg_global(const uint64_t* __restrict__ recs,
+// aggregated in one HBM hash table keyed by h (gkeys[C] + gfl[4][C + 1], C a
+// power of two; slot C is h = 0xFFFFFFFF).  Partitions hold disjoint
+// elements, so one table serves all of them.  One wave per (partition, group).
+__global__ __launch_bounds__(256) void k_agg_global(const uint32_t* __restrict__ recs,
                                                     const uint64_t* __restrict__ rec_base,
+                                                    const uint32_t* __restrict__ offsT, uint64_t nchunks, AggGeom g,
                                                     const uint32_t* __restrict__ ovl, uint32_t novl, uint32_t* gkeys,
                                                     uint32_t* gfl, uint64_t C, unsigned long long* err)
 {
-	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+	const uint32_t lane = lane_id();
+	const uint64_t ngroups = (nchunks + kAggGroup - 1) / kAggGroup, items = (uint64_t)novl * ngroups;
+	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
 	uint64_t bad = 0;
-	for (uint32_t q = 0; q < novl; q++) {
-		const uint32_t p = ovl[q];
-		const uint64_t end = rec_base[p + 1];
-		for (uint64_t j = rec_base[p] + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < end; j += stride) {
-			const uint64_t r = recs[j];
-			const uint32_t e = (uint32_t)(r >> 32), l = (uint32_t)(r >> 24) & 3, k = (uint32_t)r & kSerialMask;
+	for (uint64_t it = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); it < items; it += nwaves) {
+		const uint32_t p = ovl[it / ngroups];
+		const uint32_t* ot = offsT + (uint64_t)p * (nchunks + 1);
+		const uint32_t* pr = recs + rec_base[p];
+		CellGroup cg;
+		cg.load(ot, nchunks, it % ngroups);
+		for (uint32_t j = cg.bnd[0] + lane; j < cg.bnd[kAggGroup]; j += 64) {
+			const uint32_t r = pr[j];
+			const uint32_t k = cg.serial(j, r, g), l = g.level(r);
+			const uint32_t h = (p << g.rbits()) | g.resid(r);
 			uint64_t i = C;
-			if (e != kAggEmpty) {
-				i = fmix32(e * 0x9E3779B1u + 0x632BE5ABu) & (C - 1);
+			if (h != kAggEmpty) {
+				i = fmix32(h ^ 0x632BE5ABu) & (C - 1);
 				for (uint64_t step = 0;; step++) {
 					uint32_t key = gkeys[i];
 					if (key == kAggEmpty) {
-						key = atomicCAS(&gkeys[i], kAggEmpty, e);
+						key = atomicCAS(&gkeys[i], kAggEmpty, h);
 						if (key == kAggEmpty)
 							break;
 					}
-					if (key == e)
+					if (key == h)
 						break;
 					i = (i + 1) & (C - 1);
 					if (step >= C) {
@@ -473,13 +576,13 @@ __global__ __launch_bounds__(256) void k_agg_global_compact(const uint32_t* __re
 	for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 <= C; i0 += (uint64_t)gridDim.x * blockDim.x) {
 		const uint64_t i = i0 + threadIdx.x;
 		bool occ = false;
-		uint32_t e = kAggEmpty;
+		uint32_t h = kAggEmpty;
 		uint4 f = make_uint4(kAggNone, kAggNone, kAggNone, kAggNone);
 		if (i <= C) {
 			f = make_uint4(gfl[i], gfl[(C + 1) + i], gfl[2 * (C + 1) + i], gfl[3 * (C + 1) + i]);
 			if (i < C) {
-				e = gkeys[i];
-				occ = e != kAggEmpty;
+				h = gkeys[i];
+				occ = h != kAggEmpty;
 			} else {
 				occ = (f.x & f.y & f.z & f.w) != kAggNone;
 			}
@@ -490,16 +593,18 @@ __global__ __launch_bounds__(256) void k_agg_global_compact(const uint32_t* __re
 			wb = atomicAdd(out_cnt, (unsigned long long)__popcll(m));
 		wb = __shfl(wb, 0, 64);
 		if (occ) {
-			dist_e[wb + lane_rank(m)] = e;
+			dist_e[wb + lane_rank(m)] = fmix32_inv(h);
 			dist_f[wb + lane_rank(m)] = f;
 		}
 	}
 }
 
 // ---------------------------------------------------------------- finalize
-// Region r covers dist_*[r * kAggRegion, + cnt[r]).  Grid-stride over the
-// region slots (many independent probe chains in flight); a block gathers its
-// pairs in LDS and appends them with one global atomic per flush.
+// One workgroup per region r = dist_*[r * kAggRegion, + cnt[r]): a partition's
+// distinct elements, whose maxSignal/newSignal home buckets share one slice of
+// each table (the same top bits of h), so a block's probes stay in one slice.
+// A block gathers its pairs in LDS and appends them with one global atomic
+// per flush.
 constexpr uint32_t kFinThreads = 256, kFinBuf = 4 * kFinThreads * 2;
 
 __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __restrict__ dist_e,
@@ -518,71 +623,79 @@ __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __
 	if (threadIdx.x == 0)
 		s_n = 0;
 	__syncthreads();
-	const uint64_t total = (uint64_t)nregions * kAggRegion;
-	for (uint64_t o0 = blockIdx.x * (uint64_t)blockDim.x; o0 < total; o0 += (uint64_t)gridDim.x * blockDim.x) {
-		const uint64_t o = o0 + threadIdx.x;
-		const uint32_t r = (uint32_t)(o / kAggRegion), i = (uint32_t)(o % kAggRegion);
-		if (o < total && cnt[r] != kAggOverflow && i < cnt[r]) {
-			const uint32_t e = dist_e[o];
-			const uint4 f4 = dist_f[o];
-			const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
-			int top = -1;
+	auto flush = [&](uint32_t nb) {  // every thread; nb = s_n read after a barrier
+		if (threadIdx.x == 0)
+			s_base = atomicAdd(npairs, (unsigned long long)nb);
+		__syncthreads();
+		for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x)
+			pairs[s_base + t] = buf[t];
+		__syncthreads();
+		if (threadIdx.x == 0)
+			s_n = 0;
+		__syncthreads();
+	};
+	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
+		const uint32_t n = cnt[r] == kAggOverflow ? 0 : cnt[r];
+		for (uint32_t i0 = 0; i0 < n; i0 += kFinThreads) {
+			const uint32_t i = i0 + threadIdx.x;
+			if (i < n) {
+				const uint64_t o = (uint64_t)r * kAggRegion + i;
+				const uint32_t e = dist_e[o];
+				const uint4 f4 = dist_f[o];
+				const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
+				int top = -1;
 #pragma unroll
-			for (int l = 0; l < 4; l++)
-				if (l < (int)lm.n && f[l] != kAggNone)
-					top = l;
-			if (top >= 0) {
-				// one probe sequence: insert M_final if absent, else read M0
-				const int8_t P = lm.val[top];
-				const uint64_t word = make_slot(e, P);
-				uint64_t old = 0;
-				const int64_t idx = tbl_find_or_insert(slots, bmask, e, word, old, max_probe);
-				if (idx < 0) {
-					ovf++;
-				} else {
-					const bool present = slot_live(old);  // (old == 0: inserted just now)
-					const int p0 = present ? (int)slot_prio(old) : -1000;
-					if ((int)P > p0) {
-						if (old != 0)
-							slots[idx] = word;  // one entry per element: no other writer
-						inserted += !present;  // fresh, or an "absent" marker going live
-						changed++;
-						const int rr = tbl_merge(ns_slots, ns_bmask, e, P);
-						ns_ins += rr == 1;
-						ovf += rr < 0;
-						// the staircase: first records of strictly rising level above M0[e]
-						uint32_t mk = kAggNone;
+				for (int l = 0; l < 4; l++)
+					if (l < (int)lm.n && f[l] != kAggNone)
+						top = l;
+				if (top >= 0) {
+					// one probe sequence: insert M_final if absent, else read M0
+					const int8_t P = lm.val[top];
+					const uint64_t word = make_slot(e, P);
+					uint64_t old = 0;
+					const int64_t idx = tbl_find_or_insert(slots, bmask, e, word, old, max_probe);
+					if (idx < 0) {
+						ovf++;
+					} else {
+						const bool present = slot_live(old);  // (old == 0: inserted just now)
+						const int p0 = present ? (int)slot_prio(old) : -1000;
+						if ((int)P > p0) {
+							if (old != 0)
+								slots[idx] = word;  // one entry per element: no other writer
+							inserted += !present;   // fresh, or an "absent" marker going live
+							changed++;
+							const int rr = tbl_merge(ns_slots, ns_bmask, e, P);
+							ns_ins += rr == 1;
+							ovf += rr < 0;
+							// the staircase: first records of strictly rising level above M0[e]
+							uint32_t mk = kAggNone;
 #pragma unroll
-						for (int l = 3; l >= 0; l--) {
-							if (l > top || f[l] == kAggNone)
-								continue;
-							if ((int)lm.val[l] <= p0)
-								break;
-							if (f[l] < mk) {
-								mk = f[l];
-								const uint64_t c = c0 + f[l];
-								call_new[c] = 1;
-								buf[atomicAdd(&s_n, 1u)] = (c << 32) | e;
+							for (int l = 3; l >= 0; l--) {
+								if (l > top || f[l] == kAggNone)
+									continue;
+								if ((int)lm.val[l] <= p0)
+									break;
+								if (f[l] < mk) {
+									mk = f[l];
+									const uint64_t c = c0 + f[l];
+									call_new[c] = 1;
+									buf[atomicAdd(&s_n, 1u)] = (c << 32) | e;
+								}
 							}
 						}
 					}
 				}
 			}
-		}
-		__syncthreads();
-		const uint32_t n = s_n;
-		if (n > kFinBuf - 4 * kFinThreads || o0 + (uint64_t)gridDim.x * blockDim.x >= total) {
-			if (threadIdx.x == 0)
-				s_base = n ? atomicAdd(npairs, (unsigned long long)n) : 0;
 			__syncthreads();
-			for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
-				pairs[s_base + t] = buf[t];
-			__syncthreads();
-			if (threadIdx.x == 0)
-				s_n = 0;
-			__syncthreads();
+			const uint32_t nb = s_n;
+			if (nb > kFinBuf - 4 * kFinThreads)
+				flush(nb);
 		}
 	}
+	__syncthreads();
+	const uint32_t nb = s_n;
+	if (nb)
+		flush(nb);
 	block_count(&ctr[kCntInserted], inserted);
 	block_count(&ctr[kCntChanged], changed);
 	block_count(&ctr[kCntAux], ns_ins);
@@ -717,44 +830,51 @@ static uint64_t pow2_at_least(uint64_t x)
 	return p;
 }
 
-uint32_t agg_parts_for(syzsig_ctx* ctx, uint64_t nrec)
+static AggGeom agg_geom_for(syzsig_ctx* ctx, uint64_t nrec)
 {
+	AggGeom g;
+	if (ctx->agg_parts) {
+		g.pbits = 31 - __builtin_clz(ctx->agg_parts);  // validated power of two in [8, 2048]
+		return g;
+	}
 	// expected distinct elements: the ratio seen on the previous large batch
-	// (1/32 before the first), aiming at ~70% LDS load per partition (overflow at 80%)
+	// (1/32 before the first); big runs keep >= 256 partitions (one per CU)
 	const double ratio = ctx->agg_distinct_ratio > 0 ? ctx->agg_distinct_ratio : 1.0 / 32;
 	const double d = ratio * (double)nrec;
-	uint64_t P = (uint64_t)(d / (0.7 * kAggSlots)) + 1;
-	P = (P + 7) & ~7ull;
-	if (ctx->agg_parts)
-		P = ctx->agg_parts;
-	return (uint32_t)std::max<uint64_t>(8, std::min<uint64_t>(kAggMaxParts, P));
+	uint32_t pb = nrec >= (1ull << 24) ? 8 : kAggMinBits;
+	while (pb < kAggMaxBits && d > kAggTargetLoad * kAggSlots * (double)(1u << pb))
+		pb++;
+	g.pbits = pb;
+	return g;
 }
 
-// One run of calls [c0, c1) with level map lm.  Pairs are appended at
-// pairs[*npairs_host ...] (capacity cap_pairs, internal buffer).
-int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,
-                   const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs_out,
-                   uint64_t* npairs_io)
+// Count, scatter and aggregate (plus the HBM fallback) one run of calls
+// [c0, c1) with level map lm: every distinct element of the run with its level
+// firsts (run serials), in regions of kAggRegion entries.
+int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const LevelMap& lm,
+                  uint64_t run_recs, syzsig_batch_stats* st, AggOut* out)
 {
-	const uint32_t P = agg_parts_for(ctx, run_recs);
-	const uint64_t nchunks = (c1 - c0 + kAggCPB - 1) / kAggCPB;
+	const AggGeom g = agg_geom_for(ctx, run_recs);
+	const uint32_t P = 1u << g.pbits;
+	const uint64_t nchunks = (c1 - c0 + (1ull << g.cbits()) - 1) >> g.cbits();
 	void *recs, *cm, *pm, *de, *df, *dc, *pr;
-	SYZ_TRY(ws_get(ctx, 16, run_recs * 8 + 64, &recs));
-	SYZ_TRY(ws_get(ctx, 17, nchunks * P * 4 * 2 + 64, &cm));
+	SYZ_TRY(ws_get(ctx, 16, run_recs * 4 + 64, &recs));
+	SYZ_TRY(ws_get(ctx, 17, (2 * nchunks * P + (uint64_t)P * (nchunks + 1)) * 4 + 64, &cm));
 	SYZ_TRY(ws_get(ctx, 18, (kAggMaxParts + 1) * 8 * 2, &pm));
 	uint32_t* counts = (uint32_t*)cm;
 	uint32_t* offs = counts + nchunks * P;
+	uint32_t* offsT = offs + nchunks * P;
 	uint64_t* totals = (uint64_t*)pm;
 	uint64_t* rec_base = totals + kAggMaxParts + 1;
 	const hipStream_t s = ctx->stream;
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
 	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
-	k_agg_count<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1, P, counts);
-	k_agg_scan_chunks<<<P, 1024, 0, s>>>(counts, nchunks, P, offs, totals);
+	k_agg_count<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1, g, counts);
+	k_agg_scan_chunks<<<P, 1024, 0, s>>>(counts, nchunks, P, offs, offsT, totals);
 	k_agg_scan_totals<<<1, 1024, 0, s>>>(totals, P, rec_base);
-	k_agg_scatter<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, P, offs,
-	                                         rec_base, (uint64_t*)recs);
+	k_agg_scatter<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, g, offs,
+	                                         rec_base, (uint32_t*)recs);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
@@ -762,7 +882,8 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 	SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
-	k_agg<<<P, kAggThreads, 0, s>>>((const uint64_t*)recs, rec_base, P, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	k_agg<<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, rec_base, offsT, nchunks, g, (uint32_t*)de, (uint4*)df,
+	                                (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -810,9 +931,12 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 		SYZ_HIP(hipMemsetAsync(gk, 0xff, C * 4 + (C + 1) * 16, s));
 		SYZ_HIP(hipMemcpyAsync(ol, ovl.data(), ovl.size() * 4, hipMemcpyHostToDevice, s));
 		SYZ_TRY(counters_reset(ctx));
-		k_agg_global<<<grid_for(ovrec, 256, 8192), 256, 0, s>>>((const uint64_t*)recs, rec_base, (const uint32_t*)ol,
-		                                                         (uint32_t)ovl.size(), (uint32_t*)gk, (uint32_t*)gf, C,
-		                                                         &ctx->d_cnt[kCntError]);
+		const uint64_t items = ovl.size() * ((nchunks + kAggGroup - 1) / kAggGroup);
+		k_agg_global<<<grid_for(items * 64, 256, 8192), 256, 0, s>>>((const uint32_t*)recs, rec_base,
+		                                                              (const uint32_t*)offsT, nchunks, g,
+		                                                              (const uint32_t*)ol, (uint32_t)ovl.size(),
+		                                                              (uint32_t*)gk, (uint32_t*)gf, C,
+		                                                              &ctx->d_cnt[kCntError]);
 		k_agg_global_compact<<<grid_for(C + 1, 256, 8192), 256, 0, s>>>(
 		    (const uint32_t*)gk, (const uint32_t*)gf, C, (uint32_t*)de2 + (uint64_t)P * kAggRegion,
 		    (uint4*)df2 + (uint64_t)P * kAggRegion, &ctx->d_cnt[kCntAux2]);
@@ -860,7 +984,7 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
 	if (D)
-		k_agg_finalize<<<grid_for((uint64_t)nregions * kAggRegion, kFinThreads, 2048), kFinThreads, 0, s>>>(
+		k_agg_finalize<<<nregions, kFinThreads, 0, s>>>(
 		    (const uint32_t*)dist_e, (const uint4*)dist_f, (const uint32_t*)dc, nregions, lm, c0, ms->slots,
 		    ms->nbuckets - 1, nsp ? nsp->slots : nullptr, nsp ? nsp->nbuckets - 1 : 0, b->call_new, (uint64_t*)pr,
 		    &ctx->d_cnt[kCntAux2], ctx->d_cnt);

@@ -117,7 +117,6 @@ constexpr uint32_t kSerialMask = 0xFFFFFF;  // 24-bit serial index inside a run
 int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm);
 
 // aggregation path (agg.hip)
-uint32_t agg_parts_for(syzsig_ctx* ctx, uint64_t nrec);
 int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,
                    const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs,
                    uint64_t* npairs);
@@ -198,7 +197,13 @@ __device__ __forceinline__ Bucket load_bucket(const uint64_t* p)
 	return B;
 }
 
-__device__ __forceinline__ uint64_t home_bucket(uint32_t key, uint64_t bmask) { return fmix32(key) & bmask; }
+// Home bucket = the top bits of fmix32(key): slices of the table then hold
+// contiguous ranges of h, which is what lets the aggregation path (agg.hip,
+// partitioned by the same top bits) probe one slice per partition.
+__device__ __forceinline__ uint64_t home_bucket(uint32_t key, uint64_t bmask)
+{
+	return ((uint64_t)fmix32(key) * (bmask + 1)) >> 32;
+}
 
 // Lookup.  Returns the slot index, or -1 if absent (first empty slot reached:
 // slots only ever go EMPTY -> key, so occupied slots form a prefix of every

@@ -111,8 +111,11 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 	c->stream = c->own_stream;
 	if (const char* v = getenv("SYZSIG_PART_MODE"))
 		c->part_mode = atoi(v);
-	if (const char* v = getenv("SYZSIG_AGG_PARTS"))
-		c->agg_parts = (uint32_t)atoi(v);
+	if (const char* v = getenv("SYZSIG_AGG_PARTS")) {
+		const uint32_t n = (uint32_t)atoi(v);
+		if (n >= 8 && n <= 2048 && !(n & (n - 1)))
+			c->agg_parts = n;
+	}
 	*out = c;
 	return SYZSIG_OK;
 }
@@ -153,8 +156,8 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts)
 {
 	if (!ctx)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_agg: ctx is NULL");
-	if (mode < 0 || mode > 2 || (parts && (parts < 8 || parts > 2048)))
-		return syz::fail(SYZSIG_EINVAL, "ctx_set_agg: mode must be 0..2 and parts 0 or 8..2048");
+	if (mode < 0 || mode > 2 || (parts && (parts < 8 || parts > 2048 || (parts & (parts - 1)))))
+		return syz::fail(SYZSIG_EINVAL, "ctx_set_agg: mode must be 0..2 and parts 0 or a power of two in 8..2048");
 	ctx->part_mode = mode;
 	ctx->agg_parts = parts;
 	return SYZSIG_OK;

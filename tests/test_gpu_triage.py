@@ -103,29 +103,53 @@ def test_triage_agg_auto_vs_oracle(gpu, skew):
     assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
 
 
-@pytest.mark.parametrize("frac", [0.3, 1.0, 100.0])
-def test_triage_agg_lds_overflow_fallback(gpu, frac):
-    """Partitions whose distinct elements do not fit the LDS table are redone in
-    the HBM table: none (frac 0.3 of the limit), about half (1.0), all (100)."""
-    from syzkaller_amd import synth
+AGG_LIMIT = 7936 * 4 // 5  # csrc/agg.hip kAggLimit: distinct elements an LDS partition holds
 
-    cfg = synth.synth_default(region_log2=11)
-    nprog, cpp = 64, 32
-    cl = synth.call_lengths(nprog, cpp, 2048)
-    hb = host_batch(cfg, nprog, cpp, cl)
-    hs, hcs, hcnt, _ = hb
-    idx = np.concatenate([np.arange(a, a + n) for a, n in zip(hcs.astype(np.int64), hcnt.astype(np.int64))])
-    distinct = np.unique(hs[idx]).size
-    parts = int(min(2048, max(8, round(distinct / (6348 * frac) / 8) * 8)))
-    m0 = synth.m0(cfg, 2048, 100000)
-    st = compare(gpu, m0, hb, dev_batch(gpu, cfg, nprog, cpp, cl), agg=2, parts=parts)
-    assert st["parts"] == parts and st["distinct"] == distinct
-    if frac < 1:
-        assert st["overflow_parts"] == 0, st
-    elif frac > 10:
-        assert st["overflow_parts"] == parts, st
-    else:
-        assert 0 < st["overflow_parts"] < parts, st
+
+def fmix32_inv_np(h):
+    """Inverse of murmur3 fmix32 (csrc/agg.hip fmix32_inv), on a u32 array."""
+    h = np.asarray(h, np.uint32).copy()
+    h ^= h >> np.uint32(16)
+    h *= np.uint32(0x7ED1B41D)
+    h ^= (h >> np.uint32(13)) ^ (h >> np.uint32(26))
+    h *= np.uint32(0xA5CB9243)
+    h ^= h >> np.uint32(16)
+    return h
+
+
+@pytest.mark.parametrize("over", [(0,) * 8, (1, 0, 0, 1, 0, 1, 1, 0), (1,) * 8])
+def test_triage_agg_lds_overflow_fallback(gpu, over):
+    """8 partitions (the top 3 bits of h = fmix32(e)); partition p gets
+    kAggLimit + 300 distinct elements when over[p] (it overflows the LDS table
+    and is redone in the HBM table) or kAggLimit - 300.  h = 0 and
+    h = 0xFFFFFFFF (the HBM table's extra slot) are among the elements."""
+    rng = np.random.default_rng(sum(over) + 11)
+    pools = []
+    for p, o in enumerate(over):
+        n = AGG_LIMIT + 300 if o else AGG_LIMIT - 300
+        low = rng.choice(1 << 29, size=n, replace=False).astype(np.uint32)
+        pools.append((np.uint32(p) << np.uint32(29)) | low)
+    pools[0][0] = 0
+    pools[7][0] = 0xFFFFFFFF
+    h = np.concatenate(pools)
+    assert np.unique(h).size == h.size
+    elems = fmix32_inv_np(h)
+    # calls: every element once in a shuffled pass, then random repeats
+    ncalls = 600
+    stream = np.concatenate([rng.permutation(elems), rng.choice(elems, size=elems.size * 2)])
+    cuts = np.sort(rng.choice(np.arange(1, stream.size), size=ncalls - 1, replace=False))
+    hcs = np.concatenate([[0], cuts]).astype(np.uint64)
+    hcnt = np.diff(np.concatenate([hcs, [stream.size]])).astype(np.uint32)
+    hprio = rng.integers(0, 4, size=ncalls).astype(np.uint8)
+    hs = stream.astype(np.uint32)
+    m0e = np.concatenate([rng.choice(elems, size=5000, replace=False), rng.integers(0, 1 << 32, 3000, np.uint64)])
+    m0e = np.unique(m0e.astype(np.uint32))
+    m0p = rng.integers(0, 4, size=m0e.size).astype(np.int8)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(gpu.dev)  # noqa: E731
+    db = (t(hs, np.int32), t(hcs, np.int64), t(hcnt, np.int32), t(hprio, np.uint8))
+    st = compare(gpu, (m0e, m0p), (hs, hcs, hcnt, hprio), db, agg=2, parts=8)
+    assert st["parts"] == 8 and st["distinct"] == elems.size
+    assert st["overflow_parts"] == sum(over), st
 
 
 @pytest.mark.parametrize("agg", [0, 2])
