@@ -32,6 +32,8 @@ PROBE_BYTES_PER_REC = 12.0  # 4 B element read + 8 B maxSignal slot read (SURVEY
 # the K3 pipeline of one step on one GPU (csrc/agg.hip); roofline.avg_launch_ms is
 # their summed device time (HIP events), roofline.traffic their summed PMC bytes
 K3_KERNELS = "k_agg_count+k_agg_scan_chunks+k_agg_scan_totals+k_agg_scatter+k_agg+k_agg_finalize"
+# N > 1: the source's aggregation, then the owner's records-mode triage of the staircases
+K3_DIST_KERNELS = "k_agg_count+k_agg_scan_chunks+k_agg_scan_totals+k_agg_scatter+k_agg+k_probe+k_decide"
 
 
 def parse():
@@ -170,22 +172,27 @@ def main():
         ms = sized
     pristine = ms.clone()
     ns = S.Signal.make(4_000_000, dev.eng)
+    # checkNewSignal's outputs: the calls with new signal, every call's DiffRaw
+    # result (pairs), maxSignal and newSignal (per-record bits are not part of
+    # the reference's result and are not computed)
+    pairs = torch.empty(16 << 20, dtype=torch.int64, device=dev.dev)
+    b, bits, cnew = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
     if distributed:
-        b, bits, cnew = dev.batch(sigs, cs, cnt, prio)
-    else:
-        # checkNewSignal's outputs: the calls with new signal, every call's DiffRaw
-        # result (pairs), maxSignal and newSignal (per-record bits are not part of
-        # the reference's result and are not computed)
-        pairs = torch.empty(16 << 20, dtype=torch.int64, device=dev.dev)
-        b, bits, cnew = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
-    if distributed:
-        sharded = ShardedTriage(GpuShardOps(dev), ms, ns)
+        ops = GpuShardOps(dev)
+        sharded = ShardedTriage(ops, ms, ns)
 
     def step():
         ms.copy_from(pristine)
         ns.clear()
         if distributed:
-            return sharded.step((b, bits, cnew), prio, rank * P * C)[2]
+            st = dict(sharded.step((b, bits, cnew), prio, rank * P * C)[2])
+            src = ops.last_source_stats
+            # source-side aggregation, then the owner's records-mode triage
+            st["decide_ms"] = st["probe_ms"] + st["decide_ms"]
+            for k in ("part_ms", "probe_ms", "distinct", "parts", "overflow_parts"):
+                st[k] = src[k]
+            st["records"] = src["records"]
+            return st
         return dev.triage_b(ms, ns, b)
 
     for _ in range(a.warmup):
@@ -216,7 +223,7 @@ def main():
     decide_ms = float(np.mean([s["decide_ms"] for s in stats]))
     part_ms = float(np.mean([s["part_ms"] for s in stats]))
     k3_ms = part_ms + probe_ms + decide_ms
-    probe_units = s0["received"] if distributed else nrec
+    probe_units = nrec
     # roofline over the whole K3 pipeline (every kernel between the records in
     # HBM and the updated sets), not one kernel of it
     achieved = PROBE_BYTES_PER_REC * probe_units / (k3_ms * 1e-3) / 1e9
@@ -242,7 +249,8 @@ def main():
                        "records_per_gpu": nrec, "pcs_per_gpu": npc, "skew": a.skew,
                        "table_slots": ms.capacity(),
                        "parallelism": f"shard{world}" if distributed else "single"},
-            "roofline": {"bound": "hbm", "kernel": K3_KERNELS if not distributed else "k_probe+k_decide (records)",
+            "roofline": {"bound": "hbm",
+                         "kernel": K3_KERNELS if not distributed else K3_DIST_KERNELS,
                          "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": probe_units,

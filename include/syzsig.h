@@ -211,6 +211,27 @@ int syzsig_triage_records_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set** n
 int syzsig_shard_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* d_send_pos,
                                  const uint8_t* d_back_flags);
 
+/* Aggregated routing (the large-batch form of the two calls above).  The
+ * source aggregates its records per element and sends only each element's
+ * staircase -- for every level, the element's first record at that level if
+ * no earlier local record has a higher level -- at most 4 records per
+ * distinct element, packed and grouped by owner as above (records-mode triage
+ * on the owners is unchanged).  Records that are off the staircase can never
+ * be new nor raise maxSignal, so the result is the same as routing every
+ * record.  d_send needs room for the batch's record count (an upper bound);
+ * send_counts[g] = records for owner g, packed at their exclusive prefix sum.
+ * stats: records, distinct, parts and timings of the local aggregation;
+ * candidates = staircase records sent. */
+int syzsig_shard_agg_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
+                                   const int8_t* levels, uint32_t nlevels, uint32_t nshards, uint64_t* d_send,
+                                   uint64_t send_cap, uint64_t* send_counts, syzsig_batch_stats* stats);
+/* Source side of the aggregated routing: the owners' flags for d_send[0 .. n_send)
+ * -> b->call_new, b->new_bits (if set), b->new_pairs (if set; stats->new_pairs
+ * = the total).  serial_base as given to the partition call. */
+int syzsig_shard_agg_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
+                                     const uint64_t* d_send, uint64_t n_send, const uint8_t* d_back_flags,
+                                     syzsig_batch_stats* stats);
+
 /* ---- synthetic workload (deterministic; host and device give identical data) ---- */
 typedef struct {
 	uint64_t seed;

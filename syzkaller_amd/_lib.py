@@ -90,6 +90,10 @@ SIGNATURES = {
     "syzsig_triage_records_dev": (c_int, [_P, _P, _PP, _P, c_uint64, _P, c_uint32, _P,
                                           POINTER(BatchStats)]),
     "syzsig_shard_unpartition_dev": (c_int, [_P, POINTER(Batch), _P, _P]),
+    "syzsig_shard_agg_partition_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint32, c_uint32, _P, c_uint64,
+                                               _P, POINTER(BatchStats)]),
+    "syzsig_shard_agg_unpartition_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint64, _P,
+                                                 POINTER(BatchStats)]),
     "syzsig_synth_default": (None, [POINTER(SynthCfg)]),
     "syzsig_synth_traces_host": (c_int, [POINTER(SynthCfg), c_uint64, c_uint64, c_uint32, _P, _P, _P, _P]),
     "syzsig_synth_traces_dev": (c_int, [_P, POINTER(SynthCfg), c_uint64, c_uint64, c_uint32, _P, _P, _P, _P]),

@@ -857,7 +857,7 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	const AggGeom g = agg_geom_for(ctx, run_recs);
 	const uint32_t P = 1u << g.pbits;
 	const uint64_t nchunks = (c1 - c0 + (1ull << g.cbits()) - 1) >> g.cbits();
-	void *recs, *cm, *pm, *de, *df, *dc, *pr;
+	void *recs, *cm, *pm, *de, *df, *dc;
 	SYZ_TRY(ws_get(ctx, 16, run_recs * 4 + 64, &recs));
 	SYZ_TRY(ws_get(ctx, 17, (2 * nchunks * P + (uint64_t)P * (nchunks + 1)) * 4 + 64, &cm));
 	SYZ_TRY(ws_get(ctx, 18, (kAggMaxParts + 1) * 8 * 2, &pm));
@@ -966,6 +966,25 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	st->parts = P;
 	st->survivors += D;
 	ctx->agg_distinct_ratio = run_recs ? (double)D / (double)run_recs : 0;
+	out->dist_e = (const uint32_t*)dist_e;
+	out->dist_f = (const uint4*)dist_f;
+	out->cnt = (const uint32_t*)dc;
+	out->nregions = nregions;
+	out->D = D;
+	return SYZSIG_OK;
+}
+
+// One run of calls [c0, c1) with level map lm.  Pairs are appended at
+// pairs[*npairs_io ...] (internal buffer, grown as needed).
+int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,
+                   const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs_out,
+                   uint64_t* npairs_io)
+{
+	AggOut a;
+	SYZ_TRY(agg_aggregate(ctx, b, c0, c1, lm, run_recs, st, &a));
+	const uint64_t D = a.D;
+	const hipStream_t s = ctx->stream;
+	void* pr;
 	// capacity for every possible change, then finalize (never retried)
 	SYZ_TRY(set_reserve(ms, D));
 	// newSignal.Merge allocates a nil receiver (signal.go:121-125) -- but only
@@ -984,8 +1003,8 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
 	if (D)
-		k_agg_finalize<<<nregions, kFinThreads, 0, s>>>(
-		    (const uint32_t*)dist_e, (const uint4*)dist_f, (const uint32_t*)dc, nregions, lm, c0, ms->slots,
+		k_agg_finalize<<<a.nregions, kFinThreads, 0, s>>>(
+		    a.dist_e, a.dist_f, a.cnt, a.nregions, lm, c0, ms->slots,
 		    ms->nbuckets - 1, nsp ? nsp->slots : nullptr, nsp ? nsp->nbuckets - 1 : 0, b->call_new, (uint64_t*)pr,
 		    &ctx->d_cnt[kCntAux2], ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
@@ -1067,4 +1086,228 @@ int pairs_from_bits(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* bits
 	return SYZSIG_OK;
 }
 
+// ---------------------------------------------------------------- sharded batches
+// A GPU's batch is aggregated locally and only each distinct element's
+// staircase is routed to the element's owner: level l with first serial f[l]
+// is on it iff f[l] < f[l'] for every higher level l'.  Any other record of e
+// has an earlier local record of at least its level, so it is never new and
+// never raises M_final -- and whatever dominates a staircase record in the
+// whole batch, some staircase record (of any GPU) dominates it too.  So the
+// owner's records-mode triage of the staircases gives checkNewSignal's exact
+// result, at <= 4 records per distinct element instead of every record
+// (SURVEY.md 8(e) "local filter").
+constexpr uint32_t kMaxShardsAgg = 64;
+
+__device__ __forceinline__ uint32_t stair_levels(uint4 f4, uint32_t nlev)
+{
+	const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
+	uint32_t m = 0, mk = kAggNone;
+#pragma unroll
+	for (int l = 3; l >= 0; l--)
+		if (l < (int)nlev && f[l] < mk) {
+			mk = f[l];
+			m |= 1u << l;
+		}
+	return m;
+}
+
+// staircase records per owner (block histogram, one atomic per owner per block)
+__global__ __launch_bounds__(256) void k_stair_count(const uint32_t* __restrict__ dist_e,
+                                                     const uint4* __restrict__ dist_f,
+                                                     const uint32_t* __restrict__ cnt, uint32_t nregions,
+                                                     uint32_t nlev, uint32_t nshards, unsigned long long* counts)
+{
+	__shared__ uint32_t h[kMaxShardsAgg];
+	if (threadIdx.x < kMaxShardsAgg)
+		h[threadIdx.x] = 0;
+	__syncthreads();
+	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
+		const uint32_t n = cnt[r] == kAggOverflow ? 0 : cnt[r];
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+			const uint64_t o = (uint64_t)r * kAggRegion + i;
+			const uint32_t m = stair_levels(dist_f[o], nlev);
+			if (m)
+				atomicAdd(&h[owner_of(dist_e[o], nshards)], (uint32_t)__popc(m));
+		}
+	}
+	__syncthreads();
+	if (threadIdx.x < nshards && h[threadIdx.x])
+		atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+// staircase records -> send[], grouped by owner (cursor[g] = next free slot of g)
+__global__ __launch_bounds__(256) void k_stair_scatter(const uint32_t* __restrict__ dist_e,
+                                                       const uint4* __restrict__ dist_f,
+                                                       const uint32_t* __restrict__ cnt, uint32_t nregions,
+                                                       uint32_t nlev, uint32_t nshards, uint64_t serial_base,
+                                                       unsigned long long* cursor, uint64_t* send)
+{
+	__shared__ uint32_t h[kMaxShardsAgg];
+	__shared__ unsigned long long base[kMaxShardsAgg];
+	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
+		if (threadIdx.x < kMaxShardsAgg)
+			h[threadIdx.x] = 0;
+		__syncthreads();
+		const uint32_t n = cnt[r] == kAggOverflow ? 0 : cnt[r];
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+			const uint64_t o = (uint64_t)r * kAggRegion + i;
+			const uint32_t m = stair_levels(dist_f[o], nlev);
+			if (m)
+				atomicAdd(&h[owner_of(dist_e[o], nshards)], (uint32_t)__popc(m));
+		}
+		__syncthreads();
+		if (threadIdx.x < nshards) {
+			base[threadIdx.x] = h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)h[threadIdx.x]) : 0;
+			h[threadIdx.x] = 0;
+		}
+		__syncthreads();
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+			const uint64_t o = (uint64_t)r * kAggRegion + i;
+			const uint4 f4 = dist_f[o];
+			const uint32_t m = stair_levels(f4, nlev);
+			if (!m)
+				continue;
+			const uint32_t e = dist_e[o], g = owner_of(e, nshards);
+			const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
+			uint64_t pos = base[g] + atomicAdd(&h[g], (uint32_t)__popc(m));
+#pragma unroll
+			for (uint32_t l = 0; l < 4; l++)
+				if ((m >> l) & 1)
+					send[pos++] = ((uint64_t)e << 32) | ((uint64_t)l << 24) | ((serial_base + f[l]) & kSerialMask);
+		}
+		__syncthreads();
+	}
+}
+
+// The owners' flags back at the source: a flagged staircase record (e, serial)
+// is the pair (call = serial - serial_base, e) of that call's DiffRaw result.
+__global__ __launch_bounds__(256) void k_stair_back(const uint64_t* __restrict__ send,
+                                                    const uint8_t* __restrict__ back, uint64_t n,
+                                                    uint64_t serial_base, uint8_t* call_new, uint64_t* pairs,
+                                                    unsigned long long* npairs)
+{
+	const uint32_t lane = lane_id();
+	for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t i = i0 + threadIdx.x;
+		const bool on = i < n && back[i];
+		uint64_t v = 0;
+		if (on) {
+			const uint64_t r = send[i];
+			const uint64_t c = (r & kSerialMask) - serial_base;
+			call_new[c] = 1;
+			v = (c << 32) | (r >> 32);
+		}
+		const uint64_t m = __ballot(on);
+		unsigned long long wb = 0;
+		if (lane == 0 && m)
+			wb = atomicAdd(npairs, (unsigned long long)__popcll(m));
+		wb = __shfl(wb, 0, 64);
+		if (on)
+			pairs[wb + lane_rank(m)] = v;
+	}
+}
+
 }  // namespace syz
+
+using namespace syz;
+
+extern "C" {
+
+int syzsig_shard_agg_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
+                                   const int8_t* levels, uint32_t nlevels, uint32_t nshards, uint64_t* d_send,
+                                   uint64_t send_cap, uint64_t* send_counts, syzsig_batch_stats* stats)
+{
+	if (!ctx || !b || !send_counts || (b->nrec && !b->sigs) || (send_cap && !d_send) ||
+	    (b->ncalls && (!b->call_start || !b->call_len || !b->call_prio)))
+		return fail(SYZSIG_EINVAL, "shard_agg_partition: NULL argument");
+	if (nshards == 0 || nshards > kMaxShardsAgg)
+		return fail(SYZSIG_EINVAL, "shard_agg_partition: nshards must be 1..64");
+	if (b->nrec >= (1ull << 32))
+		return fail(SYZSIG_ERANGE, "shard_agg_partition: >= 2^32 records per GPU");
+	if (serial_base + b->ncalls > kSerialMask + 1ull)
+		return fail(SYZSIG_ERANGE, "shard_agg_partition: batch serial order exceeds 2^24 calls");
+	LevelMap lm;
+	SYZ_TRY(level_map_from_levels(levels, nlevels, &lm));
+	for (uint32_t i = 0; i < nshards; i++)
+		send_counts[i] = 0;
+	syzsig_batch_stats st;
+	memset(&st, 0, sizeof(st));
+	if (b->ncalls) {
+		uint64_t total = 0;
+		uint32_t mask[8];
+		SYZ_TRY(batch_total_records(ctx, b, &total, mask));
+		for (int p = 0; p < 256; p++)
+			if (((mask[p >> 5] >> (p & 31)) & 1) && lm.lvl[p] == 0xff)
+				return fail(SYZSIG_EINVAL, "shard_agg_partition: a call's prio is not among `levels`");
+		st.records = total;
+		if (total) {
+			AggOut a;
+			SYZ_TRY(agg_aggregate(ctx, b, 0, b->ncalls, lm, total, &st, &a));
+			const hipStream_t s = ctx->stream;
+			void* dcur;
+			SYZ_TRY(ws_get(ctx, 6, 2 * kMaxShardsAgg * 8, &dcur));
+			unsigned long long* counts = (unsigned long long*)dcur;
+			unsigned long long* cursor = counts + kMaxShardsAgg;
+			SYZ_HIP(hipMemsetAsync(counts, 0, kMaxShardsAgg * 8, s));
+			const int grid = (int)std::min<uint32_t>(a.nregions, 2048);
+			k_stair_count<<<grid, 256, 0, s>>>(a.dist_e, a.dist_f, a.cnt, a.nregions, lm.n, nshards, counts);
+			SYZ_HIP(hipGetLastError());
+			unsigned long long h[kMaxShardsAgg];
+			SYZ_HIP(hipMemcpyAsync(h, counts, nshards * 8, hipMemcpyDeviceToHost, s));
+			SYZ_HIP(hipStreamSynchronize(s));
+			unsigned long long off[kMaxShardsAgg], run = 0;
+			for (uint32_t i = 0; i < nshards; i++) {
+				off[i] = run;
+				run += h[i];
+				send_counts[i] = h[i];
+			}
+			st.candidates = run;
+			if (run > send_cap)
+				return fail(SYZSIG_ERANGE, "shard_agg_partition: send buffer too small (records suffice)");
+			SYZ_HIP(hipMemcpyAsync(cursor, off, nshards * 8, hipMemcpyHostToDevice, s));
+			k_stair_scatter<<<grid, 256, 0, s>>>(a.dist_e, a.dist_f, a.cnt, a.nregions, lm.n, nshards, serial_base,
+			                                     cursor, d_send);
+			SYZ_HIP(hipGetLastError());
+			SYZ_HIP(hipStreamSynchronize(s));
+		}
+	}
+	if (stats)
+		*stats = st;
+	return SYZSIG_OK;
+}
+
+int syzsig_shard_agg_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
+                                     const uint64_t* d_send, uint64_t n_send, const uint8_t* d_back_flags,
+                                     syzsig_batch_stats* stats)
+{
+	if (!ctx || !b || (n_send && (!d_send || !d_back_flags)) || (b->ncalls && !b->call_new) ||
+	    (b->new_pairs_cap && !b->new_pairs))
+		return fail(SYZSIG_EINVAL, "shard_agg_unpartition: NULL argument");
+	const hipStream_t s = ctx->stream;
+	if (b->new_bits)
+		SYZ_HIP(hipMemsetAsync(b->new_bits, 0, ((b->nrec + 31) / 32) * 4, s));
+	if (b->ncalls)
+		SYZ_HIP(hipMemsetAsync(b->call_new, 0, b->ncalls, s));
+	uint64_t np = 0;
+	if (n_send && b->ncalls) {
+		void* pr;
+		SYZ_TRY(ws_get(ctx, 15, n_send * 8 + 64, &pr));
+		SYZ_TRY(counters_reset(ctx));
+		k_stair_back<<<grid_for(n_send, 256, 8192), 256, 0, s>>>(d_send, d_back_flags, n_send, serial_base,
+		                                                          b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2]);
+		SYZ_HIP(hipGetLastError());
+		SYZ_TRY(counters_fetch(ctx));
+		np = ctx->h_cnt[kCntAux2];
+		SYZ_TRY(agg_mark_bits(ctx, b, 0, b->ncalls, (const uint64_t*)pr, 0, np));
+		if (b->new_pairs && np)
+			SYZ_HIP(hipMemcpyAsync(b->new_pairs, pr, std::min(np, b->new_pairs_cap) * 8, hipMemcpyDeviceToDevice, s));
+	}
+	SYZ_HIP(hipStreamSynchronize(s));
+	if (stats) {
+		memset(stats, 0, sizeof(*stats));
+		stats->new_pairs = np;
+	}
+	return SYZSIG_OK;
+}
+
+}  // extern "C"

@@ -117,6 +117,17 @@ constexpr uint32_t kSerialMask = 0xFFFFFF;  // 24-bit serial index inside a run
 int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm);
 
 // aggregation path (agg.hip)
+struct AggOut {
+	const uint32_t* dist_e;  // distinct elements; region r at [r * kAggRegion, + cnt[r])
+	const uint4* dist_f;     // their first serial per level (0xFFFFFFFF = none)
+	const uint32_t* cnt;     // per region, device
+	uint32_t nregions;
+	uint64_t D;              // distinct elements in all regions
+};
+int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const LevelMap& lm,
+                  uint64_t run_recs, syzsig_batch_stats* st, AggOut* out);
+// validates a batch's call ranges (SYZSIG_EINVAL) and sums its records (triage.hip)
+int batch_total_records(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t* total, uint32_t prio_mask[8]);
 int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,
                    const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs,
                    uint64_t* npairs);

@@ -445,7 +445,7 @@ static void level_map_from(const bool present[256], LevelMap* lm)
 	lm->n = n;
 }
 
-static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* runs, uint64_t* total_recs)
+int batch_total_records(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t* total, uint32_t prio_mask[8])
 {
 	void* dmask;
 	SYZ_TRY(ws_get(ctx, 6, 64, &dmask));
@@ -457,11 +457,20 @@ static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* r
 	uint32_t hmask[12];
 	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 48, hipMemcpyDeviceToHost, ctx->stream));
 	SYZ_HIP(hipStreamSynchronize(ctx->stream));
-	memcpy(total_recs, &hmask[8], 8);
+	memcpy(total, &hmask[8], 8);
 	uint64_t nbad;
 	memcpy(&nbad, &hmask[10], 8);
 	if (nbad)
 		return fail(SYZSIG_EINVAL, "triage_batch: a call range lies outside [0, nrec) or has >= 2^24 records");
+	if (prio_mask)
+		memcpy(prio_mask, hmask, 32);
+	return SYZSIG_OK;
+}
+
+static int plan_runs(syzsig_ctx* ctx, const syzsig_batch* b, std::vector<Run>* runs, uint64_t* total_recs)
+{
+	uint32_t hmask[8];
+	SYZ_TRY(batch_total_records(ctx, b, total_recs, hmask));
 	bool present[256];
 	int np = 0;
 	for (int i = 0; i < 256; i++) {

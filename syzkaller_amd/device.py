@@ -147,6 +147,25 @@ class Device:
     def shard_unpartition(self, b, send_pos, back_flags):
         check(self.L.syzsig_shard_unpartition_dev(self.eng.h, ctypes.byref(b), _p(send_pos), _p(back_flags)))
 
+    def shard_agg_partition(self, b, serial_base, levels, nshards, send):
+        """Aggregated routing: each distinct element's staircase records, grouped
+        by owner, into send (int64, >= b.nrec entries).  -> (counts, stats)."""
+        self._check_dev(send)
+        lv = (ctypes.c_int8 * len(levels))(*levels)
+        counts = (ctypes.c_uint64 * nshards)()
+        st = BatchStats()
+        check(self.L.syzsig_shard_agg_partition_dev(self.eng.h, ctypes.byref(b), int(serial_base), lv, len(levels),
+                                                    int(nshards), _p(send), send.numel(), counts, ctypes.byref(st)))
+        return [int(c) for c in counts], st.as_dict()
+
+    def shard_agg_unpartition(self, b, serial_base, send, back_flags):
+        """The owners' flags for send -> b's call_new / new_bits / new_pairs."""
+        self._check_dev(send, back_flags)
+        st = BatchStats()
+        check(self.L.syzsig_shard_agg_unpartition_dev(self.eng.h, ctypes.byref(b), int(serial_base), _p(send),
+                                                      send.numel(), _p(back_flags), ctypes.byref(st)))
+        return st.as_dict()
+
     # ---------------------------------------------------------------- synthetic data
     def synth_traces(self, cfg, prog_base, nprog, calls_per_prog, call_len):
         """-> (pcs int64[sum], call_start int64[n], call_prio uint8[n]) for nprog programs."""

@@ -7,11 +7,13 @@ fuzzer would see them).  maxSignal is partitioned by element:
 shard(e) = owner_of(e, world) (csrc/common.h).  One step:
 
   1. levels  = union of every rank's call prios          (all_reduce, 256 ints)
-  2. partition records by owner                          (shard.hip)
+  2. aggregate the rank's records per element and keep
+     each element's staircase, grouped by owner           (agg.hip; shard.hip
+                                                           routes every record)
   3. exchange counts, then records                       (all_to_all_single)
   4. owner triages the records it received               (triage.hip, records mode)
   5. new-flags travel back to the sources                (all_to_all_single)
-  6. sources scatter flags to record bits / call flags   (shard.hip)
+  6. sources turn flags into call flags / pairs / bits   (agg.hip or shard.hip)
 
 Only step 3/5 move data between GPUs; each element's whole history in the
 batch lands on one owner, which applies the exact serial semantics via the
@@ -42,14 +44,28 @@ def owner_of_torch(elems, nshards):
 
 
 class GpuShardOps:
-    """The device half of a sharded step, on libsyzsig."""
+    """The device half of a sharded step, on libsyzsig.
 
-    def __init__(self, dev):
+    aggregate=True (default): the source aggregates its batch per element and
+    sends only the staircase records (agg.hip, <= 4 per distinct element);
+    False: every record is sent (shard.hip).  Both give the same result."""
+
+    def __init__(self, dev, aggregate=True):
         self.dev = dev
+        self.aggregate = aggregate
+        self._send = None
+        self.last_source_stats = {}
 
     def partition(self, batch, serial_base, levels, nshards):
         b, new_bits, call_new = batch
         n = b.nrec
+        if self.aggregate:
+            if self._send is None or self._send.numel() < max(n, 1):
+                self._send = torch.empty(max(n, 1), dtype=torch.int64, device=self.dev.dev)
+            counts, st = self.dev.shard_agg_partition(b, serial_base, levels, nshards, self._send)
+            self.last_source_stats = st
+            send = self._send[: sum(counts)]
+            return send, (send, serial_base), counts
         send = torch.empty(n, dtype=torch.int64, device=self.dev.dev)
         send_pos = torch.empty(n, dtype=torch.int32, device=self.dev.dev)
         counts = self.dev.shard_partition(b, serial_base, levels, nshards, send, send_pos)
@@ -60,9 +76,13 @@ class GpuShardOps:
         st = self.dev.triage_records(shard, new_signal, recs, levels, flags)
         return flags, st
 
-    def unpartition(self, batch, send_pos, back):
+    def unpartition(self, batch, token, back):
         b, new_bits, call_new = batch
-        self.dev.shard_unpartition(b, send_pos, back)
+        if self.aggregate:
+            send, serial_base = token
+            self.dev.shard_agg_unpartition(b, serial_base, send, back)
+        else:
+            self.dev.shard_unpartition(b, token, back)
         return new_bits, call_new
 
 
@@ -92,7 +112,7 @@ class ShardedTriage:
             raise ValueError("sharded triage supports <= 4 distinct prios per batch (signalPrio gives 0..3)")
         if not levels:
             levels = [0]
-        send, send_pos, counts = self.ops.partition(batch, serial_base, levels, self.world)
+        send, token, counts = self.ops.partition(batch, serial_base, levels, self.world)
         dev = send.device
         cnt_out = torch.tensor(counts, dtype=torch.int64, device=dev)
         cnt_in = torch.empty_like(cnt_out)
@@ -103,7 +123,7 @@ class ShardedTriage:
         flags, st = self.ops.triage_records(self.shard, self.new_signal, recv, levels)
         back = torch.empty(send.numel(), dtype=torch.uint8, device=dev)
         dist.all_to_all_single(back, flags, counts, recv_counts, group=self.group)
-        new_bits, call_new = self.ops.unpartition(batch, send_pos, back)
+        new_bits, call_new = self.ops.unpartition(batch, token, back)
         st = dict(st)
         st["sent"] = int(send.numel())
         st["received"] = int(recv.numel())

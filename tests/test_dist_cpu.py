@@ -65,6 +65,45 @@ class NumpyShardOps:
         return bits, cnew
 
 
+class NumpyStairOps(NumpyShardOps):
+    """The aggregated routing of agg.hip restated: per element, the first call
+    at each level; only the staircase (a level's first call precedes every
+    higher level's) is sent; flags come back as (call, elem) pairs."""
+
+    def partition(self, batch, serial_base, levels, nshards):
+        sigs, cs, cl, prio = batch["sigs"], batch["call_start"], batch["call_len"], batch["call_prio"]
+        lvl = {(v & 0xFF): i for i, v in enumerate(levels)}
+        first = {}
+        for c in range(cl.size):
+            lv = lvl[int(prio[c])]
+            for j in range(int(cl[c])):
+                f = first.setdefault(int(sigs[int(cs[c]) + j]), [None] * 4)
+                if f[lv] is None:
+                    f[lv] = c
+        groups = [[] for _ in range(nshards)]
+        for e, f in first.items():
+            mk = None
+            for lv in range(3, -1, -1):
+                if f[lv] is not None and (mk is None or f[lv] < mk):
+                    mk = f[lv]
+                    groups[_owner(e, nshards)].append((e << 32) | (lv << 24) | ((serial_base + f[lv]) & SER))
+        send = np.array([r for g in groups for r in g], dtype=np.uint64)
+        return torch.from_numpy(send.view(np.int64).copy()), (send, serial_base), [len(g) for g in groups]
+
+    def unpartition(self, batch, token, back):
+        send, serial_base = token
+        pairs = {((int(send[i]) & SER) - serial_base, int(send[i]) >> 32) for i in np.nonzero(back.numpy())[0]}
+        sigs, cs, cl = batch["sigs"], batch["call_start"], batch["call_len"]
+        bits = np.zeros(sigs.size, np.uint8)
+        cnew = np.zeros(cl.size, np.uint8)
+        for c in range(cl.size):
+            for j in range(int(cl[c])):
+                if (c, int(sigs[int(cs[c]) + j])) in pairs:
+                    bits[int(cs[c]) + j] = 1
+                    cnew[c] = 1
+        return bits, cnew
+
+
 def make_rank_batch(rank, ncalls, seed):
     rng = np.random.default_rng(seed + rank)
     cl = rng.integers(0, 40, size=ncalls).astype(np.uint32)
@@ -81,14 +120,14 @@ def m0_global(seed):
     return {int(x): int(rng.integers(0, 4)) for x in e}
 
 
-def worker(rank, world, port, outdir, ncalls, seed):
+def worker(rank, world, port, outdir, ncalls, seed, stair):
     from syzkaller_amd.dist import ShardedTriage
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     batch = make_rank_batch(rank, ncalls, seed)
     shard = {e: p for e, p in m0_global(seed).items() if _owner(e, world) == rank}
     news = {}
-    st = ShardedTriage(NumpyShardOps(), shard, news)
+    st = ShardedTriage(NumpyStairOps() if stair else NumpyShardOps(), shard, news)
     bits, cnew, stats = st.step(batch, torch.from_numpy(batch["call_prio"]), rank * ncalls)
     json.dump({"bits": bits.tolist(), "cnew": cnew.tolist(), "shard": shard, "new": news, "stats": stats},
               open(os.path.join(outdir, f"r{rank}.json"), "w"))
@@ -103,13 +142,16 @@ def free_port():
     return p
 
 
+@pytest.mark.parametrize("stair", [False, True])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_sharded_step_equals_sequential_checknewsignal(seed):
+def test_sharded_step_equals_sequential_checknewsignal(seed, stair):
+    """stair: route only each element's staircase (the aggregated routing)."""
     from oracle import oracle as O
 
     world, ncalls = 2, 60
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(worker, args=(world, free_port(), d, ncalls, seed), nprocs=world, start_method="spawn")
+        mp.start_processes(worker, args=(world, free_port(), d, ncalls, seed, stair), nprocs=world,
+                           start_method="spawn")
         res = [json.load(open(os.path.join(d, f"r{r}.json"))) for r in range(world)]
     # sequential reference over the concatenated batch (rank-major serial order)
     parts = [make_rank_batch(r, ncalls, seed) for r in range(world)]
@@ -136,4 +178,6 @@ def test_sharded_step_equals_sequential_checknewsignal(seed):
     for r in res:
         nm.update({int(k): v for k, v in r["new"].items()})
     assert nm == ns.to_dict()
-    assert sum(r["stats"]["sent"] for r in res) == sum(r["stats"]["received"] for r in res) == sigs.size
+    sent = sum(r["stats"]["sent"] for r in res)
+    assert sent == sum(r["stats"]["received"] for r in res)
+    assert sent < sigs.size if stair else sent == sigs.size

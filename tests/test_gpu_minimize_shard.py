@@ -93,6 +93,76 @@ def test_shard_routing_equals_unsharded(gpu, nshards):
     assert nmerged == ns.to_dict()
 
 
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_shard_agg_routing_equals_unsharded(gpu, nshards):
+    """The aggregated routing on one GPU: G sources (program ranges of one
+    batch) each send their staircase records (agg.hip) to G owner shards; the
+    owners triage in records mode, flags come back, and the union of the
+    sources' call flags / record bits / pairs and of the shards equals plain
+    triage of the whole batch against the unsharded maxSignal."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+    from tests.test_gpu_triage import dev_batch, oracle_pairs
+
+    cfg = synth.synth_default(skew=1)
+    nprog, cpp = 48, 32
+    cl = synth.call_lengths(nprog, cpp, 0, ragged=(0, 3000), seed=nshards + 7)
+    ds, dcs, dcnt, dprio = dev_batch(gpu, cfg, nprog, cpp, cl)
+    m0e, m0p = synth.m0(cfg, 1024, 80000)
+    ms = S.Serial(m0e, m0p).Deserialize(gpu.eng)
+    ns = S.Signal(None, gpu.eng)
+    bits, cnew, _ = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
+    owner = np.array([_owner(int(x), nshards) for x in m0e], np.uint32)
+    shards = [S.Serial(m0e[owner == g], m0p[owner == g]).Deserialize(gpu.eng) for g in range(nshards)]
+    news = [S.Signal(None, gpu.eng) for _ in range(nshards)]
+    levels = sorted(set(int(x) for x in dprio.cpu().numpy().astype(np.int8)))
+    ncalls = nprog * cpp
+    bounds = [ncalls * s // nshards for s in range(nshards + 1)]
+    src = []
+    for s in range(nshards):
+        a, z = bounds[s], bounds[s + 1]
+        pairs = torch.full((int(dcnt[a:z].sum()) + 1,), -1, dtype=torch.int64, device=gpu.dev)
+        b, sbits, scnew = gpu.batch(ds, dcs[a:z].contiguous(), dcnt[a:z].contiguous(), dprio[a:z].contiguous(),
+                                    new_pairs=pairs)
+        send = torch.empty(ds.numel(), dtype=torch.int64, device=gpu.dev)
+        counts, st = gpu.shard_agg_partition(b, a, levels, nshards, send)
+        assert st["candidates"] == sum(counts) <= st["records"]
+        off = np.concatenate([[0], np.cumsum(counts)])
+        src.append((b, sbits, scnew, pairs, send[: off[-1]], off))
+    # owners: records of every source, in source order
+    flags = []
+    for g in range(nshards):
+        recv = torch.cat([x[4][x[5][g]: x[5][g + 1]] for x in src])
+        f = torch.zeros(recv.numel(), dtype=torch.uint8, device=gpu.dev)
+        if recv.numel():
+            gpu.triage_records(shards[g], news[g], recv, levels, f)
+        flags.append(f)
+    got_bits = torch.zeros_like(bits)
+    got_pairs = []
+    for s, (b, sbits, scnew, pairs, send, off) in enumerate(src):
+        lens = [int(off[g + 1] - off[g]) for g in range(nshards)]
+        starts = [sum(int(x[5][g + 1] - x[5][g]) for x in src[:s]) for g in range(nshards)]
+        back = torch.cat([flags[g][starts[g]: starts[g] + lens[g]] for g in range(nshards)])
+        st = gpu.shard_agg_unpartition(b, bounds[s], send, back)
+        got_bits |= sbits
+        assert torch.equal(scnew, cnew[bounds[s]: bounds[s + 1]])
+        p = pairs[: st["new_pairs"]].cpu().numpy().view(np.uint64)
+        got_pairs.append(p + (np.uint64(bounds[s]) << np.uint64(32)))
+    torch.cuda.synchronize()
+    assert torch.equal(got_bits, bits)
+    hs, hcs, hc = ds.cpu().numpy().view(np.uint32), dcs.cpu().numpy().view(np.uint64), dcnt.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(np.sort(np.concatenate(got_pairs)),
+                                  oracle_pairs(hs, hcs, hc, bits.cpu().numpy().view(np.uint32)))
+    merged = {}
+    for g in range(nshards):
+        merged.update(shards[g].to_dict())
+    assert merged == ms.to_dict()
+    nmerged = {}
+    for g in range(nshards):
+        nmerged.update(news[g].to_dict() if not news[g].is_nil() else {})
+    assert nmerged == ns.to_dict()
+
+
 def _owner(e, n):
     """syz::owner_of (csrc/common.h) restated for the test."""
     def fmix(h):
