@@ -100,6 +100,18 @@ __device__ __forceinline__ uint32_t agg_home_bucket(uint32_t key, const AggGeom&
 	return __umulhi(key << g.pbits, kAggBuckets);
 }
 
+// Workgroup flag in LDS, read and set without `volatile`: a volatile access
+// through a generic pointer compiles to a flat access whose vmcnt(0) wait
+// drains every global load in flight (the record prefetch).
+__device__ __forceinline__ uint32_t lds_flag(uint32_t* f)
+{
+	return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_flag_set(uint32_t* f)
+{
+	__hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // position of e in a 4-key bucket, 4 if absent
 __device__ __forceinline__ uint32_t bucket_find(uint4 B, uint32_t e)
 {
@@ -137,14 +149,14 @@ __device__ uint32_t agg_find_insert(uint4* kb, uint32_t e, uint32_t b, uint4 B, 
 		const uint32_t key = atomicCAS(&keys[i], kAggEmpty, e);
 		if (key == kAggEmpty) {
 			if (atomicAdd(s_n, 1u) >= kAggLimit)
-				*(volatile uint32_t*)s_ovf = 1;
+				lds_flag_set(s_ovf);
 			return i;
 		}
 		if (key == e)
 			return i;
 		B = kb[b];  // another lane filled the slot first
 	}
-	*(volatile uint32_t*)s_ovf = 1;
+	lds_flag_set(s_ovf);
 	return kAggNoSlot;
 }
 
@@ -429,26 +441,30 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 			if (lane == 0)
 				gi = atomicAdd(&s_next, 1u);
 			gi = __builtin_amdgcn_readfirstlane(__shfl(gi, 0, 64));
-			if (gi >= ngroups || *(volatile uint32_t*)&s_ovf)
+			if (gi >= ngroups || lds_flag(&s_ovf))
 				break;
 			CellGroup cg;
 			cg.load(ot, nchunks, gi);
 			const uint32_t je = cg.bnd[kAggGroup];
-			// records stream through registers one batch ahead of the LDS work
-			uint32_t nxt[U];
+			if (je <= cg.bnd[0])
+				continue;
+			// Records stream through registers one batch ahead of the LDS work,
+			// ping-ponging between two buffers (a rotating one costs register
+			// moves that wait for the prefetch).  Loads are unconditional (index
+			// clamped): a load under a branch makes the compiler drain vmcnt(0)
+			// at the first use, i.e. wait for the prefetch too.
+			const uint32_t jl = je - 1;
+			auto fetch = [&](uint32_t (&buf)[U], uint32_t j0) {
 #pragma unroll
-			for (uint32_t u = 0; u < U; u++) {
-				const uint32_t j = cg.bnd[0] + u * 64 + lane;
-				nxt[u] = j < je ? __builtin_nontemporal_load(&pr[j]) : 0;
-			}
-			for (uint32_t j0 = cg.bnd[0]; j0 < je; j0 += U * 64) {
+				for (uint32_t u = 0; u < U; u++)
+					buf[u] = __builtin_nontemporal_load(&pr[min(j0 + u * 64 + lane, jl)]);
+			};
+			auto absorb = [&](const uint32_t (&buf)[U], uint32_t j0) {
 				uint32_t key[U], lv[U], k[U], hb[U], slot[U];
 				bool ok[U], need[U];
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++) {
-					const uint32_t j = j0 + u * 64 + lane, r = nxt[u];
-					const uint32_t jn = j + U * 64;
-					nxt[u] = jn < je ? __builtin_nontemporal_load(&pr[jn]) : 0;
+					const uint32_t j = j0 + u * 64 + lane, r = buf[u];
 					ok[u] = j < je;
 					k[u] = cg.serial(j, r, g);
 					key[u] = g.resid(r);
@@ -481,7 +497,19 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				for (uint32_t u = 0; u < U; u++)
 					if (slot[u] != kAggNoSlot)
 						atomicMin(&fl[lv[u]][slot[u]], k[u]);
-				if (*(volatile uint32_t*)&s_ovf)
+			};
+			uint32_t ra[U], rb[U];
+			fetch(ra, cg.bnd[0]);
+			for (uint32_t j0 = cg.bnd[0];;) {
+				fetch(rb, j0 + U * 64);
+				absorb(ra, j0);
+				j0 += U * 64;
+				if (j0 >= je || lds_flag(&s_ovf))
+					break;
+				fetch(ra, j0 + U * 64);
+				absorb(rb, j0);
+				j0 += U * 64;
+				if (j0 >= je || lds_flag(&s_ovf))
 					break;
 			}
 		}
