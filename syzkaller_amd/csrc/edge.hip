@@ -2,27 +2,33 @@
 // bit-exact with executor/executor.h:492-512 write_coverage_signal<uint64>,
 // :677-685 hash and :687-706 dedup, and executor_linux.cc:196-204 cover_check.
 //
-// One 64-lane workgroup per program (= one forked executor child): the 32 KB
-// dedup table lives in LDS for the program's lifetime, calls run in order.
-// K1 is data-parallel: sig_i = (u32)pc_i ^ hash((u32)pc_{i-1}) with the
-// previous PC's hash taken from the neighbour lane.  K2 is a sequential state
-// machine, parallelised exactly.  Signal i reads only its 4-slot window
-// {h, h+1, h+2, h+3} (h = sig % 8192) and writes at most one slot of it (insert
-// at the first empty slot, or the forced overwrite at h); a duplicate writes
-// nothing.  Per 64-signal chunk, lanes run in rounds:
+// One workgroup of kEdgeWaves waves per program (= one forked executor
+// child): the 32 KB dedup table lives in LDS for the program's lifetime, calls
+// run in order, and the trace goes through in chunks of kEdgeChunk = 256
+// signals (4 per CU: the table bounds residency, so the waves of a program
+// are what fills the SIMDs).  K1 is data-parallel: sig_i = (u32)pc_i ^
+// hash((u32)pc_{i-1}), the previous PC's hash taken from the lane below
+// (across waves through LDS, across chunks from a carry).  K2 is a sequential
+// state machine, parallelised exactly.  Signal i reads only its 4-slot window
+// {h, h+1, h+2, h+3} (h = sig % 8192) and writes at most one slot of it
+// (insert at the first empty slot, or the forced overwrite at h); a duplicate
+// writes nothing.  Per chunk, lanes run in rounds:
 //   1. every pending lane evaluates dedup() against the table as it stands
 //      (read only): duplicate, or a write at some slot of its window;
 //   2. writers mark the 8-slot bins their window touches (LDS stamps keep the
-//      earliest marking lane per bin); a pending lane with an EARLIER marker in
-//      its bins is blocked -- and marks its own bins too, since its re-run may
-//      turn into a write (repeated until no new marks);
+//      earliest marking position per bin); a pending lane with an EARLIER
+//      marker in its bins is blocked -- and marks its own bins too, since its
+//      re-run may turn into a write (repeated until no new marks);
 //   3. unblocked lanes are final: writers store, everyone leaves the round.
 // A final lane has only final duplicates before it inside its window, and
 // duplicates change nothing, so it saw exactly the sequential table state;
 // a lane after it that writes into its window does so after it read.  Mostly
-// duplicates (repeated edges) therefore finish in one round.
-// Latency: the trace is read kEdgeDepth chunks ahead of the chunk being
-// deduplicated (registers), so the HBM round trip overlaps LDS work.
+// duplicates (repeated edges) therefore finish in few rounds (3.1 per 256-signal
+// chunk at C2, against 1.8 per 64-signal chunk: 2.3x fewer rounds per signal).
+// Rounds need workgroup barriers; they are LDS-only (lds_barrier), so the
+// trace loads in flight are never drained.  The trace is read kEdgeDepth
+// chunks ahead of the chunk being deduplicated, ping-ponging between two
+// register buffers.
 #include "internal.h"
 
 namespace syz {
@@ -30,49 +36,67 @@ namespace syz {
 constexpr uint32_t kBinShift = 3;  // 8-slot bins
 constexpr uint32_t kBins = kDedupSize >> kBinShift;
 constexpr uint32_t kEpochMax = 0xFFFFFF;
-constexpr uint32_t kEdgeDepth = 8;  // chunks of 64 PCs in flight per wave
+constexpr uint32_t kEdgeWaves = 4;
+constexpr uint32_t kEdgeChunk = 64 * kEdgeWaves;  // signals per chunk (one per thread)
+constexpr uint32_t kEdgeDepth = 4;                // chunks in flight per buffer
 
-// The workgroup is ONE wave, so LDS traffic between its lanes needs no s_barrier
-// -- and __syncthreads() would also drain every outstanding global load (the
-// workgroup-scope release waits for vmcnt(0)), defeating the trace prefetch.
-// A wave's DS instructions execute in order; wait for them (lgkmcnt(0) only)
-// and keep the compiler from moving LDS accesses across.
-__device__ __forceinline__ void wave_lds_sync()
+// Workgroup barrier that orders LDS only: a plain __syncthreads() is also a
+// release of global memory, i.e. it waits for every global load in flight.
+__device__ __forceinline__ void lds_barrier()
 {
-	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-	__builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt/expcnt untouched, lgkmcnt(0)
-	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+	__builtin_amdgcn_s_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-__device__ __forceinline__ bool stamp_earlier(uint32_t s, uint32_t epoch, uint32_t lane)
+// stamp s (epoch << 8 | 255 - position) was set by a position before pos this epoch
+__device__ __forceinline__ bool stamp_earlier(uint32_t s, uint32_t epoch, uint32_t pos)
 {
-	return (s >> 8) == epoch && 63 - (s & 255) < lane;
+	return (s >> 8) == epoch && 255 - (s & 255) < pos;
 }
 
-__global__ __launch_bounds__(64) void k_edge_dedup(const uint64_t* __restrict__ pcs, uint64_t npc,
-                                                   const uint64_t* __restrict__ call_start,
-                                                   const uint32_t* __restrict__ call_len, uint64_t ncalls,
-                                                   const uint32_t* __restrict__ prog_call, uint64_t nprog,
-                                                   uint32_t* sigs, uint32_t* sig_cnt, uint32_t* completed,
-                                                   unsigned long long* cnt)
+__global__ __launch_bounds__(kEdgeChunk) void k_edge_dedup(const uint64_t* __restrict__ pcs, uint64_t npc,
+                                                           const uint64_t* __restrict__ call_start,
+                                                           const uint32_t* __restrict__ call_len, uint64_t ncalls,
+                                                           const uint32_t* __restrict__ prog_call, uint64_t nprog,
+                                                           uint32_t* sigs, uint32_t* sig_cnt, uint32_t* completed,
+                                                           unsigned long long* cnt)
 {
 	__shared__ uint32_t table[kDedupSize];
 	__shared__ uint32_t stamp[kBins];
-	const uint32_t lane = threadIdx.x;
+	__shared__ __align__(16) uint32_t s_any[2][kEdgeWaves];
+	__shared__ uint32_t s_carry[2][kEdgeWaves];
+	__shared__ uint32_t s_wcnt[kEdgeWaves];
+	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, pos = threadIdx.x;  // pos: place in a chunk
+	uint32_t seq = 0;
+	// Workgroup OR of a predicate (one barrier): every wave writes its own
+	// flag, one ds_read_b128 reads all four.  Two rows alternate: a row is
+	// rewritten two calls later, after every wave passed the barrier between.
+	auto wg_any = [&](bool pred) -> bool {
+		uint32_t* row = s_any[seq & 1];
+		const uint32_t any = __ballot(pred) != 0;
+		if (lane == 0)
+			row[w] = any;
+		lds_barrier();
+		const uint4 a = *reinterpret_cast<const uint4*>(row);
+		seq++;
+		return (a.x | a.y | a.z | a.w) != 0;
+	};
 	uint64_t err = 0;
+	uint32_t epoch = 0;
 	for (uint64_t p = blockIdx.x; p < nprog; p += gridDim.x) {
 		const uint64_t cb = prog_call[p], ce = prog_call[p + 1];
 		if (cb > ce || ce > ncalls) {
-			err += lane == 0;
+			err += threadIdx.x == 0;
 			continue;
 		}
 		// fresh table per program (common_linux.h:1995-2030: fork zeroes it)
-		for (uint32_t i = lane; i < kDedupSize / 4; i += 64)
+		for (uint32_t i = threadIdx.x; i < kDedupSize / 4; i += kEdgeChunk)
 			reinterpret_cast<uint4*>(table)[i] = make_uint4(0, 0, 0, 0);
-		for (uint32_t i = lane; i < kBins; i += 64)
+		for (uint32_t i = threadIdx.x; i < kBins; i += kEdgeChunk)
 			stamp[i] = 0;
-		__syncthreads();
-		uint32_t epoch = 0;
+		epoch = 0;
+		lds_barrier();
 		uint64_t done = ce - cb;
 		bool aborted = false;
 		for (uint64_t c = cb; c < ce && !aborted; c++) {
@@ -80,123 +104,150 @@ __global__ __launch_bounds__(64) void k_edge_dedup(const uint64_t* __restrict__ 
 			const uint32_t len = call_len[c];
 			if (len >= kCoverSize || start > npc || len > npc - start) {
 				// executor_linux.cc:186-187 fail("too much cover") / malformed input
-				err += lane == 0;
+				err += threadIdx.x == 0;
 				aborted = true;
 				done = c - cb;
 				break;
 			}
-			uint32_t nsig = 0, carry = 0;
-			const uint32_t nch = (len + 63) / 64;
 			if (len == 0) {  // nothing to load (pcs may even be empty)
-				if (lane == 0)
+				if (threadIdx.x == 0)
 					sig_cnt[c] = 0;
 				continue;
 			}
+			uint32_t nsig = 0, carry = 0;  // carry: hash of the previous chunk's last PC
+			const uint32_t nch = (len + kEdgeChunk - 1) / kEdgeChunk;
+			const uint64_t last = start + len - 1;
 			// Loads are unconditional (index clamped into the call, value masked
 			// later): a load under a branch makes the compiler drain vmcnt(0)
 			// before the first use, i.e. wait for the whole prefetch.
-			const uint64_t last = start + (len ? len - 1 : 0);
-			uint64_t buf[kEdgeDepth];
+			auto fetch = [&](uint64_t (&buf)[kEdgeDepth], uint32_t g) {
 #pragma unroll
-			for (uint32_t u = 0; u < kEdgeDepth; u++)
-				buf[u] = pcs[min<uint64_t>(start + u * 64 + lane, last)];
-			for (uint32_t g = 0; g < nch && !aborted; g += kEdgeDepth) {
-				uint64_t cur[kEdgeDepth];
+				for (uint32_t u = 0; u < kEdgeDepth; u++)
+					buf[u] = pcs[min<uint64_t>(start + (uint64_t)(g + u) * kEdgeChunk + pos, last)];
+			};
+			// chunk q of the call; false once the program aborts
+			auto chunk = [&](uint64_t pcv, uint32_t q) -> bool {
+				const uint32_t j = q * kEdgeChunk + pos;
+				const bool valid = j < len;
+				const uint64_t pc = valid ? pcv : 0;
+				const uint32_t h = exec_hash((uint32_t)pc);
+				uint32_t up = __shfl_up(h, 1, 64);
+				if (lane == 63)
+					s_carry[q & 1][w] = h;
+				// cover_check (executor_linux.cc:196-204): doexit(0), this call and
+				// the rest of the program publish nothing
+				if (wg_any(valid && !cover_check(pc)))
+					return false;
+				if (lane == 0)
+					up = w == 0 ? carry : s_carry[q & 1][w - 1];
+				carry = s_carry[q & 1][kEdgeWaves - 1];
+				const uint32_t sig = (uint32_t)pc ^ up;
+				const uint32_t home = sig & (kDedupSize - 1);
+				const uint32_t b0 = home >> kBinShift, b1 = ((home + 3) & (kDedupSize - 1)) >> kBinShift;
+				bool pending = valid, emit = false;
+				while (wg_any(pending)) {
+					// 1. evaluate dedup() (executor.h:692-706) on the current table,
+					// branch-free: the first probe i with T[h+i] == sig (duplicate)
+					// or T[h+i] == 0 (insert there), else the forced overwrite at h
+					uint32_t eqm = 0, zm = 0;
 #pragma unroll
-				for (uint32_t u = 0; u < kEdgeDepth; u++) {
-					cur[u] = buf[u];
-					buf[u] = pcs[min<uint64_t>(start + (g + kEdgeDepth + u) * 64 + lane, last)];
-				}
-#pragma unroll
-				for (uint32_t u = 0; u < kEdgeDepth; u++) {
-					if (g + u >= nch)
-						break;
-					const uint32_t j = (g + u) * 64 + lane;
-					const bool valid = j < len;
-					const uint64_t pc = valid ? cur[u] : 0;
-					if (__ballot(valid && !cover_check(pc))) {
-						aborted = true;  // doexit(0): this call and the rest publish nothing
-						done = c - cb;
-						break;
+					for (uint32_t i = 0; i < 4; i++) {
+						const uint32_t t = table[(sig + i) & (kDedupSize - 1)];
+						eqm |= (uint32_t)(t == sig) << i;
+						zm |= (uint32_t)(t == 0) << i;
 					}
-					const uint32_t h = exec_hash((uint32_t)pc);
-					const uint32_t up = __shfl_up(h, 1, 64);
-					const uint32_t sig = (uint32_t)pc ^ (lane == 0 ? carry : up);
-					carry = __shfl(h, 63, 64);
-					const uint32_t home = sig & (kDedupSize - 1);
-					const uint32_t b0 = home >> kBinShift, b1 = ((home + 3) & (kDedupSize - 1)) >> kBinShift;
-					bool pending = valid, emit = false;
-					while (__ballot(pending)) {
-						// 1. evaluate dedup() (executor.h:692-706, literally) on the current table
-						bool writer = false;
-						uint32_t wpos = home;
-						if (pending) {
-							uint32_t t[4];
-#pragma unroll
-							for (uint32_t i = 0; i < 4; i++)
-								t[i] = table[(sig + i) & (kDedupSize - 1)];
-							bool decided = false;
-#pragma unroll
-							for (uint32_t i = 0; i < 4; i++) {
-								if (!decided && t[i] == sig) {
-									decided = true;  // duplicate
-								} else if (!decided && t[i] == 0) {
-									decided = true;
-									writer = true;
-									wpos = (sig + i) & (kDedupSize - 1);
-								}
-							}
-							writer = writer || !decided;  // all 4 taken: forced overwrite at home
-						}
-						// 2. mark / block until stable
-						if (epoch == kEpochMax) {
-							for (uint32_t i = lane; i < kBins; i += 64)
-								stamp[i] = 0;
-							epoch = 0;
-							wave_lds_sync();
-						}
-						epoch++;
-						const uint32_t v = (epoch << 8) | (63 - lane);
-						bool marker = pending && writer, blocked = false;
-						bool mark_now = marker;
-						for (;;) {
-							if (mark_now) {
-								atomicMax(&stamp[b0], v);
-								if (b1 != b0)
-									atomicMax(&stamp[b1], v);
-							}
-							wave_lds_sync();
-							blocked = pending && (stamp_earlier(stamp[b0], epoch, lane) ||
-							                      stamp_earlier(stamp[b1], epoch, lane));
-							mark_now = blocked && !marker;
-							marker = marker || mark_now;
-							if (!__ballot(mark_now))
-								break;
-						}
-						// 3. final lanes commit
-						if (pending && !blocked) {
-							if (writer)
-								table[wpos] = sig;
-							emit = writer;
-							pending = false;
-						}
-						wave_lds_sync();
+					const uint32_t first = __builtin_ctz(eqm | zm | 16u);
+					const bool writer = !((eqm >> first) & 1);
+					const uint32_t wpos = (sig + (first & 3)) & (kDedupSize - 1);
+					// 2. mark / block until stable
+					if (epoch == kEpochMax) {
+						for (uint32_t i = threadIdx.x; i < kBins; i += kEdgeChunk)
+							stamp[i] = 0;
+						epoch = 0;
+						lds_barrier();
 					}
-					const uint64_t m = __ballot(emit);
-					if (emit)
-						sigs[start + nsig + lane_rank(m)] = sig;  // write_output order == trace order
-					nsig += (uint32_t)__popcll(m);
+					epoch++;
+					const uint32_t v = (epoch << 8) | (255 - pos);
+					bool marker = pending && writer, blocked = false;
+					bool mark_now = marker;
+					for (;;) {
+						if (mark_now) {
+							atomicMax(&stamp[b0], v);
+							if (b1 != b0)
+								atomicMax(&stamp[b1], v);
+						}
+						lds_barrier();
+						const uint32_t s0 = stamp[b0], s1 = stamp[b1];
+						blocked = pending && (stamp_earlier(s0, epoch, pos) || stamp_earlier(s1, epoch, pos));
+						mark_now = blocked && !marker;
+						marker = marker || mark_now;
+						if (!wg_any(mark_now))
+							break;
+					}
+					// 3. final lanes commit (visible after the next round's barrier)
+					const bool fin_w = pending && !blocked && writer;
+					if (fin_w)
+						table[wpos] = sig;
+					emit = emit || fin_w;
+					pending = pending && blocked;
 				}
+				// write_output order == trace order: waves in order, lanes in order
+				const uint64_t m = __ballot(emit);
+				if (lane == 0)
+					s_wcnt[w] = (uint32_t)__popcll(m);
+				lds_barrier();
+				uint32_t base = nsig, tot = 0;
+#pragma unroll
+				for (uint32_t i = 0; i < kEdgeWaves; i++) {
+					const uint32_t x = s_wcnt[i];
+					base += i < w ? x : 0;
+					tot += x;
+				}
+				if (emit)
+					sigs[start + base + lane_rank(m)] = sig;
+				nsig += tot;
+				return true;
+			};
+			auto run = [&](const uint64_t (&buf)[kEdgeDepth], uint32_t g) -> bool {
+#pragma unroll
+				for (uint32_t u = 0; u < kEdgeDepth; u++)
+					if (g + u < nch && !chunk(buf[u], g + u))
+						return false;
+				return true;
+			};
+			uint64_t ba[kEdgeDepth], bb[kEdgeDepth];
+			fetch(ba, 0);
+			for (uint32_t g = 0;;) {
+				fetch(bb, g + kEdgeDepth);
+				if (!run(ba, g)) {
+					aborted = true;
+					break;
+				}
+				g += kEdgeDepth;
+				if (g >= nch)
+					break;
+				fetch(ba, g + kEdgeDepth);
+				if (!run(bb, g)) {
+					aborted = true;
+					break;
+				}
+				g += kEdgeDepth;
+				if (g >= nch)
+					break;
 			}
-			if (!aborted && lane == 0)
+			if (aborted) {
+				done = c - cb;
+				break;
+			}
+			if (threadIdx.x == 0)
 				sig_cnt[c] = nsig;
 		}
 		// calls not published (aborted and later) report no signal (ipc.go:362-365)
-		for (uint64_t c = cb + done + lane; c < ce; c += 64)
+		for (uint64_t c = cb + done + threadIdx.x; c < ce; c += kEdgeChunk)
 			sig_cnt[c] = 0;
-		if (lane == 0)
+		if (threadIdx.x == 0)
 			completed[p] = (uint32_t)done;
-		__syncthreads();
+		lds_barrier();  // the table is re-zeroed for the next program
 	}
 	block_count(&cnt[kCntError], err);
 }
@@ -217,7 +268,7 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 		return SYZSIG_OK;
 	SYZ_TRY(counters_reset(ctx));
 	const int grid = (int)std::min<uint64_t>(nprog, 256 * 4);
-	k_edge_dedup<<<grid, 64, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call, nprog,
+	k_edge_dedup<<<grid, kEdgeChunk, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call, nprog,
 	                                           d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
 	SYZ_TRY(counters_fetch(ctx));
