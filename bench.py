@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--pcs", type=int, default=4096)
     ap.add_argument("--m0", type=int, default=10_000_000, help="maxSignal elements per GPU")
     ap.add_argument("--skew", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU-baseline sample time")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time (s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--table-hint", type=int, default=0,
                     help="size maxSignal's table for this many entries (default: the library's policy)")
