@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--skew", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time (s)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (= RCCL over xGMI, the product path); gloo only to rehearse N>1 ranks "
+                         "sharing fewer GPUs (rank r uses GPU r mod device_count)")
     ap.add_argument("--table-hint", type=int, default=0,
                     help="size maxSignal's table for this many entries (default: the library's policy)")
     return ap.parse_args()
@@ -123,12 +126,17 @@ def main():
     if world != a.gpus:
         if a.gpus != 1 or world != 1:
             raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    if a.dist_backend == "gloo":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     distributed = world > 1
     if distributed:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from syzkaller_amd import signal as S
     from syzkaller_amd import synth
@@ -248,7 +256,8 @@ def main():
                        "programs_per_gpu": P, "calls": C, "pcs_per_call": L, "m0_per_gpu": a.m0,
                        "records_per_gpu": nrec, "pcs_per_gpu": npc, "skew": a.skew,
                        "table_slots": ms.capacity(),
-                       "parallelism": f"shard{world}" if distributed else "single"},
+                       "parallelism": f"shard{world}" if distributed else "single",
+                       **({"dist_backend": a.dist_backend} if distributed else {})},
             "roofline": {"bound": "hbm",
                          "kernel": K3_KERNELS if not distributed else K3_DIST_KERNELS,
                          "achieved": achieved, "peak": HBM_PEAK_GBS,

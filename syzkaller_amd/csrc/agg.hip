@@ -61,7 +61,7 @@ constexpr uint32_t kAggNone = 0xFFFFFFFFu;         // no record at this level
 constexpr uint32_t kAggOverflow = 0xFFFFFFFFu;     // partition count marker
 constexpr uint32_t kAggMinBits = 3, kAggMaxBits = 11;
 constexpr uint32_t kAggMaxParts = 1u << kAggMaxBits;
-constexpr uint32_t kAggTile = 15360;  // records per scatter tile (8 B of LDS each)
+constexpr uint32_t kAggTile = 18432;  // records per scatter tile (18 per lane; 6 B of LDS each)
 constexpr uint32_t kAggGroup = 8;     // cells per wave work item of k_agg
 
 static_assert(0x85ebca6bu * 0xa5cb9243u == 1u, "fmix32_inv multiplier");
@@ -293,9 +293,13 @@ __global__ __launch_bounds__(1024) void k_agg_scan_totals(const uint64_t* totals
 }
 
 // Records of each chunk -> their cells (fixed by the scan, so no global
-// atomics).  A tile of kAggTile records is staged in LDS as (h, meta),
-// counting-sorted by partition and written as one run per partition; the
-// runs of one chunk's consecutive tiles continue each other.
+// atomics).  A tile of kAggTile records lives in registers (kPer per lane),
+// is counting-sorted by partition into LDS and written out as one run per
+// partition; the runs of one chunk's consecutive tiles continue each other.
+// The next tile's loads are issued before the write-out of the current one,
+// so HBM reads overlap the stores instead of following them.
+constexpr uint32_t kScatChunkMax = 1u << (kAggMaxBits - 2);  // calls per chunk (cbits <= 9)
+
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __restrict__ sigs,
                                                              const uint64_t* __restrict__ call_start,
                                                              const uint32_t* __restrict__ call_len,
@@ -306,75 +310,95 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 {
 	constexpr uint32_t kWaves = kAggThreads / 64, kQuota = kAggTile / kWaves, kPer = kQuota / 64;
 	static_assert(kQuota % 64 == 0, "tile quota per wave");
-	__shared__ uint32_t t_h[kAggTile];    // fmix32(e)
-	__shared__ uint16_t t_m[kAggTile];    // level << cbits | serial in chunk
-	__shared__ uint16_t s_idx[kAggTile];  // sorted position -> staged record
+	__shared__ uint32_t t_rec[kAggTile];   // sorted by partition: packed records
+	__shared__ uint16_t t_part[kAggTile];  // ... and their partitions
 	__shared__ uint64_t cur[kAggMaxParts];
 	__shared__ uint32_t hist[kAggMaxParts], pos[kAggMaxParts];
-	__shared__ uint32_t tile_n, more;
+	__shared__ uint64_t c_start[kScatChunkMax];  // the chunk's calls
+	__shared__ uint32_t c_len[kScatChunkMax];
+	__shared__ uint16_t c_meta[kScatChunkMax];
+	__shared__ uint32_t tile_n;
 	const uint32_t P = 1u << g.pbits, cb = g.cbits();
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
 	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << cb) - 1) >> cb;
 	const uint32_t per_t = (P + blockDim.x - 1) / blockDim.x;
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-		const uint64_t cbeg = ch << cb, ce = min<uint64_t>(ncalls, cbeg + (1ull << cb));
-		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
+		const uint64_t cbeg = ch << cb;
+		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << cb);
+		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
 			cur[i] = rec_base[i] + offs[ch * P + i];
-		uint64_t wc = cbeg + w;  // this wave's call (serial), then +kWaves
-		uint32_t wo = 0;         // offset inside it
-		for (;;) {
-			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
-				hist[i] = 0;
-			if (threadIdx.x == 0) {
-				tile_n = 0;
-				more = 0;
-			}
-			__syncthreads();
-			uint32_t quota = kQuota;
-			while (quota && wc < ce) {
-				const uint64_t c = c0 + wc, start = call_start[c];
-				const uint32_t len = call_len[c];
-				const uint32_t m = min(quota, len - wo);
-				uint32_t tb = 0;
-				if (lane == 0 && m)
-					tb = atomicAdd(&tile_n, m);
-				tb = __shfl(tb, 0, 64);
-				const uint32_t meta = g.meta(lm.lvl[call_prio[c]], wc);
-				uint32_t ev[kPer];
+			hist[i] = 0;
+		}
+		for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
+			const uint64_t c = c0 + cbeg + i;
+			c_start[i] = call_start[c];
+			c_len[i] = call_len[c];
+			c_meta[i] = (uint16_t)g.meta(lm.lvl[call_prio[c]], cbeg + i);
+		}
+		if (threadIdx.x == 0)
+			tile_n = 0;
+		__syncthreads();
+		// this wave's walk: local call wc (then +kWaves), offset wo inside it
+		uint32_t wc = w, wo = 0;
+		// Per record slot: loc = (wave call number j << 24) | offset in the call
+		// (calls hold < 2^24 records, batch validation); the wave's j-th call
+		// is local call w + j * kWaves (j < 2^cbits / kWaves <= 32).
+		uint32_t ev[kPer], loc[kPer];
+		// issue the loads of this wave's next quota; returns how many records it has
+		auto fetch = [&]() -> uint32_t {
+			uint32_t q = 0;
+			while (q < kQuota && wc < nc) {
+				const uint32_t len = c_len[wc], m = min(kQuota - q, len - wo);
+				const uint32_t tag = ((wc - w) / kWaves) << 24;
+				if (q == 0) {
 #pragma unroll
-				for (uint32_t u = 0; u < kPer; u++) {
-					const uint32_t i = u * 64 + lane;
-					ev[u] = i < m ? __builtin_nontemporal_load(&sigs[start + wo + i]) : 0;
+					for (uint32_t u = 0; u < kPer; u++)
+						loc[u] = tag | wo;  // clamped default: a valid address
 				}
 #pragma unroll
 				for (uint32_t u = 0; u < kPer; u++) {
 					const uint32_t i = u * 64 + lane;
-					if (i < m) {
-						const uint32_t h = fmix32(ev[u]);
-						t_h[tb + i] = h;
-						t_m[tb + i] = (uint16_t)meta;
-						atomicAdd(&hist[g.part(h)], 1u);
-					}
+					loc[u] = i >= q && i < q + m ? tag | (wo + i - q) : loc[u];
 				}
-				quota -= m;
+				q += m;
 				wo += m;
 				if (wo == len) {
 					wc += kWaves;
 					wo = 0;
 				}
 			}
-			if (lane == 0 && wc < ce)
-				atomicOr(&more, 1u);
+			if (q) {
+#pragma unroll
+				for (uint32_t u = 0; u < kPer; u++)
+					ev[u] = __builtin_nontemporal_load(&sigs[c_start[w + (loc[u] >> 24) * kWaves] + (loc[u] & 0xFFFFFFu)]);
+			}
+			return q;
+		};
+		uint32_t n = fetch();
+		for (;;) {
+			// stage: partition and rank of every record of the tile
+			if (lane == 0 && n)
+				atomicAdd(&tile_n, n);
+#pragma unroll
+			for (uint32_t u = 0; u < kPer; u++) {
+				const uint32_t i = u * 64 + lane;
+				if (i < n) {
+					const uint32_t h = fmix32(ev[u]), p = g.part(h);
+					const uint32_t r = atomicAdd(&hist[p], 1u);
+					ev[u] = g.rec(h, c_meta[w + (loc[u] >> 24) * kWaves]);
+					loc[u] = p | (r << 16);
+				}
+			}
 			__syncthreads();
-			const uint32_t n = tile_n;
+			const uint32_t nt = tile_n;
 			// exclusive scan of hist; pos[p] = the partition's first sorted position
-			uint32_t loc = 0;
+			uint32_t hsum = 0;
 			for (uint32_t q = 0; q < per_t; q++) {
 				const uint32_t i = threadIdx.x * per_t + q;
-				loc += i < P ? hist[i] : 0;
+				hsum += i < P ? hist[i] : 0;
 			}
 			uint32_t ex;
-			block_excl_scan_1k(loc, &ex);
+			block_excl_scan_1k(hsum, &ex);
 			for (uint32_t q = 0; q < per_t; q++) {
 				const uint32_t i = threadIdx.x * per_t + q;
 				if (i < P) {
@@ -384,20 +408,29 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 				}
 			}
 			__syncthreads();
-			for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
-				s_idx[atomicAdd(&pos[g.part(t_h[i])], 1u)] = (uint16_t)i;
+#pragma unroll
+			for (uint32_t u = 0; u < kPer; u++) {
+				const uint32_t i = u * 64 + lane;
+				if (i < n) {
+					const uint32_t p = loc[u] & 0xFFFFu, d = pos[p] + (loc[u] >> 16);
+					t_rec[d] = ev[u];
+					t_part[d] = (uint16_t)p;
+				}
+			}
+			// next tile's loads fly during the write-out
+			n = fetch();
 			__syncthreads();
 			// consecutive threads write consecutive records of one partition's run
-			for (uint32_t d = threadIdx.x; d < n; d += blockDim.x) {
-				const uint32_t i = s_idx[d], h = t_h[i];
-				recs[cur[g.part(h)] + d] = g.rec(h, t_m[i]);
+			for (uint32_t d = threadIdx.x; d < nt; d += blockDim.x)
+				recs[cur[t_part[d]] + d] = t_rec[d];
+			__syncthreads();
+			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+				cur[i] += pos[i] + hist[i];  // advance by the run
+				hist[i] = 0;
 			}
-			__syncthreads();
-			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
-				cur[i] += pos[i];  // pos[p] = old start + hist[p]: advance by the run
-			const bool again = more != 0;
-			__syncthreads();
-			if (!again)
+			if (threadIdx.x == 0)
+				tile_n = 0;
+			if (!__syncthreads_or(n != 0))
 				break;
 		}
 	}
