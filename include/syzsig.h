@@ -184,6 +184,37 @@ int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, uint64_t npc,
                            const uint32_t* d_call_len, uint64_t ncalls, const uint32_t* d_prog_call,
                            uint64_t nprog, uint32_t* d_sigs, uint32_t* d_sig_cnt, uint32_t* d_completed);
 
+/* ---- pkg/ipc/ipc.go:328-468 readOutCoverage over a batch of executor output regions ----
+ * Program p's output region (executor.h:566-604 records, the executor's shmem
+ * out file) is d_out[prog_off[p] .. prog_off[p+1]); it has the calls
+ * [prog_call[p], prog_call[p+1]) (len(p.Calls)), call_num[c] = the expected
+ * syscall ID (c.Meta.ID; NULL = unchecked) and call_any[c] = CallContainsAny
+ * (prog/any.go:177-185).  Writes per call: the Signal range inside d_out
+ * (aliasing it, ipc.go:410; call_len = 0 if the call has no record), its Errno
+ * (-1 = not executed), and its signalPrio (fuzzer.go:513-521); optionally the
+ * Cover range.  The result feeds syzsig_triage_batch with sigs = d_out,
+ * nrec = nwords.  prog_status[p] = SYZSIG_INGEST_* (the ipc.go error branch
+ * hit); a failed program gets no signal (the fuzzer retries that Exec,
+ * proc.go:269-278).  *n_failed (optional) = programs with status != 0.
+ * Returns SYZSIG_EINVAL if an offset or call range is out of bounds. */
+#define SYZSIG_INGEST_OK 0
+#define SYZSIG_INGEST_ENCMD 1      /* no ncmd word (ipc.go:356-359) */
+#define SYZSIG_INGEST_EHEADER 2    /* short call header (:378-383) */
+#define SYZSIG_INGEST_EINDEX 3     /* callIndex >= len(p.Calls) (:384-388) */
+#define SYZSIG_INGEST_ECALLNUM 4   /* callNum != c.Meta.ID (:389-395) */
+#define SYZSIG_INGEST_EDOUBLE 5    /* double coverage for a call (:396-400) */
+#define SYZSIG_INGEST_ESIGNAL 6    /* signalSize past the region (:403-407) */
+#define SYZSIG_INGEST_ECOVER 7     /* coverSize past the region (:411-415) */
+#define SYZSIG_INGEST_ECOMPS 8     /* short comparison record (:420-445) */
+#define SYZSIG_INGEST_ECOMPTYPE 9  /* comparison type > compConstMask|compSizeMask (:429-433) */
+#define SYZSIG_INGEST_EBOUNDS 10   /* prog_off / prog_call out of bounds (ABI check) */
+int syzsig_ingest_exec_output_dev(syzsig_ctx* ctx, const uint32_t* d_out, uint64_t nwords,
+                                  const uint64_t* d_prog_off, uint64_t nprog, const uint32_t* d_prog_call,
+                                  uint64_t ncalls, const uint32_t* d_call_num, const uint8_t* d_call_any,
+                                  uint64_t* d_call_start, uint32_t* d_call_len, uint8_t* d_call_prio,
+                                  int32_t* d_call_errno, uint64_t* d_cover_start, uint32_t* d_cover_len,
+                                  int32_t* d_prog_status, uint64_t* n_failed);
+
 /* ---- hash-sharded maxSignal across GPUs (one process per GPU) ----
  * The batch is split by program range over G GPUs (serial order = GPU-major);
  * every record is routed to the GPU owning its element

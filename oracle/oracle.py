@@ -190,10 +190,11 @@ def minimize(off, elems, prios):
     return [int(x) for x in out[:k]]
 
 
-def run_reference_executor(programs):
+def run_reference_executor(programs, raw=False):
     """Run the REFERENCE executor's signal code (oracle/_ref/ref_harness, built
     from /root/reference by oracle/Makefile) on programs = [[(failed, pcs u64[]), ...], ...].
-    Returns per program (completed, [(call_index, errno, sigs u32[]), ...])."""
+    Returns per program (completed, [(call_index, errno, sigs u32[]), ...]), or with raw=True the program's
+    output region words as the executor wrote them (executor.h:566-604)."""
     import struct
 
     data = [struct.pack("<I", len(programs))]
@@ -209,6 +210,9 @@ def run_reference_executor(programs):
         (nw,) = struct.unpack_from("<I", out, pos)
         words = np.frombuffer(out, np.uint32, nw, pos + 4)
         pos += 4 + 4 * nw
+        if raw:
+            res.append(words.copy())
+            continue
         completed = int(words[0])
         calls, q = [], 1
         for _ in range(completed):
@@ -233,3 +237,86 @@ def triage_batch_into(ms, sigs, call_start, call_len, call_prio, ns=None):
                            _p(cnew))
     ms.h, ns.h = mh.value, nh.value
     return ns, bits, cnew
+
+
+# ---- pkg/ipc/ipc.go:328-468 readOutCoverage (restated; test infrastructure only) ----
+INGEST_OK, INGEST_ENCMD, INGEST_EHEADER, INGEST_EINDEX, INGEST_ECALLNUM, INGEST_EDOUBLE = 0, 1, 2, 3, 4, 5
+INGEST_ESIGNAL, INGEST_ECOVER, INGEST_ECOMPS, INGEST_ECOMPTYPE = 6, 7, 8, 9
+
+
+def read_out_coverage(words, ncalls, call_num=None):
+    """One executor output region -> (status, info) with info[i] = (errno, sig_off, sig_len, cov_off, cov_len) or
+    None for a call without a record (Errno = -1, Signal = nil; ipc.go:362-365).  Offsets are word indices into
+    `words`.  status != 0 names the ipc.go error branch taken (see include/syzsig.h SYZSIG_INGEST_*)."""
+    out = [int(x) for x in words]
+    pos, n = 0, len(out)
+    info = [None] * ncalls
+    if n == 0:  # ipc.go:356-359
+        return INGEST_ENCMD, info
+    ncmd = out[0]
+    pos = 1
+    for _ in range(ncmd):
+        if n - pos < 7:  # ipc.go:378-383
+            return INGEST_EHEADER, info
+        idx, num, err, _fault, nsig, ncover, ncomps = out[pos:pos + 7]
+        pos += 7
+        if idx >= ncalls:  # ipc.go:384-388
+            return INGEST_EINDEX, info
+        if call_num is not None and int(call_num[idx]) != num:  # ipc.go:389-395
+            return INGEST_ECALLNUM, info
+        if info[idx] is not None:  # ipc.go:396-400
+            return INGEST_EDOUBLE, info
+        if nsig > n - pos:  # ipc.go:403-407
+            return INGEST_ESIGNAL, info
+        so = pos
+        pos += nsig
+        if ncover > n - pos:  # ipc.go:411-415
+            return INGEST_ECOVER, info
+        info[idx] = (err - (1 << 32) if err >= 1 << 31 else err, so, nsig, pos, ncover)
+        pos += ncover
+        for _j in range(ncomps):  # ipc.go:420-458
+            if pos >= n:
+                return INGEST_ECOMPS, info
+            typ = out[pos]
+            pos += 1
+            if typ > (1 | 6):  # compConstMask | compSizeMask
+                return INGEST_ECOMPTYPE, info
+            w = 4 if (typ & 6) == 6 else 2
+            if n - pos < w:
+                return INGEST_ECOMPS, info
+            pos += w
+    return INGEST_OK, info
+
+
+def signal_prio(errno, any_):
+    """syz-fuzzer/fuzzer.go:513-521"""
+    return (2 if errno == 0 else 0) | (0 if any_ else 1)
+
+
+def ingest_batch(regions, ncalls, call_any, call_num=None):
+    """readOutCoverage over a batch; regions = list of u32 arrays, ncalls[p] = len(p.Calls).  Returns flat
+    (out_words, prog_off, prog_call, call_start, call_len, call_prio, call_errno, status) with the expected
+    result: a failed program (status != 0) contributes no signal (syz-fuzzer/proc.go:269-278)."""
+    prog_off, prog_call = [0], [0]
+    for r, nc in zip(regions, ncalls):
+        prog_off.append(prog_off[-1] + len(r))
+        prog_call.append(prog_call[-1] + int(nc))
+    out = np.concatenate([np.asarray(r, np.uint32) for r in regions]) if regions else np.empty(0, np.uint32)
+    nct = prog_call[-1]
+    cs = np.zeros(nct, np.uint64)
+    cl = np.zeros(nct, np.uint32)
+    ce = np.full(nct, -1, np.int32)
+    st = np.zeros(len(regions), np.int32)
+    for p, r in enumerate(regions):
+        c0 = prog_call[p]
+        nums = None if call_num is None else call_num[c0:prog_call[p + 1]]
+        s, info = read_out_coverage(r, int(ncalls[p]), nums)
+        st[p] = s
+        for i, inf in enumerate(info):
+            cs[c0 + i] = prog_off[p]
+            if s == INGEST_OK and inf is not None:
+                ce[c0 + i] = inf[0]
+                cs[c0 + i] = prog_off[p] + inf[1]
+                cl[c0 + i] = inf[2]
+    cp = np.array([signal_prio(int(e), int(a)) for e, a in zip(ce, call_any)], np.uint8)
+    return (out, np.array(prog_off, np.uint64), np.array(prog_call, np.uint32), cs, cl, cp, ce, st)

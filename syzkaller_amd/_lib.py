@@ -86,6 +86,8 @@ SIGNATURES = {
                                         POINTER(c_uint32), _P]),
     "syzsig_triage_batch": (c_int, [_P, _P, _PP, POINTER(Batch), POINTER(BatchStats)]),
     "syzsig_edge_derive_dev": (c_int, [_P, _P, c_uint64, _P, _P, c_uint64, _P, c_uint64, _P, _P, _P]),
+    "syzsig_ingest_exec_output_dev": (c_int, [_P, _P, c_uint64, _P, c_uint64, _P, c_uint64, _P, _P, _P, _P, _P, _P,
+                                              _P, _P, _P, POINTER(c_uint64)]),
     "syzsig_shard_partition_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint32, c_uint32, _P, _P, _P]),
     "syzsig_triage_records_dev": (c_int, [_P, _P, _PP, _P, c_uint64, _P, c_uint32, _P,
                                           POINTER(BatchStats)]),

@@ -115,6 +115,37 @@ class Device:
                                             _p(completed)))
         return sigs, sig_cnt, completed
 
+    # ---------------------------------------------------------------- executor output ingest
+    def ingest_exec_output(self, out, prog_off, prog_call, call_any, call_num=None, want_cover=False):
+        """pkg/ipc/ipc.go:328-468 readOutCoverage over a batch of executor output
+        regions (program p's at out[prog_off[p]:prog_off[p+1]]).  Returns a dict of
+        device tensors call_start (int64), call_len (int32), call_prio (uint8),
+        call_errno (int32), prog_status (int32), cover_start/cover_len (if
+        want_cover), and n_failed.  call_start/len index `out`, so
+        triage(max, new, out, call_start, call_len, call_prio) runs checkNewSignal
+        on the batch without copying the signal."""
+        self._check_dev(out, prog_off, prog_call, call_any, call_num)
+        nprog, ncalls = prog_off.numel() - 1, call_any.numel()
+        if prog_call.numel() != prog_off.numel():
+            raise ValueError("prog_call and prog_off need nprog + 1 entries")
+        if call_num is not None and call_num.numel() != ncalls:
+            raise ValueError("call_num needs one entry per call")
+        r = {"call_start": torch.empty(ncalls, dtype=torch.int64, device=self.dev),
+             "call_len": torch.empty(ncalls, dtype=torch.int32, device=self.dev),
+             "call_prio": torch.empty(ncalls, dtype=torch.uint8, device=self.dev),
+             "call_errno": torch.empty(ncalls, dtype=torch.int32, device=self.dev),
+             "prog_status": torch.empty(max(nprog, 0), dtype=torch.int32, device=self.dev)}
+        if want_cover:
+            r["cover_start"] = torch.empty(ncalls, dtype=torch.int64, device=self.dev)
+            r["cover_len"] = torch.empty(ncalls, dtype=torch.int32, device=self.dev)
+        nf = ctypes.c_uint64()
+        check(self.L.syzsig_ingest_exec_output_dev(
+            self.eng.h, _p(out), out.numel(), _p(prog_off), max(nprog, 0), _p(prog_call), ncalls, _p(call_num),
+            _p(call_any), _p(r["call_start"]), _p(r["call_len"]), _p(r["call_prio"]), _p(r["call_errno"]),
+            _p(r.get("cover_start")), _p(r.get("cover_len")), _p(r["prog_status"]), ctypes.byref(nf)))
+        r["n_failed"] = int(nf.value)
+        return r
+
     # ---------------------------------------------------------------- K5
     def minimize(self, ctx_off, elems, prios, hint_distinct=0):
         self._check_dev(ctx_off, elems, prios)

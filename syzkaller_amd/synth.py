@@ -47,3 +47,30 @@ def m0(cfg, known_sys, n):
     prios = np.empty(n, dtype=np.int8)
     check(_lib.lib().syzsig_synth_m0_host(ctypes.byref(cfg), known_sys, n, _p(elems), _p(prios)))
     return elems, prios
+
+
+def frame_exec_output(sigs, call_start, sig_cnt, completed, prog_call, call_errno, order_seed=None):
+    """Frame per-call signals as executor output regions (executor.h:566-604
+    handle_completion records: callIndex, callNum = call index, errno,
+    faultInjected = 0, nsig, ncover = 0, ncomps = 0, sig[nsig]) -- the synthetic
+    stand-in for a batch of executors' shmem out files.  Program p published
+    its first completed[p] calls; order_seed shuffles the record order inside a
+    program (calls completing out of order).  Returns (out u32[], prog_off u64[nprog+1])."""
+    sigs = np.asarray(sigs, np.uint32)
+    rng = np.random.default_rng(order_seed) if order_seed is not None else None
+    parts, off = [], [0]
+    for p in range(len(prog_call) - 1):
+        c0 = int(prog_call[p])
+        idx = np.arange(int(completed[p]))
+        if rng is not None:
+            rng.shuffle(idx)
+        words = [np.array([idx.size], np.uint32)]
+        for i in idx:
+            c = c0 + int(i)
+            n, s = int(sig_cnt[c]), int(call_start[c])
+            words.append(np.array([i, i, np.uint32(np.int64(call_errno[c]) & 0xFFFFFFFF), 0, n, 0, 0], np.uint32))
+            words.append(sigs[s:s + n])
+        w = np.concatenate(words)
+        parts.append(w)
+        off.append(off[-1] + w.size)
+    return np.concatenate(parts) if parts else np.empty(0, np.uint32), np.array(off, np.uint64)

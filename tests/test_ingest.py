@@ -1,0 +1,167 @@
+"""Executor output regions -> triage batch (pkg/ipc/ipc.go:328-468 readOutCoverage).
+
+CPU: the readOutCoverage restatement against the REFERENCE executor's own
+regions (oracle/_ref/ref_harness, container only) and the committed fixture.
+GPU: k_ingest_exec_output bit-exact against the fixture (well-formed regions
+written by the reference executor plus one corrupted region per ipc.go error
+branch), then ingest -> checkNewSignal end to end against the oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.conftest import GOLDEN
+
+FIX = os.path.join(GOLDEN, "ingest", "exec_regions.npz")
+
+
+def load():
+    with np.load(FIX, allow_pickle=False) as f:
+        return {k: f[k] for k in f.files}
+
+
+def regions_of(fx):
+    po = fx["prog_off"].astype(np.int64)
+    pc = fx["prog_call"].astype(np.int64)
+    regs = [fx["out"][po[p]:po[p + 1]] for p in range(po.size - 1)]
+    return regs, np.diff(pc)
+
+
+def test_fixture_reproduced_by_restatement():
+    fx = load()
+    regs, ncalls = regions_of(fx)
+    out, po, pc, cs, cl, cp, ce, st = O.ingest_batch(regs, ncalls, fx["call_any"], fx["call_num"])
+    for k, v in dict(out=out, prog_off=po, prog_call=pc, exp_call_start=cs, exp_call_len=cl, exp_call_prio=cp,
+                     exp_call_errno=ce, exp_status=st).items():
+        np.testing.assert_array_equal(v, fx[k], err_msg=k)
+    # one region per ipc.go error branch is present
+    assert set(range(1, 10)) <= set(st.tolist())
+
+
+@pytest.mark.skipif(not os.path.exists(O.REF_HARNESS), reason="reference executor harness not built (container only)")
+def test_restatement_vs_reference_executor_regions():
+    from syzkaller_amd import synth
+
+    progs = []
+    cfg = synth.synth_default(bad_pc_ppm=200)
+    cl = synth.call_lengths(12, 6, 0, ragged=(0, 2500), seed=5)
+    pcs, cs, prio = synth.traces(cfg, 900, 12, 6, cl)
+    for p in range(12):
+        progs.append([(((prio[c] >> 1) & 1) == 0, pcs[cs[c]:cs[c] + cl[c]]) for c in range(p * 6, (p + 1) * 6)])
+    regions = O.run_reference_executor(progs, raw=True)
+    parsed = O.run_reference_executor(progs)
+    for reg, (completed, calls) in zip(regions, parsed):
+        st, info = O.read_out_coverage(reg, 6, list(range(6)))
+        assert st == 0 and sum(i is not None for i in info) == completed
+        for idx, err, sigs in calls:
+            e, so, sl, _, _ = info[idx]
+            assert e == err
+            np.testing.assert_array_equal(reg[so:so + sl], sigs)
+
+
+def test_frame_exec_output_roundtrip():
+    """The synthetic framer writes regions the restatement parses back."""
+    from syzkaller_amd import synth
+
+    sigs = np.arange(100, dtype=np.uint32)
+    cs = np.array([0, 10, 30, 60], np.uint64)
+    cnt = np.array([5, 0, 20, 7], np.uint32)
+    out, off = synth.frame_exec_output(sigs, cs, cnt, [2, 1], np.array([0, 2, 4]), np.array([0, -1, 22, 0]),
+                                       order_seed=3)
+    st0, i0 = O.read_out_coverage(out[off[0]:off[1]], 2)
+    st1, i1 = O.read_out_coverage(out[off[1]:off[2]], 2)
+    assert st0 == st1 == 0
+    assert i0[0][0] == 0 and i0[0][2] == 5 and i0[1][0] == -1 and i0[1][2] == 0
+    assert i1[0][0] == 22 and i1[0][2] == 20 and i1[1] is None
+
+
+def _dev_ingest(gpu, out, po, pc, call_any, call_num, want_cover=False):
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(gpu.dev)  # noqa: E731
+    r = gpu.ingest_exec_output(t(out, np.int32), t(po, np.int64), t(pc, np.int32), t(call_any, np.uint8),
+                               None if call_num is None else t(call_num, np.int32), want_cover=want_cover)
+    return t(out, np.int32), r
+
+
+def _np(x, dt):
+    return x.cpu().numpy().view(dt)
+
+
+@pytest.mark.gpu
+def test_ingest_matches_fixture(gpu):
+    fx = load()
+    _, r = _dev_ingest(gpu, fx["out"], fx["prog_off"], fx["prog_call"], fx["call_any"], fx["call_num"],
+                       want_cover=True)
+    np.testing.assert_array_equal(_np(r["prog_status"], np.int32), fx["exp_status"])
+    np.testing.assert_array_equal(_np(r["call_len"], np.uint32), fx["exp_call_len"])
+    np.testing.assert_array_equal(_np(r["call_errno"], np.int32), fx["exp_call_errno"])
+    np.testing.assert_array_equal(_np(r["call_prio"], np.uint8), fx["exp_call_prio"])
+    np.testing.assert_array_equal(_np(r["call_start"], np.uint64), fx["exp_call_start"])
+    assert r["n_failed"] == int((fx["exp_status"] != 0).sum())
+    assert int(_np(r["cover_len"], np.uint32).sum()) == 0
+
+
+@pytest.mark.gpu
+def test_ingest_without_call_num_and_empty(gpu):
+    fx = load()
+    _, r = _dev_ingest(gpu, fx["out"], fx["prog_off"], fx["prog_call"], fx["call_any"], None)
+    exp = fx["exp_status"].copy()
+    exp[exp == 4] = 0  # the callNum check is skipped without call_num
+    np.testing.assert_array_equal(_np(r["prog_status"], np.int32), exp)
+    _, r = _dev_ingest(gpu, np.empty(0, np.uint32), np.zeros(1, np.uint64), np.zeros(1, np.uint32),
+                       np.empty(0, np.uint8), None)
+    assert r["n_failed"] == 0
+
+
+@pytest.mark.gpu
+def test_ingest_rejects_out_of_bounds_offsets(gpu):
+    from syzkaller_amd._lib import SyzsigError
+
+    with pytest.raises(SyzsigError):
+        _dev_ingest(gpu, np.zeros(4, np.uint32), np.array([0, 9], np.uint64), np.array([0, 1], np.uint32),
+                    np.zeros(1, np.uint8), None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order_seed", [None, 7])
+def test_ingest_then_triage_vs_oracle(gpu, order_seed):
+    """64 programs x 32 calls: oracle executor -> executor regions (records in
+    call or shuffled completion order) -> device ingest -> batch checkNewSignal,
+    against the oracle's checkNewSignal on the same calls."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default(bad_pc_ppm=50)
+    nprog, cpp = 64, 32
+    cl = synth.call_lengths(nprog, cpp, 0, ragged=(0, 3000), seed=9)
+    pcs, cs, prio = synth.traces(cfg, 0, nprog, cpp, cl)
+    prog_call = synth.prog_call_index(nprog, cpp)
+    sigs, cnt, comp = O.exec_batch(pcs, cs, cl, prog_call)
+    rng = np.random.default_rng(1)
+    errno = np.where(((prio >> 1) & 1) == 0, rng.integers(1, 40, prio.size), 0).astype(np.int32)
+    call_any = ((prio & 1) == 0).astype(np.uint8)
+    out, po = synth.frame_exec_output(sigs, cs, cnt, comp, prog_call, errno, order_seed=order_seed)
+    dout, r = _dev_ingest(gpu, out, po, prog_call, call_any, np.tile(np.arange(cpp, dtype=np.uint32), nprog))
+    assert r["n_failed"] == 0
+    # un-published calls (after an abort) have errno -1 -> prio loses the errno bit, like signalPrio on Errno=-1
+    exec_ = np.zeros(prio.size, bool)
+    for p in range(nprog):
+        exec_[prog_call[p]:prog_call[p] + comp[p]] = True
+    hprio = np.where(exec_, prio, prio & 1).astype(np.uint8)
+    np.testing.assert_array_equal(_np(r["call_prio"], np.uint8), hprio)
+    np.testing.assert_array_equal(_np(r["call_len"], np.uint32), np.where(exec_, cnt, 0))
+    m0 = synth.m0(cfg, 2048, 200000)
+    ms = S.Serial(*m0).Deserialize(gpu.eng)
+    ns = S.Signal(None, gpu.eng)
+    pairs = torch.full((int(cnt.sum()) + 1,), -1, dtype=torch.int64, device=gpu.dev)
+    _, cnew, st = gpu.triage(ms, ns, dout, r["call_start"], r["call_len"], r["call_prio"], new_pairs=pairs)
+    oms, ons, obits, ocnew = O.triage_batch(m0[0], m0[1], sigs, cs, cnt, hprio)
+    np.testing.assert_array_equal(_np(cnew, np.uint8), ocnew)
+    r_ = np.nonzero(np.unpackbits(obits.view(np.uint8), bitorder="little"))[0].astype(np.uint64)
+    call = np.searchsorted(cs.astype(np.uint64) + cnt.astype(np.uint64), r_, side="right").astype(np.uint64)
+    op = np.unique((call << np.uint64(32)) | sigs[r_].astype(np.uint64))
+    assert st["new_pairs"] == op.size
+    np.testing.assert_array_equal(np.sort(_np(pairs[:op.size], np.uint64)), op)
+    assert ms.to_dict() == oms.to_dict()
+    assert ns.to_dict() == ons.to_dict()
