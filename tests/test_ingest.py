@@ -99,7 +99,13 @@ def test_ingest_matches_fixture(gpu):
     np.testing.assert_array_equal(_np(r["call_prio"], np.uint8), fx["exp_call_prio"])
     np.testing.assert_array_equal(_np(r["call_start"], np.uint64), fx["exp_call_start"])
     assert r["n_failed"] == int((fx["exp_status"] != 0).sum())
-    assert int(_np(r["cover_len"], np.uint32).sum()) == 0
+    regs, ncalls = regions_of(fx)
+    exp_cov = []
+    for reg, nc, pst in zip(regs, ncalls, fx["exp_status"]):
+        _, info = O.read_out_coverage(reg, int(nc))
+        exp_cov += [i[4] if (i is not None and pst == 0) else 0 for i in info]
+    np.testing.assert_array_equal(_np(r["cover_len"], np.uint32), exp_cov)
+    assert sum(exp_cov) == 1  # the well-formed region with comparisons carries one cover word
 
 
 @pytest.mark.gpu
