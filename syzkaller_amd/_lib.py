@@ -8,7 +8,7 @@ import os
 from ctypes import POINTER, c_char_p, c_int, c_int8, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsyzsig.so")
+LIB_PATH = os.environ.get("SYZSIG_LIB") or os.path.join(_HERE, "libsyzsig.so")  # SYZSIG_LIB: an experiment build
 
 SYZSIG_OK = 0
 SYZSIG_EIO = -5

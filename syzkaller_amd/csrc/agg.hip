@@ -665,8 +665,12 @@ __global__ __launch_bounds__(256) void k_agg_global_compact(const uint32_t* __re
 // distinct elements, whose maxSignal/newSignal home buckets share one slice of
 // each table (the same top bits of h), so a block's probes stay in one slice.
 // A block gathers its pairs in LDS and appends them with one global atomic
-// per flush.
-constexpr uint32_t kFinThreads = 256, kFinBuf = 4 * kFinThreads * 2;
+// per flush (a pair that finds the buffer full is appended directly).
+// Each thread takes kFinIlp elements per pass and issues the loads of all their
+// home buckets (maxSignal and newSignal) before walking any of them: the
+// kernel is bound by the latency of these dependent random reads, not by
+// bandwidth, so more of them in flight per wave is what makes it faster.
+constexpr uint32_t kFinThreads = 256, kFinBuf = 4 * kFinThreads * 2, kFinIlp = 2;
 
 __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __restrict__ dist_e,
                                                               const uint4* __restrict__ dist_f,
@@ -685,6 +689,7 @@ __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __
 		s_n = 0;
 	__syncthreads();
 	auto flush = [&](uint32_t nb) {  // every thread; nb = s_n read after a barrier
+		nb = min(nb, kFinBuf);
 		if (threadIdx.x == 0)
 			s_base = atomicAdd(npairs, (unsigned long long)nb);
 		__syncthreads();
@@ -695,61 +700,85 @@ __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __
 			s_n = 0;
 		__syncthreads();
 	};
+	auto emit = [&](uint64_t v) {
+		const uint32_t k = atomicAdd(&s_n, 1u);
+		if (k < kFinBuf)
+			buf[k] = v;
+		else
+			pairs[atomicAdd(npairs, 1ull)] = v;
+	};
 	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
 		const uint32_t n = cnt[r] == kAggOverflow ? 0 : cnt[r];
-		for (uint32_t i0 = 0; i0 < n; i0 += kFinThreads) {
-			const uint32_t i = i0 + threadIdx.x;
-			if (i < n) {
-				const uint64_t o = (uint64_t)r * kAggRegion + i;
-				const uint32_t e = dist_e[o];
-				const uint4 f4 = dist_f[o];
-				const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
-				int top = -1;
+		for (uint32_t i0 = 0; i0 < n; i0 += kFinIlp * kFinThreads) {
+			uint32_t e[kFinIlp];
+			uint4 f4[kFinIlp];
+			int top[kFinIlp];
+#pragma unroll
+			for (uint32_t k = 0; k < kFinIlp; k++) {
+				const uint32_t i = i0 + k * kFinThreads + threadIdx.x;
+				const uint64_t o = (uint64_t)r * kAggRegion + min(i, n - 1);
+				e[k] = dist_e[o];
+				f4[k] = dist_f[o];
+				top[k] = -1;
+				const uint32_t f[4] = {f4[k].x, f4[k].y, f4[k].z, f4[k].w};
 #pragma unroll
 				for (int l = 0; l < 4; l++)
-					if (l < (int)lm.n && f[l] != kAggNone)
-						top = l;
-				if (top >= 0) {
-					// one probe sequence: insert M_final if absent, else read M0
-					const int8_t P = lm.val[top];
-					const uint64_t word = make_slot(e, P);
-					uint64_t old = 0;
-					const int64_t idx = tbl_find_or_insert(slots, bmask, e, word, old, max_probe);
-					if (idx < 0) {
-						ovf++;
-					} else {
-						const bool present = slot_live(old);  // (old == 0: inserted just now)
-						const int p0 = present ? (int)slot_prio(old) : -1000;
-						if ((int)P > p0) {
-							if (old != 0)
-								slots[idx] = word;  // one entry per element: no other writer
-							inserted += !present;   // fresh, or an "absent" marker going live
-							changed++;
-							const int rr = tbl_merge(ns_slots, ns_bmask, e, P);
-							ns_ins += rr == 1;
-							ovf += rr < 0;
-							// the staircase: first records of strictly rising level above M0[e]
-							uint32_t mk = kAggNone;
+					if (i < n && l < (int)lm.n && f[l] != kAggNone)
+						top[k] = l;
+			}
+			Bucket bm[kFinIlp], bn[kFinIlp];
 #pragma unroll
-							for (int l = 3; l >= 0; l--) {
-								if (l > top || f[l] == kAggNone)
-									continue;
-								if ((int)lm.val[l] <= p0)
-									break;
-								if (f[l] < mk) {
-									mk = f[l];
-									const uint64_t c = c0 + f[l];
-									call_new[c] = 1;
-									buf[atomicAdd(&s_n, 1u)] = (c << 32) | e;
-								}
-							}
-						}
+			for (uint32_t k = 0; k < kFinIlp; k++) {
+				if (top[k] >= 0) {
+					bm[k] = load_bucket(slots + (home_bucket(e[k], bmask) << kBucketShift));
+					if (ns_slots)
+						bn[k] = load_bucket(ns_slots + (home_bucket(e[k], ns_bmask) << kBucketShift));
+				}
+			}
+#pragma unroll
+			for (uint32_t k = 0; k < kFinIlp; k++) {
+				if (top[k] < 0)
+					continue;
+				const uint32_t f[4] = {f4[k].x, f4[k].y, f4[k].z, f4[k].w};
+				// one probe sequence: insert M_final if absent, else read M0
+				const int8_t P = lm.val[top[k]];
+				const uint64_t word = make_slot(e[k], P);
+				uint64_t old = 0;
+				const int64_t idx = tbl_find_or_insert_from(slots, bmask, e[k], word, old, max_probe, bm[k]);
+				if (idx < 0) {
+					ovf++;
+					continue;
+				}
+				const bool present = slot_live(old);  // (old == 0: inserted just now)
+				const int p0 = present ? (int)slot_prio(old) : -1000;
+				if ((int)P <= p0)
+					continue;
+				if (old != 0)
+					slots[idx] = word;  // one entry per element: no other writer
+				inserted += !present;   // fresh, or an "absent" marker going live
+				changed++;
+				const int rr = tbl_merge_from(ns_slots, ns_bmask, e[k], P, bn[k]);
+				ns_ins += rr == 1;
+				ovf += rr < 0;
+				// the staircase: first records of strictly rising level above M0[e]
+				uint32_t mk = kAggNone;
+#pragma unroll
+				for (int l = 3; l >= 0; l--) {
+					if (l > top[k] || f[l] == kAggNone)
+						continue;
+					if ((int)lm.val[l] <= p0)
+						break;
+					if (f[l] < mk) {
+						mk = f[l];
+						const uint64_t c = c0 + f[l];
+						call_new[c] = 1;
+						emit((c << 32) | e[k]);
 					}
 				}
 			}
 			__syncthreads();
 			const uint32_t nb = s_n;
-			if (nb > kFinBuf - 4 * kFinThreads)
+			if (nb > kFinBuf / 2)
 				flush(nb);
 		}
 	}

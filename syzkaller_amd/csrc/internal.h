@@ -269,6 +269,38 @@ __device__ __forceinline__ int64_t tbl_find_or_insert(uint64_t* slots, uint64_t 
 	return -1;
 }
 
+// tbl_find_or_insert with the home bucket already loaded (B = load_bucket of
+// home_bucket(key)): a thread can issue the home-bucket loads of several keys
+// before it walks any of them.  A stale B is safe for the same reason a fresh
+// one is: slots only go EMPTY -> key, and the CAS sees the current word.
+__device__ __forceinline__ int64_t tbl_find_or_insert_from(uint64_t* slots, uint64_t bmask, uint32_t key,
+                                                           uint64_t ins, uint64_t& old, uint64_t max_probe, Bucket B)
+{
+	uint64_t b = home_bucket(key, bmask);
+	for (uint64_t n = 0; n < max_probe; n++) {
+		uint64_t* bp = slots + (b << kBucketShift);
+		if (n)
+			B = load_bucket(bp);
+#pragma unroll
+		for (int i = 0; i < (int)kBucketSlots; i++) {
+			uint64_t s = B.s[i];
+			if (s == kSlotEmpty) {
+				s = atomicCAS(reinterpret_cast<unsigned long long*>(bp + i), 0ull, (unsigned long long)ins);
+				if (s == kSlotEmpty) {
+					old = 0;
+					return (int64_t)((b << kBucketShift) + i);
+				}
+			}
+			if (slot_key(s) == key) {
+				old = s;
+				return (int64_t)((b << kBucketShift) + i);
+			}
+		}
+		b = (b + 1) & bmask;
+	}
+	return -1;
+}
+
 __device__ __forceinline__ uint64_t max_probe_for(uint64_t bmask)
 {
 	uint64_t nb = bmask + 1;
@@ -280,6 +312,20 @@ __device__ __forceinline__ int tbl_merge(uint64_t* slots, uint64_t bmask, uint32
 {
 	uint64_t v = make_slot(key, prio), old;
 	int64_t idx = tbl_find_or_insert(slots, bmask, key, v, old, max_probe_for(bmask));
+	if (idx < 0)
+		return -1;
+	if (old == 0)
+		return 1;
+	if (old < v)
+		atomicMax(reinterpret_cast<unsigned long long*>(slots + idx), (unsigned long long)v);
+	return 0;
+}
+
+// tbl_merge from a preloaded home bucket (see tbl_find_or_insert_from).
+__device__ __forceinline__ int tbl_merge_from(uint64_t* slots, uint64_t bmask, uint32_t key, int8_t prio, Bucket B)
+{
+	uint64_t v = make_slot(key, prio), old;
+	int64_t idx = tbl_find_or_insert_from(slots, bmask, key, v, old, max_probe_for(bmask), B);
 	if (idx < 0)
 		return -1;
 	if (old == 0)
