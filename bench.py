@@ -118,6 +118,49 @@ def cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, calls_per_prog, target_s):
                       f"oracle/oracle.c single thread, {dt:.2f} s"}
 
 
+def ingest_stage(dev, sigs, cs, cnt, prio, comp, P, C, reps=5):
+    """Frame the batch as executor output regions (executor.h:566-604 records,
+    one region per program) on device, then time readOutCoverage on device
+    (syzsig_ingest_exec_output_dev, pkg/ipc/ipc.go:328-468) over all of them.
+    Not part of `value`; reported as stages.ingest_ms.  Returns (ms, check_ok)."""
+    d = sigs.device
+    n = P * C
+    ar = torch.arange(n, device=d)
+    callidx, progidx = ar % C, ar // C
+    done = callidx < comp.to(torch.int64)[progidx]
+    c64 = cnt.to(torch.int64)
+    L = torch.where(done, c64 + 7, torch.zeros_like(c64)).view(P, C)
+    poff = torch.zeros(P + 1, dtype=torch.int64, device=d)
+    poff[1:] = (L.sum(1) + 1).cumsum(0)
+    roff = (poff[:-1].unsqueeze(1) + 1 + L.cumsum(1) - L).view(-1)
+    out = torch.zeros(int(poff[-1].item()), dtype=torch.int32, device=d)
+    out[poff[:-1]] = comp.to(torch.int32)
+    p64 = prio.to(torch.int64)
+    errno = torch.where(((p64 >> 1) & 1) == 0, 22, 0)
+    z = torch.zeros_like(c64)
+    hdr = torch.stack([callidx, callidx, errno, z, c64, z, z], 1)[done]
+    out[(roff[done].unsqueeze(1) + torch.arange(7, device=d)).view(-1)] = hdr.view(-1).to(torch.int32)
+    rep = c64[done]
+    call_of = torch.repeat_interleave(torch.arange(rep.numel(), device=d), rep)
+    within = torch.arange(call_of.numel(), device=d) - (rep.cumsum(0) - rep)[call_of]
+    out[(roff[done] + 7)[call_of] + within] = sigs[cs[done][call_of] + within]
+    del call_of, within, hdr
+    any_ = ((p64 & 1) == 0).to(torch.uint8)
+    pc = (torch.arange(P + 1, device=d, dtype=torch.int32) * C)
+    ms = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        r = dev.ingest_exec_output(out, poff, pc, any_, callidx.to(torch.int32))
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t) * 1e3)
+    exp_prio = torch.where(done, p64, p64 & 1)
+    ok = (r["n_failed"] == 0 and bool((r["call_len"].to(torch.int64) == torch.where(done, c64, z)).all())
+          and bool((r["call_prio"].to(torch.int64) == exp_prio).all()))
+    del out
+    return float(np.median(ms)), ok
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -224,6 +267,7 @@ def main():
         tr = torch.tensor([nrec], dtype=torch.int64, device=dev.dev)
         dist.all_reduce(tr)
         total_rec = int(tr.item())
+    ingest_ms, ingest_ok = ingest_stage(dev, sigs, cs, cnt, prio, comp, P, C) if not distributed else (None, None)
     ms_per_step = dt / a.steps * 1e3
     value = total_rec * a.steps / dt
     s0 = stats[-1]
@@ -266,7 +310,8 @@ def main():
                          "avg_launch_ms": k3_ms},
             "stages": {"edge_ms": float(np.median(edge_ms)), "part_ms": part_ms, "agg_ms": probe_ms,
                        "finalize_ms": decide_ms,
-                       "edge_pcs_per_s": npc / (np.median(edge_ms) * 1e-3)},
+                       "edge_pcs_per_s": npc / (np.median(edge_ms) * 1e-3),
+                       "ingest_ms": ingest_ms, "ingest_check": ingest_ok},
             "triage": {k: v for k, v in s0.items() if k not in ("probe_ms", "decide_ms", "part_ms")},
         }
     if rank == 0:
