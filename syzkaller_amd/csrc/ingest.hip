@@ -25,7 +25,9 @@
 //
 // One thread per program: the records of a region form a dependent chain (each
 // record's length places the next), so a program is a sequential walk of <=
-// len(p.Calls) headers; programs are independent.  prio = signalPrio
+// len(p.Calls) headers; programs are independent.  Nothing else in the kernel
+// waits on memory: which calls have a record is kept in LDS, and each call's
+// outputs are written exactly once.  prio = signalPrio
 // (syz-fuzzer/fuzzer.go:513-521) from errno and the caller's per-call
 // CallContainsAny bit (prog/any.go:177-185, a property of the program).
 #include "internal.h"
@@ -35,15 +37,21 @@ namespace syz {
 constexpr uint32_t kNilLen = 0xFFFFFFFFu;  // "Signal == nil" while a program is parsed
 constexpr uint32_t kCompSizeMask = 6, kCompSize8 = 6, kCompConstMask = 1;  // ipc.go:185-190
 
-__global__ void k_ingest_exec_output(const uint32_t* __restrict__ out, uint64_t nwords,
-                                     const uint64_t* __restrict__ prog_off, uint64_t nprog,
-                                     const uint32_t* __restrict__ prog_call, uint64_t ncalls,
-                                     const uint32_t* __restrict__ call_num, const uint8_t* __restrict__ call_any,
-                                     uint64_t* __restrict__ call_start, uint32_t* __restrict__ call_len,
-                                     uint8_t* __restrict__ call_prio, int32_t* __restrict__ call_errno,
-                                     uint64_t* __restrict__ cover_start, uint32_t* __restrict__ cover_len,
-                                     int32_t* __restrict__ prog_status, unsigned long long* __restrict__ cnt)
+constexpr uint32_t kIngestThreads = 256;
+constexpr uint32_t kSeenCalls = 256;  // calls per program tracked in LDS (beyond: a global sentinel)
+
+__global__ __launch_bounds__(kIngestThreads) void k_ingest_exec_output(
+	const uint32_t* __restrict__ out, uint64_t nwords, const uint64_t* __restrict__ prog_off, uint64_t nprog,
+	const uint32_t* __restrict__ prog_call, uint64_t ncalls, const uint32_t* __restrict__ call_num,
+	const uint8_t* __restrict__ call_any, uint64_t* __restrict__ call_start, uint32_t* __restrict__ call_len,
+	uint8_t* __restrict__ call_prio, int32_t* __restrict__ call_errno, uint64_t* __restrict__ cover_start,
+	uint32_t* __restrict__ cover_len, int32_t* __restrict__ prog_status, unsigned long long* __restrict__ cnt)
 {
+	// "Signal != nil" of the program's first kSeenCalls calls, one bitmap per
+	// thread: the record walk is the only dependent chain, the call arrays are
+	// written once and never read back.
+	__shared__ uint32_t seen_w[kIngestThreads][kSeenCalls / 32 + 1];  // +1: no bank aliasing between threads
+	uint32_t* seen = seen_w[threadIdx.x];
 	const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (p >= nprog)
 		return;
@@ -55,15 +63,14 @@ __global__ void k_ingest_exec_output(const uint32_t* __restrict__ out, uint64_t 
 		return;
 	}
 	const uint64_t nc = c1 - c0;
-	for (uint64_t c = c0; c < c1; c++) {
-		call_start[c] = lo;
+#pragma unroll
+	for (uint32_t w = 0; w < kSeenCalls / 32; w++)
+		seen[w] = 0;
+	for (uint64_t c = c0 + kSeenCalls; c < c1; c++)  // long programs only
 		call_len[c] = kNilLen;
-		call_errno[c] = -1;
-		if (cover_start) {
-			cover_start[c] = lo;
-			cover_len[c] = 0;
-		}
-	}
+	auto is_seen = [&](uint64_t i) -> bool {
+		return i < kSeenCalls ? (seen[i >> 5] >> (i & 31)) & 1 : call_len[c0 + i] != kNilLen;
+	};
 	int32_t status = SYZSIG_INGEST_OK;
 	uint64_t pos = lo;
 	if (pos >= hi) {
@@ -87,22 +94,26 @@ __global__ void k_ingest_exec_output(const uint32_t* __restrict__ out, uint64_t 
 				status = SYZSIG_INGEST_ECALLNUM;
 				break;
 			}
-			if (call_len[c] != kNilLen) {  // ipc.go:396-400 (an empty Signal is non-nil too)
+			if (is_seen(idx)) {  // ipc.go:396-400 (an empty Signal is non-nil too)
 				status = SYZSIG_INGEST_EDOUBLE;
 				break;
 			}
-			call_errno[c] = (int32_t)err;
 			if (nsig > hi - pos) {  // ipc.go:403-407
 				status = SYZSIG_INGEST_ESIGNAL;
 				break;
 			}
-			call_start[c] = pos;
-			call_len[c] = nsig;
+			const uint64_t sig_pos = pos;
 			pos += nsig;
 			if (ncover > hi - pos) {  // ipc.go:411-415
 				status = SYZSIG_INGEST_ECOVER;
 				break;
 			}
+			if (idx < kSeenCalls)
+				seen[idx >> 5] |= 1u << (idx & 31);
+			call_start[c] = sig_pos;
+			call_len[c] = nsig;
+			call_errno[c] = (int32_t)err;
+			call_prio[c] = signal_prio(err != 0, call_any[c]);
 			if (cover_start) {
 				cover_start[c] = pos;
 				cover_len[c] = ncover;
@@ -127,18 +138,21 @@ __global__ void k_ingest_exec_output(const uint32_t* __restrict__ out, uint64_t 
 			}
 		}
 	}
+	// calls without a record: Errno = -1, Signal = nil (ipc.go:362-365); a failed
+	// Exec is retried, so none of its calls reaches checkNewSignal
 	const bool bad = status != SYZSIG_INGEST_OK;
-	for (uint64_t c = c0; c < c1; c++) {
-		if (bad) {  // the Exec is retried; nothing of it reaches checkNewSignal
-			call_errno[c] = -1;
-			if (cover_start)
-				cover_len[c] = 0;
+	for (uint64_t i = 0; i < nc; i++) {
+		if (!bad && is_seen(i))
+			continue;
+		const uint64_t c = c0 + i;
+		call_start[c] = lo;
+		call_len[c] = 0;
+		call_errno[c] = -1;
+		call_prio[c] = signal_prio(1, call_any[c]);
+		if (cover_start) {
+			cover_start[c] = lo;
+			cover_len[c] = 0;
 		}
-		if (bad || call_len[c] == kNilLen) {
-			call_start[c] = lo;
-			call_len[c] = 0;
-		}
-		call_prio[c] = signal_prio(call_errno[c] != 0, call_any[c]);
 	}
 	prog_status[p] = status;
 	if (bad)
@@ -165,9 +179,8 @@ extern "C" int syzsig_ingest_exec_output_dev(syzsig_ctx* ctx, const uint32_t* d_
 	if (nprog == 0)
 		return SYZSIG_OK;
 	SYZ_TRY(counters_reset(ctx));
-	constexpr int kThreads = 256;
-	const uint64_t blocks = (nprog + kThreads - 1) / kThreads;
-	k_ingest_exec_output<<<(unsigned)blocks, kThreads, 0, ctx->stream>>>(
+	const uint64_t blocks = (nprog + kIngestThreads - 1) / kIngestThreads;
+	k_ingest_exec_output<<<(unsigned)blocks, kIngestThreads, 0, ctx->stream>>>(
 		d_out, nwords, d_prog_off, nprog, d_prog_call, ncalls, d_call_num, d_call_any, d_call_start, d_call_len,
 		d_call_prio, d_call_errno, d_cover_start, d_cover_len, d_prog_status, ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
