@@ -977,11 +977,14 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
-	std::vector<uint32_t> hc(P);
-	std::vector<uint64_t> hb(P + 1);
-	SYZ_HIP(hipMemcpyAsync(hc.data(), dc, P * 4, hipMemcpyDeviceToHost, s));
-	SYZ_HIP(hipMemcpyAsync(hb.data(), rec_base, (P + 1) * 8, hipMemcpyDeviceToHost, s));
+	static_assert(kPinCounts + kAggMaxParts * 4 + (kAggMaxParts + 1) * 8 <= kPinBytes, "pinned staging");
+	uint64_t* hbp = (uint64_t*)(ctx->h_pin + kPinCounts);
+	uint32_t* hcp = (uint32_t*)(hbp + kAggMaxParts + 1);
+	SYZ_HIP(hipMemcpyAsync(hcp, dc, P * 4, hipMemcpyDeviceToHost, s));
+	SYZ_HIP(hipMemcpyAsync(hbp, rec_base, (P + 1) * 8, hipMemcpyDeviceToHost, s));
 	SYZ_HIP(hipStreamSynchronize(s));
+	const std::vector<uint32_t> hc(hcp, hcp + P);
+	const std::vector<uint64_t> hb(hbp, hbp + P + 1);
 	if (ctx->timing) {
 		float t0 = 0, t1 = 0;
 		SYZ_HIP(hipEventElapsedTime(&t0, ctx->ev[0], ctx->ev[1]));
@@ -1088,7 +1091,8 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 	SYZ_TRY(ws_grow_keep(ctx, 15, need_pairs * 8 + 64, *npairs_io * 8, &pr));
 	*pairs_out = (uint64_t*)pr;
 	SYZ_TRY(counters_reset(ctx));
-	SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], npairs_io, 8, hipMemcpyHostToDevice, s));
+	memcpy(ctx->h_pin + kPinPairs, npairs_io, 8);  // consumed before the counters_fetch below
+	SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], ctx->h_pin + kPinPairs, 8, hipMemcpyHostToDevice, s));
 	syzsig_set* nsp = *ns;
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -1165,7 +1169,8 @@ int pairs_from_bits(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* bits
 	SYZ_TRY(ws_grow_keep(ctx, 15, (*npairs_io + n) * 8 + 64, *npairs_io * 8, &out));
 	*pairs_io = (uint64_t*)out;
 	SYZ_TRY(counters_reset(ctx));
-	SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], npairs_io, 8, hipMemcpyHostToDevice, s));
+	memcpy(ctx->h_pin + kPinPairs, npairs_io, 8);  // consumed before the counters_fetch below
+	SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], ctx->h_pin + kPinPairs, 8, hipMemcpyHostToDevice, s));
 	k_pairs_set<<<grid_for(n, 256, 8192), 256, 0, s>>>((const uint64_t*)raw, n, (uint64_t*)set, C,
 	                                                   &ctx->d_cnt[kCntAux]);
 	k_pairs_compact<<<grid_for(C, 256, 8192), 256, 0, s>>>((const uint64_t*)set, C, (uint64_t*)out,

@@ -56,6 +56,9 @@ struct Workspace {
 	size_t size = 0;
 };
 
+// ctx->h_pin layout
+constexpr size_t kPinMask = 0, kPinPairs = 64, kPinCounts = 1024, kPinBytes = 64 * 1024;
+
 }  // namespace syz
 
 struct syzsig_ctx {
@@ -64,6 +67,9 @@ struct syzsig_ctx {
 	hipStream_t stream = nullptr;
 	unsigned long long* d_cnt = nullptr;  // kNumCounters
 	unsigned long long* h_cnt = nullptr;  // pinned mirror
+	// pinned staging for the small per-batch copies (a pageable copy is staged
+	// and synchronous): syz::kPin* offsets
+	char* h_pin = nullptr;
 	// grow-only scratch buffers by role: 0-2 set ops, 3-6 triage candidates and
 	// small state, 7-10 host uploads of minimize, 11-14 triage partitions and
 	// minimize internals and triage pairs (13-15), 16-23 + 30-31 triage aggregation,

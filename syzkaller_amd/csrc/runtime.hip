@@ -104,6 +104,8 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 		e = hipMalloc(&c->d_cnt, sizeof(unsigned long long) * syz::kNumCounters);
 	if (e == hipSuccess)
 		e = hipHostMalloc(&c->h_cnt, sizeof(unsigned long long) * syz::kNumCounters, hipHostMallocDefault);
+	if (e == hipSuccess)
+		e = hipHostMalloc(&c->h_pin, syz::kPinBytes, hipHostMallocDefault);
 	if (e != hipSuccess) {
 		syzsig_ctx_destroy(c);
 		return syz::hip_fail(e, "ctx_create", __FILE__, __LINE__);
@@ -134,6 +136,8 @@ void syzsig_ctx_destroy(syzsig_ctx* c)
 		(void)hipFree(c->d_cnt);
 	if (c->h_cnt)
 		(void)hipHostFree(c->h_cnt);
+	if (c->h_pin)
+		(void)hipHostFree(c->h_pin);
 	for (auto& e : c->ev)
 		if (e)
 			(void)hipEventDestroy(e);

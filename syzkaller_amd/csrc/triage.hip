@@ -454,7 +454,7 @@ int batch_total_records(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t* total,
 	    b->call_prio, b->call_len, b->call_start, b->ncalls, b->nrec, (uint32_t*)dmask,
 	    (unsigned long long*)((char*)dmask + 32), (unsigned long long*)((char*)dmask + 40));
 	SYZ_HIP(hipGetLastError());
-	uint32_t hmask[12];
+	uint32_t* hmask = (uint32_t*)(ctx->h_pin + kPinMask);
 	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 48, hipMemcpyDeviceToHost, ctx->stream));
 	SYZ_HIP(hipStreamSynchronize(ctx->stream));
 	memcpy(total, &hmask[8], 8);
