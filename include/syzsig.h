@@ -112,6 +112,14 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, const uint32
                         const int8_t* d_prios, uint64_t nctx, uint64_t hint_distinct, uint8_t* d_keep,
                         uint64_t* n_out);
 
+/* ---- pkg/cover/cover.go:7-30: type Cover map[uint32]struct{} ----
+ * A Cover is a syzsig_set whose entries all carry prio 0.  Merge(raw)
+ * (cover.go:9-18) allocates a NULL *cov even when n == 0, then inserts every
+ * PC (manager corpusCover.Merge, syz-manager/manager.go:998).  Len is
+ * syzsig_len; Serialize (cover.go:20-26) is syzsig_serialize's elems. */
+int syzsig_cover_merge(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* raw, uint64_t n);
+int syzsig_cover_merge_dev(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* d_raw, uint64_t n);
+
 /* ---- syz-fuzzer/fuzzer.go:494-511 checkNewSignal (+ signalPrio :513-521 by caller) ----
  * One program's CallInfo signals in host memory: call i's raw signal is
  * sigs[call_start[i] .. +call_len[i]) with prio call_prio[i].  Sequential over

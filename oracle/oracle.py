@@ -320,3 +320,18 @@ def ingest_batch(regions, ncalls, call_any, call_num=None):
                 cl[c0 + i] = inf[2]
     cp = np.array([signal_prio(int(e), int(a)) for e, a in zip(ce, call_any)], np.uint8)
     return (out, np.array(prog_off, np.uint64), np.array(prog_call, np.uint32), cs, cl, cp, ce, st)
+
+
+class OCover:
+    """pkg/cover/cover.go:7-30 restated: Cover = map[uint32]struct{} (None = nil map)."""
+
+    def __init__(self):
+        self.c = None
+
+    def Merge(self, raw):  # cover.go:9-18
+        if self.c is None:
+            self.c = set()
+        self.c.update(int(x) for x in np.asarray(raw, np.uint32))
+
+    def Serialize(self):  # cover.go:20-26
+        return sorted(self.c or ())

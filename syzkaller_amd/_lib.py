@@ -80,6 +80,8 @@ SIGNATURES = {
     "syzsig_diff_raw": (c_int, [_P, _P, _P, c_uint64, c_uint8, _PP]),
     "syzsig_intersection": (c_int, [_P, _P, _P, _PP]),
     "syzsig_merge": (c_int, [_P, _PP, _P]),
+    "syzsig_cover_merge": (c_int, [_P, _PP, _P, c_uint64]),
+    "syzsig_cover_merge_dev": (c_int, [_P, _PP, _P, c_uint64]),
     "syzsig_minimize": (c_int, [_P, _P, _P, _P, c_uint64, c_uint64, _P, POINTER(c_uint64)]),
     "syzsig_minimize_dev": (c_int, [_P, _P, _P, _P, c_uint64, c_uint64, _P, POINTER(c_uint64)]),
     "syzsig_check_new_signal": (c_int, [_P, _PP, _PP, _P, c_uint64, _P, _P, _P, c_uint32, _P,

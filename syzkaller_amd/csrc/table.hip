@@ -580,6 +580,43 @@ int syzsig_intersection(syzsig_ctx* ctx, const syzsig_set* s, const syzsig_set* 
 	});
 }
 
+// pkg/cover/cover.go:9-18 Cover.Merge(raw): the receiver is allocated when nil
+// (even for an empty raw), then every PC is inserted; a Cover's entries all
+// carry prio 0 (map[uint32]struct{}: the value is unused).
+static int cover_merge_dev(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* d_raw, uint64_t n)
+{
+	if (!*cov)
+		SYZ_TRY(syzsig_set_make(ctx, n, cov));
+	if (n == 0)
+		return SYZSIG_OK;
+	syzsig_set* s = *cov;
+	SYZ_TRY(set_reserve(s, n));
+	SYZ_TRY(counters_reset(ctx));
+	k_from_raw<<<grid_for(n, 256), 256, 0, ctx->stream>>>(s->slots, s->nbuckets - 1, d_raw, n, 0, ctx->d_cnt);
+	SYZ_HIP(hipGetLastError());
+	SYZ_TRY(counters_fetch(ctx));
+	if (ctx->h_cnt[kCntOverflow])
+		return fail(SYZSIG_EIO, "cover merge overflow (internal error)");
+	s->len += ctx->h_cnt[kCntInserted];
+	return SYZSIG_OK;
+}
+
+int syzsig_cover_merge(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* raw, uint64_t n)
+{
+	if (!ctx || !cov || (n && !raw))
+		return fail(SYZSIG_EINVAL, "cover_merge: NULL argument");
+	void* d = nullptr;
+	SYZ_TRY(upload(ctx, 0, raw, n * 4, &d));
+	return cover_merge_dev(ctx, cov, (const uint32_t*)d, n);
+}
+
+int syzsig_cover_merge_dev(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* d_raw, uint64_t n)
+{
+	if (!ctx || !cov || (n && !d_raw))
+		return fail(SYZSIG_EINVAL, "cover_merge_dev: NULL argument");
+	return cover_merge_dev(ctx, cov, d_raw, n);
+}
+
 int syzsig_merge(syzsig_ctx* ctx, syzsig_set** sp, const syzsig_set* s1)
 {
 	if (!ctx || !sp)

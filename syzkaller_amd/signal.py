@@ -20,7 +20,7 @@ import numpy as np
 from . import _lib
 from ._lib import check
 
-__all__ = ["Engine", "engine", "Signal", "Serial", "Context", "FromRaw", "Minimize", "signal_prio",
+__all__ = ["Engine", "engine", "Signal", "Cover", "Serial", "Context", "FromRaw", "Minimize", "signal_prio",
            "check_new_signal"]
 
 
@@ -174,6 +174,35 @@ class Signal:
 
     def copy_from(self, src):
         check(self._e.L.syzsig_set_copy_from(self._e.h, self.handle, src.handle))
+
+
+class Cover:
+    """type Cover map[uint32]struct{} (pkg/cover/cover.go:7), device-resident;
+    the zero value is nil, as in Go."""
+
+    __slots__ = ("_s",)
+
+    def __init__(self, eng=None):
+        self._s = Signal(None, eng)
+
+    def is_nil(self):
+        return self._s.is_nil()
+
+    def Merge(self, raw):
+        """cover.go:9-18 (allocates a nil receiver, even for an empty raw)."""
+        raw = np.ascontiguousarray(raw, dtype=np.uint32)
+        e = self._s._e
+        h = ctypes.c_void_p(self._s.handle.value or 0)
+        check(e.L.syzsig_cover_merge(e.h, ctypes.byref(h), _ptr(raw), raw.size))
+        if self._s.is_nil() and h.value:
+            self._s._h = h
+
+    def Serialize(self):
+        """cover.go:20-26: the PCs in unspecified order."""
+        return self._s.Serialize().Elems if not self._s.is_nil() else np.empty(0, np.uint32)
+
+    def __len__(self):
+        return self._s.Len()
 
 
 class Serial:
