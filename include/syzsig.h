@@ -120,6 +120,26 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, const uint32
 int syzsig_cover_merge(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* raw, uint64_t n);
 int syzsig_cover_merge_dev(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* d_raw, uint64_t n);
 
+/* ---- syz-fuzzer/proc.go:107-140 triageInput signal re-runs, over a batch ----
+ * Item i's newSignal (corpusSignalDiff of its input signal, serialized) is
+ * elems/prios[item_off[i] .. item_off[i+1]); item_flags[i] = SYZSIG_TRIAGE_*.
+ * Item i's re-runs are r = i*runs .. i*runs+runs-1 (runs = signalRuns, <= 8):
+ * run r's raw signal is run_sigs[run_off[r] .. run_off[r+1]) with
+ * run_prio[r] = signalPrio, run_errno[r] = its Errno, run_exec[r] = 0 when
+ * len(info) == 0.  Applies the loop of proc.go:119-139 (skip and count runs
+ * that did not execute or failed; newSignal = newSignal.Intersection(run);
+ * drop the item when it empties unless minimized, or after more than
+ * runs/2+1 skipped runs).  Writes item_keep[i] (1 = the item goes on to
+ * minimization and the corpus) and elem_keep[j] (1 = element j is in the
+ * item's final newSignal).  All pointers are device pointers. */
+#define SYZSIG_TRIAGE_MINIMIZED 1 /* item.flags & ProgMinimized */
+#define SYZSIG_TRIAGE_ORIG_OK 2   /* item.info.Errno == 0 */
+int syzsig_triage_runs_dev(syzsig_ctx* ctx, const uint64_t* d_item_off, uint64_t nitems, const uint32_t* d_elems,
+                           const int8_t* d_prios, const uint8_t* d_item_flags, uint32_t runs,
+                           const uint64_t* d_run_off, const uint32_t* d_run_sigs, const uint8_t* d_run_prio,
+                           const int32_t* d_run_errno, const uint8_t* d_run_exec, uint8_t* d_item_keep,
+                           uint8_t* d_elem_keep);
+
 /* ---- syz-fuzzer/fuzzer.go:494-511 checkNewSignal (+ signalPrio :513-521 by caller) ----
  * One program's CallInfo signals in host memory: call i's raw signal is
  * sigs[call_start[i] .. +call_len[i]) with prio call_prio[i].  Sequential over

@@ -335,3 +335,31 @@ class OCover:
 
     def Serialize(self):  # cover.go:20-26
         return sorted(self.c or ())
+
+
+def triage_runs(item_off, elems, prios, item_flags, runs, run_off, run_sigs, run_prio, run_errno, run_exec):
+    """syz-fuzzer/proc.go:107-140 restated per item with the oracle Signal ops.  Returns (item_keep u8[],
+    final newSignal per item as a dict elem -> prio, or None if dropped)."""
+    keep, finals = [], []
+    for i in range(len(item_off) - 1):
+        a, b = int(item_off[i]), int(item_off[i + 1])
+        ns = deserialize(elems[a:b], prios[a:b])
+        minimized, orig_ok = bool(item_flags[i] & 1), bool(item_flags[i] & 2)
+        ok = ns.Len() > 0  # proc.go:109-111
+        notexec = 0
+        for r in range(runs):
+            if not ok:
+                break
+            rr = i * runs + r
+            ra, rb = int(run_off[rr]), int(run_off[rr + 1])
+            if not run_exec[rr] or rb == ra or (orig_ok and run_errno[rr] != 0):  # proc.go:122-128
+                notexec += 1
+                if notexec > runs // 2 + 1:
+                    ok = False
+                continue
+            ns = ns.Intersection(from_raw(run_sigs[ra:rb], int(run_prio[rr])))  # proc.go:131-132
+            if ns.Len() == 0 and not minimized:  # proc.go:133-137
+                ok = False
+        keep.append(int(ok))
+        finals.append(ns.to_dict() if ok else None)
+    return np.array(keep, np.uint8), finals

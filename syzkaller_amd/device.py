@@ -146,6 +146,23 @@ class Device:
         r["n_failed"] = int(nf.value)
         return r
 
+    # ---------------------------------------------------------------- triageInput re-runs
+    def triage_runs(self, item_off, elems, prios, item_flags, runs, run_off, run_sigs, run_prio, run_errno,
+                    run_exec):
+        """syz-fuzzer/proc.go:107-140 over a batch of triage items (see
+        include/syzsig.h syzsig_triage_runs_dev).  Returns (item_keep, elem_keep)
+        as uint8 device tensors."""
+        self._check_dev(item_off, elems, prios, item_flags, run_off, run_sigs, run_prio, run_errno, run_exec)
+        nitems = item_off.numel() - 1
+        if run_off.numel() != nitems * runs + 1 and nitems > 0:
+            raise ValueError("run_off needs nitems * runs + 1 entries")
+        item_keep = torch.empty(max(nitems, 0), dtype=torch.uint8, device=self.dev)
+        elem_keep = torch.empty(elems.numel(), dtype=torch.uint8, device=self.dev)
+        check(self.L.syzsig_triage_runs_dev(self.eng.h, _p(item_off), max(nitems, 0), _p(elems), _p(prios),
+                                            _p(item_flags), int(runs), _p(run_off), _p(run_sigs), _p(run_prio),
+                                            _p(run_errno), _p(run_exec), _p(item_keep), _p(elem_keep)))
+        return item_keep, elem_keep
+
     # ---------------------------------------------------------------- K5
     def minimize(self, ctx_off, elems, prios, hint_distinct=0):
         self._check_dev(ctx_off, elems, prios)
