@@ -140,6 +140,17 @@ int syzsig_triage_runs_dev(syzsig_ctx* ctx, const uint64_t* d_item_off, uint64_t
                            const int32_t* d_run_errno, const uint8_t* d_run_exec, uint8_t* d_item_keep,
                            uint8_t* d_elem_keep);
 
+/* The minimize predicate of triageInput (proc.go:141-160) over a batch:
+ * same item/run layout as syzsig_triage_runs_dev, with `attempts` runs per
+ * item (minimizeAttempts).  pred[i] = 1 iff, going through the attempts in
+ * order and skipping ones that did not execute or have no signal, an attempt
+ * keeps all of newSignal (newSignal.Intersection(thisSignal).Len() ==
+ * newSignal.Len()) before one fails after a successful original. */
+int syzsig_minimize_pred_dev(syzsig_ctx* ctx, const uint64_t* d_item_off, uint64_t nitems, const uint32_t* d_elems,
+                             const int8_t* d_prios, const uint8_t* d_item_flags, uint32_t attempts,
+                             const uint64_t* d_run_off, const uint32_t* d_run_sigs, const uint8_t* d_run_prio,
+                             const int32_t* d_run_errno, const uint8_t* d_run_exec, uint8_t* d_pred);
+
 /* ---- syz-fuzzer/fuzzer.go:494-511 checkNewSignal (+ signalPrio :513-521 by caller) ----
  * One program's CallInfo signals in host memory: call i's raw signal is
  * sigs[call_start[i] .. +call_len[i]) with prio call_prio[i].  Sequential over

@@ -363,3 +363,26 @@ def triage_runs(item_off, elems, prios, item_flags, runs, run_off, run_sigs, run
         keep.append(int(ok))
         finals.append(ns.to_dict() if ok else None)
     return np.array(keep, np.uint8), finals
+
+
+def minimize_pred(item_off, elems, prios, item_flags, attempts, run_off, run_sigs, run_prio, run_errno, run_exec):
+    """The prog.Minimize predicate of syz-fuzzer/proc.go:141-160, restated per item."""
+    out = []
+    for i in range(len(item_off) - 1):
+        a, b = int(item_off[i]), int(item_off[i + 1])
+        ns = deserialize(elems[a:b], prios[a:b])
+        orig_ok = bool(item_flags[i] & 2)
+        res = 0
+        for r in range(attempts):
+            rr = i * attempts + r
+            ra, rb = int(run_off[rr]), int(run_off[rr + 1])
+            if not run_exec[rr] or rb == ra:  # proc.go:146-148
+                continue
+            if orig_ok and run_errno[rr] != 0:  # proc.go:150-154
+                break
+            this = from_raw(run_sigs[ra:rb], int(run_prio[rr]))
+            if ns.Intersection(this).Len() == ns.Len():  # proc.go:155-159
+                res = 1
+                break
+        out.append(res)
+    return np.array(out, np.uint8)

@@ -83,6 +83,7 @@ SIGNATURES = {
     "syzsig_cover_merge": (c_int, [_P, _PP, _P, c_uint64]),
     "syzsig_cover_merge_dev": (c_int, [_P, _PP, _P, c_uint64]),
     "syzsig_triage_runs_dev": (c_int, [_P, _P, c_uint64, _P, _P, _P, ctypes.c_uint32, _P, _P, _P, _P, _P, _P, _P]),
+    "syzsig_minimize_pred_dev": (c_int, [_P, _P, c_uint64, _P, _P, _P, ctypes.c_uint32, _P, _P, _P, _P, _P, _P]),
     "syzsig_minimize": (c_int, [_P, _P, _P, _P, c_uint64, c_uint64, _P, POINTER(c_uint64)]),
     "syzsig_minimize_dev": (c_int, [_P, _P, _P, _P, c_uint64, c_uint64, _P, POINTER(c_uint64)]),
     "syzsig_check_new_signal": (c_int, [_P, _PP, _PP, _P, c_uint64, _P, _P, _P, c_uint32, _P,

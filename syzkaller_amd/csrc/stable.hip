@@ -93,7 +93,7 @@ __global__ void k_stable_elems(const uint64_t* __restrict__ item_off, uint64_t n
                                const uint64_t* __restrict__ run_off, const uint8_t* __restrict__ run_exec,
                                const int32_t* __restrict__ run_errno, const uint8_t* __restrict__ run_prio,
                                const uint8_t* __restrict__ item_flags, const uint64_t* __restrict__ set, uint64_t C,
-                               uint8_t* __restrict__ alive, unsigned long long* __restrict__ alive_cnt)
+                               uint8_t* __restrict__ alive, unsigned long long* __restrict__ alive_cnt, bool chain)
 {
 	for (uint64_t it = blockIdx.x; it < nitems; it += gridDim.x) {
 		const uint64_t a = item_off[it], b = item_off[it + 1];
@@ -107,7 +107,8 @@ __global__ void k_stable_elems(const uint64_t* __restrict__ item_off, uint64_t n
 					m |= live << r;  // a skipped run changes nothing
 					continue;
 				}
-				live &= (int)(int8_t)run_prio[rr] >= pe && runs_has(set, C, (rr << 32) | e);
+				const uint32_t here = (int)(int8_t)run_prio[rr] >= pe && runs_has(set, C, (rr << 32) | e);
+				live = chain ? live & here : here;  // chained Intersections, or each run on its own
 				m |= live << r;
 				if (live)
 					atomicAdd(&alive_cnt[rr], 1ull);
@@ -156,6 +157,35 @@ __global__ void k_stable_final(const uint64_t* __restrict__ item_off, uint64_t n
 		for (uint64_t i = a + threadIdx.x; i < b; i += blockDim.x)
 			keep_elem[i] = k && (stop < 0 || ((alive[i] >> stop) & 1));
 	}
+}
+
+// The minimize predicate (proc.go:141-160) per item: attempts in order; one
+// that did not execute or has no signal is skipped; a failure after a
+// successful original is a "no"; a run whose Intersection with newSignal keeps
+// all of it is a "yes"; running out of attempts is a "no".
+__global__ void k_pred_items(const uint64_t* __restrict__ item_off, uint64_t nitems, uint32_t R,
+                             const uint64_t* __restrict__ run_off, const uint8_t* __restrict__ run_exec,
+                             const int32_t* __restrict__ run_errno, const uint8_t* __restrict__ item_flags,
+                             const unsigned long long* __restrict__ alive_cnt, uint8_t* __restrict__ pred)
+{
+	const uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (it >= nitems)
+		return;
+	const bool orig_ok = item_flags[it] & SYZSIG_TRIAGE_ORIG_OK;
+	const uint64_t len = item_off[it + 1] - item_off[it];
+	uint8_t res = 0;
+	for (uint32_t r = 0; r < R; r++) {
+		const uint64_t rr = it * R + r;
+		if (!run_exec[rr] || run_off[rr + 1] == run_off[rr])
+			continue;  // proc.go:146-148
+		if (orig_ok && run_errno[rr] != 0)
+			break;  // proc.go:150-154
+		if (alive_cnt[rr] == len) {
+			res = 1;  // proc.go:157-159
+			break;
+		}
+	}
+	pred[it] = res;
 }
 
 static uint64_t pow2_ge(uint64_t v)
@@ -207,7 +237,7 @@ extern "C" int syzsig_triage_runs_dev(syzsig_ctx* ctx, const uint64_t* d_item_of
 		k_runs_insert<<<(int)std::min<uint64_t>(nruns, 8192), 256, 0, s>>>(d_run_off, nruns, d_run_sigs, (uint64_t*)set, C);
 	k_stable_elems<<<(int)std::min<uint64_t>(nitems, 8192), 256, 0, s>>>(
 		d_item_off, nitems, d_elems, d_prios, runs, d_run_off, d_run_exec, d_run_errno, d_run_prio, d_item_flags,
-		(const uint64_t*)set, C, (uint8_t*)alive, (unsigned long long*)cnt);
+		(const uint64_t*)set, C, (uint8_t*)alive, (unsigned long long*)cnt, true);
 	k_stable_items<<<(int)((nitems + 255) / 256), 256, 0, s>>>(
 		d_item_off, nitems, runs, d_run_off, d_run_exec, d_run_errno, d_item_flags,
 		(const unsigned long long*)cnt, d_item_keep, (int8_t*)stop);
@@ -215,6 +245,54 @@ extern "C" int syzsig_triage_runs_dev(syzsig_ctx* ctx, const uint64_t* d_item_of
 		k_stable_final<<<(int)std::min<uint64_t>(nitems, 8192), 256, 0, s>>>(d_item_off, nitems, d_item_keep,
 		                                                           (const int8_t*)stop, (const uint8_t*)alive,
 		                                                           d_elem_keep);
+	SYZ_HIP(hipGetLastError());
+	SYZ_HIP(hipStreamSynchronize(s));
+	return SYZSIG_OK;
+}
+
+extern "C" int syzsig_minimize_pred_dev(syzsig_ctx* ctx, const uint64_t* d_item_off, uint64_t nitems,
+                                        const uint32_t* d_elems, const int8_t* d_prios, const uint8_t* d_item_flags,
+                                        uint32_t attempts, const uint64_t* d_run_off, const uint32_t* d_run_sigs,
+                                        const uint8_t* d_run_prio, const int32_t* d_run_errno,
+                                        const uint8_t* d_run_exec, uint8_t* d_pred)
+{
+	if (!ctx || (nitems && (!d_item_off || !d_item_flags || !d_pred)) ||
+	    (nitems && attempts && (!d_run_off || !d_run_prio || !d_run_errno || !d_run_exec)))
+		return fail(SYZSIG_EINVAL, "minimize_pred: NULL argument");
+	if (attempts > kStableMaxRuns)
+		return fail(SYZSIG_ERANGE, "minimize_pred: at most 8 attempts per item");
+	if (nitems == 0)
+		return SYZSIG_OK;
+	const hipStream_t s = ctx->stream;
+	const uint64_t nruns = nitems * attempts;
+	uint64_t h_off[2] = {0, 0}, h_roff = 0;
+	SYZ_HIP(hipMemcpyAsync(&h_off[1], d_item_off + nitems, 8, hipMemcpyDeviceToHost, s));
+	if (nruns)
+		SYZ_HIP(hipMemcpyAsync(&h_roff, d_run_off + nruns, 8, hipMemcpyDeviceToHost, s));
+	SYZ_HIP(hipStreamSynchronize(s));
+	const uint64_t nelem = h_off[1], nsig = h_roff;
+	if ((nelem && (!d_elems || !d_prios)) || (nsig && !d_run_sigs))
+		return fail(SYZSIG_EINVAL, "minimize_pred: NULL argument");
+	if (nruns >= (1ull << 32))
+		return fail(SYZSIG_ERANGE, "minimize_pred: too many runs");
+	const uint64_t C = pow2_ge(std::max<uint64_t>(2 * nsig + 16, 64));
+	void *set, *alive, *cnt;
+	SYZ_TRY(ws_get(ctx, 0, C * 8, &set));
+	SYZ_TRY(ws_get(ctx, 1, nelem + 64, &alive));
+	SYZ_TRY(ws_get(ctx, 2, nruns * 8 + 64, &cnt));
+	SYZ_HIP(hipMemsetAsync(set, 0xff, C * 8, s));
+	SYZ_HIP(hipMemsetAsync(cnt, 0, nruns * 8 + 8, s));
+	if (nsig)
+		k_runs_insert<<<(int)std::min<uint64_t>(nruns, 8192), 256, 0, s>>>(d_run_off, nruns, d_run_sigs,
+		                                                                    (uint64_t*)set, C);
+	// every attempt is checked on its own: an attempt the predicate skips
+	// (run_ok false for other reasons) is never consulted by k_pred_items
+	k_stable_elems<<<(int)std::min<uint64_t>(nitems, 8192), 256, 0, s>>>(
+		d_item_off, nitems, d_elems, d_prios, attempts, d_run_off, d_run_exec, d_run_errno, d_run_prio,
+		d_item_flags, (const uint64_t*)set, C, (uint8_t*)alive, (unsigned long long*)cnt, false);
+	k_pred_items<<<(int)((nitems + 255) / 256), 256, 0, s>>>(d_item_off, nitems, attempts, d_run_off, d_run_exec,
+	                                                          d_run_errno, d_item_flags,
+	                                                          (const unsigned long long*)cnt, d_pred);
 	SYZ_HIP(hipGetLastError());
 	SYZ_HIP(hipStreamSynchronize(s));
 	return SYZSIG_OK;

@@ -163,6 +163,19 @@ class Device:
                                             _p(run_errno), _p(run_exec), _p(item_keep), _p(elem_keep)))
         return item_keep, elem_keep
 
+    def minimize_pred(self, item_off, elems, prios, item_flags, attempts, run_off, run_sigs, run_prio, run_errno,
+                      run_exec):
+        """triageInput's minimize predicate (proc.go:141-160) per item; uint8 tensor."""
+        self._check_dev(item_off, elems, prios, item_flags, run_off, run_sigs, run_prio, run_errno, run_exec)
+        nitems = item_off.numel() - 1
+        if run_off.numel() != nitems * attempts + 1 and nitems > 0:
+            raise ValueError("run_off needs nitems * attempts + 1 entries")
+        pred = torch.empty(max(nitems, 0), dtype=torch.uint8, device=self.dev)
+        check(self.L.syzsig_minimize_pred_dev(self.eng.h, _p(item_off), max(nitems, 0), _p(elems), _p(prios),
+                                              _p(item_flags), int(attempts), _p(run_off), _p(run_sigs),
+                                              _p(run_prio), _p(run_errno), _p(run_exec), _p(pred)))
+        return pred
+
     # ---------------------------------------------------------------- K5
     def minimize(self, ctx_off, elems, prios, hint_distinct=0):
         self._check_dev(ctx_off, elems, prios)

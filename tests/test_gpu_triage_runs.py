@@ -66,3 +66,15 @@ def test_triage_runs_empty_batch(gpu):
     u8 = torch.empty(0, dtype=torch.uint8, device=gpu.dev)
     ik, ek = gpu.triage_runs(z64, e, u8.view(torch.int8), u8, 3, z64, e, u8, e, u8)
     assert ik.numel() == 0 and ek.numel() == 0
+
+
+@pytest.mark.parametrize("attempts,seed", [(3, 11), (1, 12), (4, 13)])
+def test_minimize_pred_vs_restatement(gpu, attempts, seed):
+    rng = np.random.default_rng(seed)
+    io, el, pr, fl, ro, rs, rp, re, rx = make_items(rng, 400, attempts)
+    pred = gpu.minimize_pred(_t(gpu, io, np.int64), _t(gpu, el, np.int32), _t(gpu, pr, np.int8),
+                             _t(gpu, fl, np.uint8), attempts, _t(gpu, ro, np.int64), _t(gpu, rs, np.int32),
+                             _t(gpu, rp, np.uint8), _t(gpu, re, np.int32), _t(gpu, rx, np.uint8))
+    exp = O.minimize_pred(io, el, pr, fl, attempts, ro, rs, rp, re, rx)
+    np.testing.assert_array_equal(pred.cpu().numpy(), exp)
+    assert 0 < exp.sum() < exp.size
