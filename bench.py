@@ -78,7 +78,7 @@ def pmc_traffic(kernel_prefixes, cfg):
             if any(name == k or name.startswith(k + "<") for k in kernel_prefixes) and "traffic_bytes" in e:
                 tot += e["traffic_bytes"]
                 hit = True
-        t = f  # profiles/rNN_* sort by round
+        t = (d.get("created", 0), f)  # the newest summary (created stamp), then name
         if hit and (best is None or t > best[0]):
             best = (t, tot, os.path.relpath(f, ROOT))
     return (best[1], best[2]) if best else (None, None)

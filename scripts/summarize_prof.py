@@ -60,7 +60,9 @@ def main(src, dst):
         for line in open(log):
             if line.startswith("{"):
                 bench = json.loads(line)
-    summary = {"source": src, "bench_args": os.environ.get("BENCH_ARGS", ""), "kernels": out}
+    import time
+
+    summary = {"source": src, "bench_args": os.environ.get("BENCH_ARGS", ""), "created": time.time(), "kernels": out}
     if bench:
         summary["bench_config"] = bench.get("config")
         with open(os.path.join(dst, "bench.json"), "w") as f:
