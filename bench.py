@@ -118,11 +118,11 @@ def cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, calls_per_prog, target_s):
                       f"oracle/oracle.c single thread, {dt:.2f} s"}
 
 
-def ingest_stage(dev, sigs, cs, cnt, prio, comp, P, C, reps=5):
-    """Frame the batch as executor output regions (executor.h:566-604 records,
-    one region per program) on device, then time readOutCoverage on device
-    (syzsig_ingest_exec_output_dev, pkg/ipc/ipc.go:328-468) over all of them.
-    Not part of `value`; reported as stages.ingest_ms.  Returns (ms, check_ok)."""
+def frame_regions(sigs, cs, cnt, prio, comp, P, C):
+    """The batch as executor output regions (executor.h:566-604 records, one
+    region per program; errno 22 for failed calls), built with torch ops on
+    the batch's device.  Returns (out int32, prog_off int64, call index,
+    published-call mask)."""
     d = sigs.device
     n = P * C
     ar = torch.arange(n, device=d)
@@ -144,7 +144,19 @@ def ingest_stage(dev, sigs, cs, cnt, prio, comp, P, C, reps=5):
     call_of = torch.repeat_interleave(torch.arange(rep.numel(), device=d), rep)
     within = torch.arange(call_of.numel(), device=d) - (rep.cumsum(0) - rep)[call_of]
     out[(roff[done] + 7)[call_of] + within] = sigs[cs[done][call_of] + within]
-    del call_of, within, hdr
+    return out, poff, callidx, done
+
+
+def ingest_stage(dev, sigs, cs, cnt, prio, comp, P, C, reps=5):
+    """Frame the batch as executor output regions on device (frame_regions),
+    then time readOutCoverage on device (syzsig_ingest_exec_output_dev,
+    pkg/ipc/ipc.go:328-468) over all of them.  Not part of `value`; reported
+    as stages.ingest_ms.  Returns (ms, check_ok)."""
+    d = sigs.device
+    out, poff, callidx, done = frame_regions(sigs, cs, cnt, prio, comp, P, C)
+    c64 = cnt.to(torch.int64)
+    z = torch.zeros_like(c64)
+    p64 = prio.to(torch.int64)
     any_ = ((p64 & 1) == 0).to(torch.uint8)
     pc = (torch.arange(P + 1, device=d, dtype=torch.int32) * C)
     ms = []

@@ -171,3 +171,34 @@ def test_ingest_then_triage_vs_oracle(gpu, order_seed):
     np.testing.assert_array_equal(np.sort(_np(pairs[:op.size], np.uint64)), op)
     assert ms.to_dict() == oms.to_dict()
     assert ns.to_dict() == ons.to_dict()
+
+
+def test_bench_frame_regions_parse_back():
+    """bench.py's device-side framer (torch ops, run here on CPU) writes regions
+    that the readOutCoverage restatement parses back to the batch."""
+    import bench
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default(bad_pc_ppm=100)
+    P, C = 12, 6
+    cl = synth.call_lengths(P, C, 0, ragged=(0, 900), seed=4)
+    pcs, cs, prio = synth.traces(cfg, 40, P, C, cl)
+    pc = synth.prog_call_index(P, C)
+    sigs, cnt, comp = O.exec_batch(pcs, cs, cl, pc)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt))  # noqa: E731
+    out, poff, _, done = bench.frame_regions(t(sigs, np.int32), t(cs, np.int64), t(cnt, np.int32),
+                                             t(prio, np.uint8), t(comp, np.int32), P, C)
+    out, poff, done = out.numpy().view(np.uint32), poff.numpy(), done.numpy()
+    assert done.sum() == comp.sum()
+    for p in range(P):
+        st, info = O.read_out_coverage(out[poff[p]:poff[p + 1]], C, list(range(C)))
+        assert st == 0
+        for i in range(C):
+            c = p * C + i
+            if i >= comp[p]:
+                assert info[i] is None
+                continue
+            err, so, sl, _, _ = info[i]
+            assert err == (0 if (prio[c] >> 1) & 1 else 22) and sl == cnt[c]
+            reg = out[poff[p]:poff[p + 1]]
+            np.testing.assert_array_equal(reg[so:so + sl], sigs[cs[c]:cs[c] + cnt[c]])
