@@ -14,8 +14,14 @@
  *    (signal.go:121-125).  Results that Go returns as nil come back as NULL.
  *  - Host arrays passed in are copied during the call and never retained (cgo
  *    pointer rules; CallInfo.Signal aliases executor shmem, pkg/ipc/ipc.go:410).
- *  - Sets are not thread-safe; callers serialize like the reference does
- *    (fuzzer.signalMu, syz-fuzzer/fuzzer.go:55; mgr.mu, syz-manager/manager.go:66).
+ *  - Threading: every entry point locks its context for the duration of the
+ *    call, so concurrent readers -- Diff / DiffRaw / Intersection / Len from
+ *    several goroutines under fuzzer.signalMu.RLock (syz-fuzzer/fuzzer.go:
+ *    488-498) -- are safe and see consistent results.  Writers (Merge, triage)
+ *    still need the caller's write lock for Go-level atomicity of their
+ *    read-modify-write sequences, exactly as in the reference (signalMu.Lock,
+ *    fuzzer.go:500-505; mgr.mu, syz-manager/manager.go:66).  A set must not be
+ *    freed while another thread uses it.
  *  - "_dev" / batch entry points take device pointers and run on the context's
  *    stream (syzsig_ctx_set_stream); they return after the work completes.
  */
@@ -47,7 +53,8 @@ const char* syzsig_last_error(void);
 /* ---- context: one per process and GPU ---- */
 int syzsig_ctx_create(int device, syzsig_ctx** out);
 void syzsig_ctx_destroy(syzsig_ctx* ctx);
-/* Run subsequent work on `stream` (a hipStream_t; NULL = the context's own). */
+/* Run subsequent work on `stream` (a hipStream_t; NULL = the context's own,
+ * which is a blocking stream: ordered against the null stream both ways). */
 int syzsig_ctx_set_stream(syzsig_ctx* ctx, void* stream);
 void* syzsig_ctx_stream(syzsig_ctx* ctx);
 /* Record HIP events around the triage kernels (batch stats probe_ms/decide_ms). */

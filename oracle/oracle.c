@@ -5,6 +5,7 @@
  */
 #include "oracle.h"
 
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -435,4 +436,105 @@ void orc_triage_batch(orc_sig** max_signal, orc_sig** new_signal, const uint32_t
 		orc_merge(new_signal, diff);
 		orc_sig_free(diff);
 	}
+}
+
+/* ---- multi-core CPU baseline: fuzzer.go:494-511 as `procs` goroutines run it ----
+ * nthreads workers (the fuzzer's Procs, fuzzer.go:288-295) take programs in
+ * order; per call: DiffRaw under signalMu.RLock, and when non-empty the
+ * RUnlock/Lock upgrade, maxSignal.Merge + newSignal.Merge, Unlock/RLock
+ * (fuzzer.go:494-511).  Like the reference, the interleaving of the procs
+ * makes which call reports a shared new element nondeterministic; the final
+ * maxSignal is deterministic (max is order-independent).  Timing baseline only. */
+typedef struct {
+	orc_sig** ms;
+	orc_sig** ns;
+	const uint32_t* sigs;
+	const uint64_t* call_start;
+	const uint32_t* call_len;
+	const uint8_t* call_prio;
+	uint64_t nprog, calls_per_prog;
+	uint64_t next; /* next program (atomic) */
+	uint64_t ncalls_new;
+	pthread_rwlock_t mu; /* fuzzer.signalMu */
+} orc_mt;
+
+static void* orc_mt_proc(void* arg)
+{
+	orc_mt* m = (orc_mt*)arg;
+	uint64_t nnew = 0;
+	for (;;) {
+		uint64_t p = __atomic_fetch_add(&m->next, 1, __ATOMIC_RELAXED);
+		if (p >= m->nprog)
+			break;
+		pthread_rwlock_rdlock(&m->mu);
+		for (uint64_t k = p * m->calls_per_prog; k < (p + 1) * m->calls_per_prog; k++) {
+			orc_sig* diff = orc_diff_raw(*m->ms, m->sigs + m->call_start[k], m->call_len[k], m->call_prio[k]);
+			if (orc_sig_len(diff) == 0) {
+				orc_sig_free(diff);
+				continue;
+			}
+			nnew++;
+			pthread_rwlock_unlock(&m->mu);
+			pthread_rwlock_wrlock(&m->mu);
+			orc_merge(m->ms, diff);
+			orc_merge(m->ns, diff);
+			pthread_rwlock_unlock(&m->mu);
+			pthread_rwlock_rdlock(&m->mu);
+			orc_sig_free(diff);
+		}
+		pthread_rwlock_unlock(&m->mu);
+	}
+	__atomic_fetch_add(&m->ncalls_new, nnew, __ATOMIC_RELAXED);
+	return NULL;
+}
+
+uint64_t orc_triage_batch_mt(orc_sig** max_signal, orc_sig** new_signal, const uint32_t* sigs,
+                             const uint64_t* call_start, const uint32_t* call_len, const uint8_t* call_prio,
+                             uint64_t nprog, uint64_t calls_per_prog, uint32_t nthreads)
+{
+	orc_mt m;
+	memset(&m, 0, sizeof(m));
+	m.ms = max_signal;
+	m.ns = new_signal;
+	m.sigs = sigs;
+	m.call_start = call_start;
+	m.call_len = call_len;
+	m.call_prio = call_prio;
+	m.nprog = nprog;
+	m.calls_per_prog = calls_per_prog;
+	pthread_rwlock_init(&m.mu, NULL);
+	if (!*max_signal) /* the zero-value maxSignal is usable: Merge allocates (signal.go:121-125) */
+		*max_signal = orc_sig_new(0);
+	if (nthreads < 1)
+		nthreads = 1;
+	pthread_t* th = (pthread_t*)calloc(nthreads, sizeof(pthread_t));
+	for (uint32_t i = 0; i < nthreads; i++)
+		pthread_create(&th[i], NULL, orc_mt_proc, &m);
+	for (uint32_t i = 0; i < nthreads; i++)
+		pthread_join(th[i], NULL);
+	free(th);
+	pthread_rwlock_destroy(&m.mu);
+	return m.ncalls_new;
+}
+
+/* Test helper (not a reference function): the entries of a Serial whose
+ * element is in keys[], in input order -- Deserialize of the result agrees
+ * with Deserialize of the whole Serial on every key (later duplicates still
+ * overwrite earlier ones, signal.go:66-69).  Returns the count written. */
+uint64_t orc_filter_keys(const uint32_t* elems, const int8_t* prios, uint64_t n, const uint32_t* keys,
+                         uint64_t nkeys, uint32_t* out_e, int8_t* out_p)
+{
+	orc_sig* set = orc_from_raw(keys, nkeys, 0);
+	uint64_t k = 0;
+	if (set) {
+		for (uint64_t i = 0; i < n; i++) {
+			if (orc_sig_get(set, elems[i], NULL)) {
+				out_e[k] = elems[i];
+				out_p[k] = prios[i];
+				k++;
+			}
+		}
+	}
+	orc_sig_free(set);
+	return k;
 }

@@ -14,7 +14,7 @@
  *   - pkg/signal + checkNewSignal half: the Go reference cannot be built here
  *     (no Go toolchain in the image), and the reference holds no tests or
  *     fixtures for pkg/signal.  Pinned only by hand-derived known-answer tests
- *     (tests/test_oracle_kat.py) => "parity partially pinned" (see DESIGN.md).
+ *     (tests/kat_cases.py) => "parity partially pinned" (see DESIGN.md).
  */
 #ifndef SYZSIG_ORACLE_H
 #define SYZSIG_ORACLE_H
@@ -79,6 +79,20 @@ uint64_t orc_minimize(const uint64_t* ctx_off, const uint32_t* elems, const int8
 void orc_triage_batch(orc_sig** max_signal, orc_sig** new_signal, const uint32_t* sigs,
                       const uint64_t* call_start, const uint32_t* call_len, const uint8_t* call_prio,
                       uint64_t ncalls, uint32_t* new_bits, uint8_t* call_new);
+
+/*
+ * The multi-core CPU baseline: fuzzer.go:494-511 as `nthreads` Procs run it
+ * (fuzzer.go:288-295), program p = calls [p*calls_per_prog, (p+1)*calls_per_prog),
+ * DiffRaw under a reader lock, Merge under the writer lock (pthread rwlock =
+ * signalMu).  Returns the number of calls that reported new signal.
+ */
+uint64_t orc_triage_batch_mt(orc_sig** max_signal, orc_sig** new_signal, const uint32_t* sigs,
+                             const uint64_t* call_start, const uint32_t* call_len, const uint8_t* call_prio,
+                             uint64_t nprog, uint64_t calls_per_prog, uint32_t nthreads);
+
+/* Test helper: the Serial entries whose element is in keys[] (input order kept). */
+uint64_t orc_filter_keys(const uint32_t* elems, const int8_t* prios, uint64_t n, const uint32_t* keys,
+                         uint64_t nkeys, uint32_t* out_e, int8_t* out_p);
 
 #ifdef __cplusplus
 }

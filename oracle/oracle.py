@@ -46,6 +46,9 @@ def lib():
             "orc_merge": (None, [POINTER(c_void_p), P]),
             "orc_minimize": (c_uint64, [P, P, P, c_uint64, P]),
             "orc_triage_batch": (None, [POINTER(c_void_p), POINTER(c_void_p), P, P, P, P, c_uint64, P, P]),
+            "orc_triage_batch_mt": (c_uint64, [POINTER(c_void_p), POINTER(c_void_p), P, P, P, P, c_uint64, c_uint64,
+                                               c_uint32]),
+            "orc_filter_keys": (c_uint64, [P, P, c_uint64, P, c_uint64, P, P]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -237,6 +240,51 @@ def triage_batch_into(ms, sigs, call_start, call_len, call_prio, ns=None):
                            _p(cnew))
     ms.h, ns.h = mh.value, nh.value
     return ns, bits, cnew
+
+
+def triage_batch_mt(ms, sigs, call_start, call_len, call_prio, calls_per_prog, nthreads, ns=None):
+    """orc_triage_batch_mt: checkNewSignal as `nthreads` Procs run it under
+    signalMu (fuzzer.go:494-511) -- the multi-core CPU baseline.  Returns
+    (newSignal, number of calls with new signal)."""
+    ns = ns if ns is not None else OSig()
+    sigs = np.ascontiguousarray(sigs, np.uint32)
+    cs = np.ascontiguousarray(call_start, np.uint64)
+    cl = np.ascontiguousarray(call_len, np.uint32)
+    cp = np.ascontiguousarray(call_prio, np.uint8)
+    mh, nh = c_void_p(ms.h or 0), c_void_p(ns.h or 0)
+    n = lib().orc_triage_batch_mt(ctypes.byref(mh), ctypes.byref(nh), _p(sigs), _p(cs), _p(cl), _p(cp),
+                                  cl.size // calls_per_prog, calls_per_prog, int(nthreads))
+    ms.h, ns.h = mh.value, nh.value
+    return ns, int(n)
+
+
+def filter_keys(elems, prios, keys):
+    """The Serial entries (elems, prios) whose element is in keys, input order kept."""
+    e = np.ascontiguousarray(elems, np.uint32)
+    p = np.ascontiguousarray(prios, np.int8)
+    k = np.ascontiguousarray(keys, np.uint32)
+    oe = np.empty(max(e.size, 1), np.uint32)
+    op = np.empty(max(e.size, 1), np.int8)
+    n = lib().orc_filter_keys(_p(e), _p(p), e.size, _p(k), k.size, _p(oe), _p(op))
+    return oe[:n].copy(), op[:n].copy()
+
+
+def poll(max_signal, new_max, fuzzer, serial):
+    """syz-manager/manager.go:1027-1052 Manager.Poll restated over oracle sets:
+    new_max = list of every fuzzer's newMaxSignal (OSig), `fuzzer` the caller's
+    index, serial its a.MaxSignal.  Returns the reply's MaxSignal (elems, prios)
+    and updates max_signal / new_max in place."""
+    nm = max_signal.Diff(deserialize(*serial))
+    if nm.Len():
+        max_signal.Merge(nm)
+        for i, f1 in enumerate(new_max):
+            if i != fuzzer:
+                f1.Merge(nm)
+    reply = (np.empty(0, np.uint32), np.empty(0, np.int8))
+    if new_max[fuzzer].Len():
+        reply = new_max[fuzzer].Serialize()
+        new_max[fuzzer] = OSig()
+    return reply
 
 
 # ---- pkg/ipc/ipc.go:328-468 readOutCoverage (restated; test infrastructure only) ----

@@ -1312,6 +1312,7 @@ int syzsig_shard_agg_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint6
                                    const int8_t* levels, uint32_t nlevels, uint32_t nshards, uint64_t* d_send,
                                    uint64_t send_cap, uint64_t* send_counts, syzsig_batch_stats* stats)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !b || !send_counts || (b->nrec && !b->sigs) || (send_cap && !d_send) ||
 	    (b->ncalls && (!b->call_start || !b->call_len || !b->call_prio)))
 		return fail(SYZSIG_EINVAL, "shard_agg_partition: NULL argument");
@@ -1375,6 +1376,7 @@ int syzsig_shard_agg_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uin
                                      const uint64_t* d_send, uint64_t n_send, const uint8_t* d_back_flags,
                                      syzsig_batch_stats* stats)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !b || (n_send && (!d_send || !d_back_flags)) || (b->ncalls && !b->call_new) ||
 	    (b->new_pairs_cap && !b->new_pairs))
 		return fail(SYZSIG_EINVAL, "shard_agg_unpartition: NULL argument");

@@ -261,6 +261,7 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
                                       const uint32_t* d_prog_call, uint64_t nprog, uint32_t* d_sigs,
                                       uint32_t* d_sig_cnt, uint32_t* d_completed)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || (nprog && (!d_prog_call || !d_completed)) || (ncalls && (!d_call_start || !d_call_len || !d_sig_cnt)) ||
 	    (npc && (!d_pcs || !d_sigs)))
 		return fail(SYZSIG_EINVAL, "edge_derive: NULL argument");

@@ -170,6 +170,7 @@ extern "C" int syzsig_ingest_exec_output_dev(syzsig_ctx* ctx, const uint32_t* d_
                                              int32_t* d_call_errno, uint64_t* d_cover_start, uint32_t* d_cover_len,
                                              int32_t* d_prog_status, uint64_t* n_failed)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || (nwords && !d_out) || (nprog && (!d_prog_off || !d_prog_call || !d_prog_status)) ||
 	    (ncalls && (!d_call_any || !d_call_start || !d_call_len || !d_call_prio || !d_call_errno)) ||
 	    (!d_cover_start != !d_cover_len))

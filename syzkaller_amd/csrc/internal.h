@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../../include/syzsig.h"
@@ -25,6 +26,10 @@ int hip_fail(hipError_t e, const char* what, const char* file, int line);
 		if (e__ != hipSuccess)                                                     \
 			return syz::hip_fail(e__, #expr, __FILE__, __LINE__);                  \
 	} while (0)
+
+// Serialize this C-ABI call against every other call on the same context
+// (NULL-safe: the entry point's own argument check then reports the error).
+#define SYZ_LOCK(ctx) syz::CtxLock syz_lock__(ctx)
 
 #define SYZ_TRY(expr)                                                              \
 	do {                                                                           \
@@ -62,6 +67,12 @@ constexpr size_t kPinMask = 0, kPinPairs = 64, kPinCounts = 1024, kPinBytes = 64
 }  // namespace syz
 
 struct syzsig_ctx {
+	// Every C-ABI entry point holds this for its whole duration (SYZ_LOCK): the
+	// context's stream, scratch slots, counters and pinned staging are shared by
+	// all callers, and the reference runs Diff/DiffRaw concurrently under
+	// signalMu.RLock (syz-fuzzer/fuzzer.go:488-498).  Recursive: entry points
+	// call each other (e.g. triage allocates newSignal through syzsig_set_make).
+	std::recursive_mutex mu;
 	int device = 0;
 	hipStream_t own_stream = nullptr;
 	hipStream_t stream = nullptr;
@@ -96,6 +107,22 @@ struct syzsig_set {
 };
 
 namespace syz {
+
+struct CtxLock {
+	syzsig_ctx* c;
+	explicit CtxLock(syzsig_ctx* x) : c(x)
+	{
+		if (c)
+			c->mu.lock();
+	}
+	~CtxLock()
+	{
+		if (c)
+			c->mu.unlock();
+	}
+	CtxLock(const CtxLock&) = delete;
+	CtxLock& operator=(const CtxLock&) = delete;
+};
 
 // scratch buffer `i` of the context, grown to at least `bytes` (contents lost on growth)
 int ws_get(syzsig_ctx* ctx, int i, size_t bytes, void** out);

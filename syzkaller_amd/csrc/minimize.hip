@@ -87,6 +87,7 @@ extern "C" {
 int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
                         uint64_t nctx, uint64_t hint_distinct, uint8_t* d_keep, uint64_t* n_out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !n_out || (nctx && (!d_off || !d_keep)))
 		return fail(SYZSIG_EINVAL, "minimize: NULL argument");
 	*n_out = 0;
@@ -150,6 +151,7 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* 
 int syzsig_minimize(syzsig_ctx* ctx, const uint64_t* ctx_off, const uint32_t* elems, const int8_t* prios,
                     uint64_t nctx, uint64_t hint_distinct, uint64_t* out_idx, uint64_t* n_out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !n_out || (nctx && (!ctx_off || !out_idx)))
 		return fail(SYZSIG_EINVAL, "minimize: NULL argument");
 	*n_out = 0;

@@ -99,7 +99,12 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 	SYZ_HIP(hipSetDevice(device));
 	syzsig_ctx* c = new syzsig_ctx();
 	c->device = device;
-	hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+	// A BLOCKING stream: it is ordered after work already queued on the null
+	// stream and the null stream after it (legacy default-stream semantics).
+	// torch's default stream is the null stream, so tensors produced there --
+	// and RCCL results a synchronous collective made it wait for -- are ready
+	// when a library kernel on this stream reads them, without a host sync.
+	hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault);
 	if (e == hipSuccess)
 		e = hipMalloc(&c->d_cnt, sizeof(unsigned long long) * syz::kNumCounters);
 	if (e == hipSuccess)
@@ -148,16 +153,22 @@ void syzsig_ctx_destroy(syzsig_ctx* c)
 
 int syzsig_ctx_set_stream(syzsig_ctx* ctx, void* stream)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_stream: ctx is NULL");
 	ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
 	return SYZSIG_OK;
 }
 
-void* syzsig_ctx_stream(syzsig_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+void* syzsig_ctx_stream(syzsig_ctx* ctx)
+{
+	SYZ_LOCK(ctx);
+	return ctx ? (void*)ctx->stream : nullptr;
+}
 
 int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_agg: ctx is NULL");
 	if (mode < 0 || mode > 2 || (parts && (parts < 8 || parts > 2048 || (parts & (parts - 1)))))
@@ -169,6 +180,7 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts)
 
 int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_timing: ctx is NULL");
 	if (enable && !ctx->ev[0])

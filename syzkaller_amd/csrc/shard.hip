@@ -130,6 +130,7 @@ int syzsig_shard_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t 
                                uint32_t nlevels, uint32_t nshards, uint64_t* d_send, uint32_t* d_send_pos,
                                uint64_t* send_counts)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !b || !send_counts || (b->nrec && (!d_send || !d_send_pos || !b->sigs)) ||
 	    (b->ncalls && (!b->call_start || !b->call_len || !b->call_prio)))
 		return fail(SYZSIG_EINVAL, "shard_partition: NULL argument");
@@ -177,6 +178,7 @@ int syzsig_shard_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t 
 int syzsig_shard_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* d_send_pos,
                                  const uint8_t* d_back_flags)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !b || (b->nrec && (!d_send_pos || !d_back_flags || !b->new_bits)) || (b->ncalls && !b->call_new))
 		return fail(SYZSIG_EINVAL, "shard_unpartition: NULL argument");
 	SYZ_HIP(hipMemsetAsync(b->new_bits, 0, ((b->nrec + 31) / 32) * 4, ctx->stream));

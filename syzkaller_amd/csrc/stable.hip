@@ -206,6 +206,7 @@ extern "C" int syzsig_triage_runs_dev(syzsig_ctx* ctx, const uint64_t* d_item_of
                                       const uint8_t* d_run_prio, const int32_t* d_run_errno,
                                       const uint8_t* d_run_exec, uint8_t* d_item_keep, uint8_t* d_elem_keep)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || (nitems && (!d_item_off || !d_item_flags || !d_item_keep)) ||
 	    (nitems && runs && (!d_run_off || !d_run_prio || !d_run_errno || !d_run_exec)))
 		return fail(SYZSIG_EINVAL, "triage_runs: NULL argument");
@@ -256,6 +257,7 @@ extern "C" int syzsig_minimize_pred_dev(syzsig_ctx* ctx, const uint64_t* d_item_
                                         const uint8_t* d_run_prio, const int32_t* d_run_errno,
                                         const uint8_t* d_run_exec, uint8_t* d_pred)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || (nitems && (!d_item_off || !d_item_flags || !d_pred)) ||
 	    (nitems && attempts && (!d_run_off || !d_run_prio || !d_run_errno || !d_run_exec)))
 		return fail(SYZSIG_EINVAL, "minimize_pred: NULL argument");

@@ -84,6 +84,7 @@ int syzsig_synth_traces_dev(syzsig_ctx* ctx, const syzsig_synth_cfg* cfg, uint64
                             uint32_t cpp, const uint64_t* d_call_start, const uint32_t* d_call_len, uint64_t* d_pcs,
                             uint8_t* d_call_prio)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !cfg_ok(cfg) || cpp == 0)
 		return fail(SYZSIG_EINVAL, "synth_traces: bad argument");
 	const uint64_t ncalls = nprog * cpp;
@@ -110,6 +111,7 @@ int syzsig_synth_m0_host(const syzsig_synth_cfg* cfg, uint64_t known_sys, uint64
 int syzsig_synth_m0_dev(syzsig_ctx* ctx, const syzsig_synth_cfg* cfg, uint64_t known_sys, uint64_t n,
                         uint32_t* d_elems, int8_t* d_prios)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !cfg_ok(cfg))
 		return fail(SYZSIG_EINVAL, "synth_m0: bad argument");
 	if (!n)

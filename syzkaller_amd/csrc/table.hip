@@ -396,6 +396,7 @@ extern "C" {
 
 int syzsig_set_make(syzsig_ctx* ctx, uint64_t hint, syzsig_set** out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !out)
 		return fail(SYZSIG_EINVAL, "set_make: NULL argument");
 	return set_alloc(ctx, buckets_for(hint), out);
@@ -403,6 +404,7 @@ int syzsig_set_make(syzsig_ctx* ctx, uint64_t hint, syzsig_set** out)
 
 void syzsig_set_free(syzsig_set* s)
 {
+	SYZ_LOCK(s ? s->ctx : nullptr);
 	if (!s)
 		return;
 	set_release_storage(s);
@@ -411,6 +413,7 @@ void syzsig_set_free(syzsig_set* s)
 
 int syzsig_set_clone(syzsig_ctx* ctx, const syzsig_set* s, syzsig_set** out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !out)
 		return fail(SYZSIG_EINVAL, "set_clone: NULL argument");
 	*out = nullptr;
@@ -427,6 +430,7 @@ int syzsig_set_clone(syzsig_ctx* ctx, const syzsig_set* s, syzsig_set** out)
 
 int syzsig_set_clear(syzsig_ctx* ctx, syzsig_set* s)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !s)
 		return fail(SYZSIG_EINVAL, "set_clear: NULL argument");
 	SYZ_HIP(hipMemsetAsync(s->slots, 0, s->nslots() * sizeof(uint64_t), ctx->stream));
@@ -436,6 +440,7 @@ int syzsig_set_clear(syzsig_ctx* ctx, syzsig_set* s)
 
 int syzsig_set_copy_from(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !dst || !src)
 		return fail(SYZSIG_EINVAL, "set_copy_from: NULL argument");
 	if (dst->nbuckets != src->nbuckets)
@@ -446,14 +451,23 @@ int syzsig_set_copy_from(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src
 	return SYZSIG_OK;
 }
 
-uint64_t syzsig_len(const syzsig_set* s) { return s ? s->len : 0; }
+uint64_t syzsig_len(const syzsig_set* s)
+{
+	SYZ_LOCK(s ? s->ctx : nullptr);
+	return s ? s->len : 0;
+}
 
 int syzsig_empty(const syzsig_set* s) { return syzsig_len(s) == 0; }
 
-uint64_t syzsig_capacity(const syzsig_set* s) { return s ? s->nslots() : 0; }
+uint64_t syzsig_capacity(const syzsig_set* s)
+{
+	SYZ_LOCK(s ? s->ctx : nullptr);
+	return s ? s->nslots() : 0;
+}
 
 int syzsig_from_raw(syzsig_ctx* ctx, const uint32_t* raw, uint64_t n, uint8_t prio, syzsig_set** out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !out || (n && !raw))
 		return fail(SYZSIG_EINVAL, "from_raw: NULL argument");
 	*out = nullptr;
@@ -470,6 +484,7 @@ int syzsig_from_raw(syzsig_ctx* ctx, const uint32_t* raw, uint64_t n, uint8_t pr
 int syzsig_serialize(syzsig_ctx* ctx, const syzsig_set* s, uint32_t* elems, int8_t* prios, uint64_t cap,
                      uint64_t* n_out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !n_out || (cap && (!elems || !prios)))
 		return fail(SYZSIG_EINVAL, "serialize: NULL argument");
 	*n_out = 0;
@@ -501,6 +516,7 @@ int syzsig_serialize(syzsig_ctx* ctx, const syzsig_set* s, uint32_t* elems, int8
 int syzsig_deserialize_dev(syzsig_ctx* ctx, const uint32_t* d_elems, const int8_t* d_prios, uint64_t n,
                            syzsig_set** out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !out || (n && (!d_elems || !d_prios)))
 		return fail(SYZSIG_EINVAL, "deserialize: NULL argument");
 	*out = nullptr;
@@ -517,6 +533,7 @@ int syzsig_deserialize_dev(syzsig_ctx* ctx, const uint32_t* d_elems, const int8_
 int syzsig_deserialize(syzsig_ctx* ctx, const uint32_t* elems, uint64_t n_elems, const int8_t* prios,
                        uint64_t n_prios, syzsig_set** out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !out)
 		return fail(SYZSIG_EINVAL, "deserialize: NULL argument");
 	*out = nullptr;
@@ -534,6 +551,7 @@ int syzsig_deserialize(syzsig_ctx* ctx, const uint32_t* elems, uint64_t n_elems,
 
 int syzsig_diff(syzsig_ctx* ctx, const syzsig_set* s, const syzsig_set* s1, syzsig_set** out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !out)
 		return fail(SYZSIG_EINVAL, "diff: NULL argument");
 	*out = nullptr;
@@ -550,6 +568,7 @@ int syzsig_diff(syzsig_ctx* ctx, const syzsig_set* s, const syzsig_set* s1, syzs
 int syzsig_diff_raw(syzsig_ctx* ctx, const syzsig_set* s, const uint32_t* raw, uint64_t n, uint8_t prio,
                     syzsig_set** out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !out || (n && !raw))
 		return fail(SYZSIG_EINVAL, "diff_raw: NULL argument");
 	*out = nullptr;
@@ -567,6 +586,7 @@ int syzsig_diff_raw(syzsig_ctx* ctx, const syzsig_set* s, const uint32_t* raw, u
 
 int syzsig_intersection(syzsig_ctx* ctx, const syzsig_set* s, const syzsig_set* s1, syzsig_set** out)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !out)
 		return fail(SYZSIG_EINVAL, "intersection: NULL argument");
 	*out = nullptr;
@@ -603,6 +623,7 @@ static int cover_merge_dev(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* d_
 
 int syzsig_cover_merge(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* raw, uint64_t n)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !cov || (n && !raw))
 		return fail(SYZSIG_EINVAL, "cover_merge: NULL argument");
 	void* d = nullptr;
@@ -612,6 +633,7 @@ int syzsig_cover_merge(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* raw, u
 
 int syzsig_cover_merge_dev(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* d_raw, uint64_t n)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !cov || (n && !d_raw))
 		return fail(SYZSIG_EINVAL, "cover_merge_dev: NULL argument");
 	return cover_merge_dev(ctx, cov, d_raw, n);
@@ -619,6 +641,7 @@ int syzsig_cover_merge_dev(syzsig_ctx* ctx, syzsig_set** cov, const uint32_t* d_
 
 int syzsig_merge(syzsig_ctx* ctx, syzsig_set** sp, const syzsig_set* s1)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !sp)
 		return fail(SYZSIG_EINVAL, "merge: NULL argument");
 	if (syzsig_empty(s1))

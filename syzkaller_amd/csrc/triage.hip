@@ -549,9 +549,14 @@ static int triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, Prep pre
 			SYZ_HIP(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
 			st->probe_ms += ms;
 		}
-		if (ctx->h_cnt[kCntError])
+		if (ctx->h_cnt[kCntError]) {
+			// The valid records of this launch already left absent markers and run
+			// hints in maxSignal; a same-size rehash that drops absent slots and
+			// masks hints restores exactly M0 before the error is reported.
+			SYZ_TRY(set_rehash(ms, ms->nbuckets, true));
 			return fail(SYZSIG_EINVAL, "triage: a call range lies outside [0, nrec), a call has >= 2^24 "
 			                           "records, or a record's prio level is out of range");
+		}
 		if (ctx->h_cnt[kCntOverflow]) {
 			SYZ_TRY(set_rehash(ms, ms->nbuckets * 8, true));
 			st->retries++;
@@ -722,6 +727,7 @@ extern "C" {
 int syzsig_triage_batch(syzsig_ctx* ctx, syzsig_set* max_signal, syzsig_set** new_signal, const syzsig_batch* b,
                         syzsig_batch_stats* stats)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !max_signal || !new_signal || !b)
 		return fail(SYZSIG_EINVAL, "triage_batch: NULL argument");
 	if (*new_signal == max_signal)
@@ -745,6 +751,7 @@ int syzsig_check_new_signal(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set
                             const uint8_t* call_prio, uint32_t ncalls, uint32_t* out_calls, uint32_t* n_out,
                             uint32_t* new_bits)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !max_signal || !new_signal || !n_out || (ncalls && (!call_start || !call_len || !call_prio)) ||
 	    (nrec && !sigs) || (ncalls && !out_calls))
 		return fail(SYZSIG_EINVAL, "check_new_signal: NULL argument");
@@ -801,6 +808,7 @@ int syzsig_triage_records_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set** n
                               uint64_t nrec, const int8_t* levels, uint32_t nlevels, uint8_t* d_new_flags,
                               syzsig_batch_stats* stats)
 {
+	SYZ_LOCK(ctx);
 	if (!ctx || !shard || !new_signal || (nrec && (!d_recs || !d_new_flags)))
 		return fail(SYZSIG_EINVAL, "triage_records: NULL argument");
 	if (*new_signal == shard)

@@ -37,7 +37,11 @@ class Device:
         self.sync_stream()
 
     def sync_stream(self):
-        """Run library work on torch's current stream of this device."""
+        """Run library work on torch's current stream of this device.  torch's
+        default stream is HIP's null stream (handle 0); the library's own
+        stream (selected by 0) is a blocking stream, ordered against the null
+        stream both ways, so inputs torch (or a synchronous RCCL collective)
+        produced there are complete when a library kernel reads them."""
         self.eng.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
 
     @property

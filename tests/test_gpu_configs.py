@@ -1,0 +1,251 @@
+"""GPU: BASELINE.json's configs at their full sizes, checked against the oracle.
+
+  C2  the whole 4096 x 64 x 4096 batch vs a 10M-element maxSignal on the
+      aggregation path the bench runs (2048 partitions), against sequential
+      checkNewSignal (oracle/oracle.c orc_triage_batch) over the same records.
+  C3  signal.Minimize over a 200k-context corpus (geometric lengths, mean 2k,
+      ~400M entries), against orc_minimize; plus a distinct-length corpus where
+      the reference's unstable sort.Slice order cannot matter.
+  C4  a 1B-element maxSignal: hash-sharded into 8 shard tables on one GPU, one
+      C2 batch split into 8 source program ranges routed through the staircase
+      exchange (shard_agg_partition -> owners' records-mode triage ->
+      shard_agg_unpartition), against the same batch on the unsharded 1B table;
+      plus the oracle on a program prefix (M0 restricted to the prefix's keys).
+  C5  streaming, skewed: two consecutive batches of 4096 programs x 64 x 1k
+      (skew=1, hot syscalls) triaged against the state the previous batch left,
+      against the oracle over both batches in order.
+
+References: syz-fuzzer/fuzzer.go:494-511 (checkNewSignal), pkg/signal/signal.go
+:73-166 (Diff/DiffRaw/Merge/Minimize).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _u(t, dt):
+    return t.cpu().numpy().view(dt)
+
+
+def _sorted_ser(elems, prios):
+    o = np.argsort(elems, kind="stable")
+    return elems[o], prios[o]
+
+
+def assert_same_set(dev_set, osig):
+    """Device Signal == oracle Signal, compared as sorted (elem, prio) arrays."""
+    ge, gp = _sorted_ser(*(lambda s: (s.Elems, s.Prios))(dev_set.Serialize()))
+    oe, op = _sorted_ser(*osig.Serialize())
+    np.testing.assert_array_equal(ge, oe)
+    np.testing.assert_array_equal(gp, op)
+
+
+def pairs_from_bits(sigs, cs, cnt, bits):
+    """Every call's DiffRaw result as sorted unique (call << 32 | elem) from
+    per-record new bits (sparse record layout)."""
+    r = np.nonzero(np.unpackbits(bits.view(np.uint8), bitorder="little"))[0].astype(np.uint64)
+    ends = cs.astype(np.uint64) + cnt.astype(np.uint64)
+    call = np.searchsorted(ends, r, side="right").astype(np.uint64)
+    return np.unique((call << np.uint64(32)) | sigs[r].astype(np.uint64))
+
+
+def device_batch(gpu, cfg, prog_base, nprog, cpp, pcs_per_call):
+    """synthetic traces -> K1+K2 on device; returns (sigs, call_start, sig_cnt, prio)."""
+    from syzkaller_amd import synth
+
+    cl = torch.full((nprog * cpp,), pcs_per_call, dtype=torch.int32)
+    pcs, cs, cl, prio = gpu.synth_traces(cfg, prog_base, nprog, cpp, cl)
+    pidx = torch.from_numpy(synth.prog_call_index(nprog, cpp).view(np.int32)).to(gpu.dev)
+    sigs, cnt, comp = gpu.edge_derive(pcs, cs, cl, pidx)
+    del pcs
+    return sigs, cs, cnt, prio
+
+
+def test_c2_full_batch_vs_oracle(gpu):
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default()
+    P, C, L = 4096, 64, 4096
+    sigs, cs, cnt, prio = device_batch(gpu, cfg, 0, P, C, L)
+    m0e, m0p = gpu.synth_m0(cfg, 2048, 10_000_000)
+    ms = gpu.deserialize(m0e, m0p)
+    ns = S.Signal(None, gpu.eng)
+    nrec = int(cnt.to(torch.int64).sum())
+    pairs = torch.full((16 << 20,), -1, dtype=torch.int64, device=gpu.dev)
+    _, cnew, st = gpu.triage(ms, ns, sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
+    torch.cuda.synchronize()
+    # the geometry the bench reports: one run on the aggregation path, 2048 partitions, no overflow
+    assert st["records"] == nrec and st["runs"] == 1
+    assert st["parts"] == 2048 and st["overflow_parts"] == 0
+    hs, hcs, hcnt, hprio = _u(sigs, np.uint32), _u(cs, np.uint64), _u(cnt, np.uint32), _u(prio, np.uint8)
+    oms, ons, obits, ocnew = O.triage_batch(_u(m0e, np.uint32), _u(m0p, np.int8), hs, hcs, hcnt, hprio)
+    np.testing.assert_array_equal(_u(cnew, np.uint8), ocnew)
+    op = pairs_from_bits(hs, hcs, hcnt, obits)
+    assert st["new_pairs"] == op.size <= pairs.numel()
+    np.testing.assert_array_equal(np.sort(_u(pairs[: op.size], np.uint64)), op)
+    assert ms.Len() == oms.Len() and ns.Len() == ons.Len()
+    assert_same_set(ms, oms)
+    assert_same_set(ns, ons)
+
+
+def _corpus_dev(dev, n, lens, U, seed):
+    """Minimize corpus on device: context c has lens[c] distinct elements
+    (base_c + k * stride_c) mod U (stride odd, U a power of two) and prio
+    uniform 0..3 per entry."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    lens_t = torch.as_tensor(lens, dtype=torch.int64, device=dev)
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    off[1:] = torch.cumsum(lens_t, 0)
+    N = int(off[-1])
+    base = torch.randint(0, U, (n,), generator=g, device=dev, dtype=torch.int64)
+    stride = torch.randint(0, U // 2, (n,), generator=g, device=dev, dtype=torch.int64) * 2 + 1
+    ctx = torch.repeat_interleave(torch.arange(n, device=dev), lens_t)
+    k = torch.arange(N, device=dev, dtype=torch.int64) - off[:-1][ctx]
+    elems = ((base[ctx] + k * stride[ctx]) & (U - 1)).to(torch.int32)
+    del ctx, k
+    prios = torch.randint(0, 4, (N,), generator=g, device=dev, dtype=torch.int8)
+    return off, elems, prios
+
+
+@pytest.mark.parametrize("n,mean,U,distinct", [(200_000, 2000, 1 << 22, False), (4000, 2000, 1 << 16, True)],
+                         ids=["c3_200k", "distinct_len"])
+def test_c3_minimize_vs_oracle(gpu, n, mean, U, distinct):
+    rng = np.random.default_rng(2018)
+    if distinct:
+        lens = rng.permutation(np.arange(1, 2 * mean + 1))[:n]  # distinct Len: sort order is unambiguous
+    else:
+        lens = np.minimum(rng.geometric(1.0 / mean, size=n), U)
+    off, elems, prios = _corpus_dev(gpu.dev, n, lens, U, seed=n)
+    keep, cnt = gpu.minimize(off, elems, prios, hint_distinct=U)
+    torch.cuda.synchronize()
+    got = np.nonzero(keep.cpu().numpy())[0]
+    exp = np.array(O.minimize(_u(off, np.uint64), _u(elems, np.uint32), _u(prios, np.int8)), np.int64)
+    assert cnt == exp.size
+    np.testing.assert_array_equal(got, exp)
+
+
+def _owner_split(gpu, m0e, m0p, G, chunk=1 << 27):
+    """M0 entries per owner shard (order kept), computed on device in chunks."""
+    from syzkaller_amd.dist import owner_of_torch
+
+    parts = [[] for _ in range(G)]
+    for a in range(0, m0e.numel(), chunk):
+        e, p = m0e[a:a + chunk], m0p[a:a + chunk]
+        own = owner_of_torch(e, G)
+        for g in range(G):
+            m = own == g
+            parts[g].append((e[m], p[m]))
+        del own
+    return [(torch.cat([x[0] for x in q]), torch.cat([x[1] for x in q])) for q in parts]
+
+
+def test_c4_sharded_1b_vs_unsharded(gpu):
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+
+    G, NM0 = 8, 1_000_000_000
+    cfg = synth.synth_default()
+    P, C, L = 4096, 64, 4096
+    sigs, cs, cnt, prio = device_batch(gpu, cfg, 0, P, C, L)
+    m0e, m0p = gpu.synth_m0(cfg, 2048, NM0)
+    # unsharded: the whole batch against the 1B table
+    ms = gpu.deserialize(m0e, m0p)
+    assert ms.capacity() == 1 << 31
+    ns = S.Signal(None, gpu.eng)
+    pairs = torch.full((16 << 20,), -1, dtype=torch.int64, device=gpu.dev)
+    _, cnew, st = gpu.triage(ms, ns, sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
+    ref_pairs = np.sort(_u(pairs[: st["new_pairs"]], np.uint64))
+    ref_cnew = cnew.clone()
+    # sharded: 8 owner tables, 8 source program ranges
+    split = _owner_split(gpu, m0e, m0p, G)
+    shards = [gpu.deserialize(e, p) for e, p in split]
+    del split
+    news = [S.Signal(None, gpu.eng) for _ in range(G)]
+    levels = sorted(set(int(x) for x in prio.cpu().numpy().astype(np.int8)))
+    ncalls = P * C
+    bounds = [ncalls * s // G for s in range(G + 1)]
+    src = []
+    for s in range(G):
+        a, z = bounds[s], bounds[s + 1]
+        sp = torch.full((16 << 20,), -1, dtype=torch.int64, device=gpu.dev)
+        b, _, scnew = gpu.batch(sigs, cs[a:z].contiguous(), cnt[a:z].contiguous(), prio[a:z].contiguous(),
+                                new_pairs=sp, want_bits=False)
+        send = torch.empty(int(cnt[a:z].to(torch.int64).sum()), dtype=torch.int64, device=gpu.dev)
+        counts, _ = gpu.shard_agg_partition(b, a, levels, G, send)
+        off = np.concatenate([[0], np.cumsum(counts)])
+        src.append((b, scnew, sp, send[: off[-1]], off))
+    flags = []
+    for g in range(G):
+        recv = torch.cat([x[3][x[4][g]: x[4][g + 1]] for x in src])
+        f = torch.zeros(recv.numel(), dtype=torch.uint8, device=gpu.dev)
+        if recv.numel():
+            gpu.triage_records(shards[g], news[g], recv, levels, f)
+        flags.append(f)
+    got_pairs = []
+    for s, (b, scnew, sp, send, off) in enumerate(src):
+        lens = [int(off[g + 1] - off[g]) for g in range(G)]
+        starts = [sum(int(x[4][g + 1] - x[4][g]) for x in src[:s]) for g in range(G)]
+        back = torch.cat([flags[g][starts[g]: starts[g] + lens[g]] for g in range(G)])
+        st2 = gpu.shard_agg_unpartition(b, bounds[s], send, back)
+        assert torch.equal(scnew, ref_cnew[bounds[s]: bounds[s + 1]])
+        got_pairs.append(_u(sp[: st2["new_pairs"]], np.uint64) + (np.uint64(bounds[s]) << np.uint64(32)))
+    np.testing.assert_array_equal(np.sort(np.concatenate(got_pairs)), ref_pairs)
+    # the union of the shards == the unsharded M_final (and newSignal): equal
+    # lengths and an empty Diff both ways (Diff is pinned against the oracle in
+    # test_gpu_signal.py)
+    assert sum(s.Len() for s in shards) == ms.Len()
+    U = S.Signal(None, gpu.eng)
+    for s in shards:
+        U.Merge(s)
+    assert U.Len() == ms.Len()
+    assert ms.Diff(U).is_nil() and U.Diff(ms).is_nil()
+    NU = S.Signal(None, gpu.eng)
+    for s in news:
+        NU.Merge(s)
+    assert NU.Len() == ns.Len() and ns.Diff(NU).is_nil() and NU.Diff(ns).is_nil()
+    del U, NU, shards
+    # oracle on a program prefix: M0 restricted to the prefix's elements gives
+    # the same checkNewSignal result for those calls as the whole 1B M0
+    npre = 16 * C
+    end = int(cs[npre - 1]) + int(cnt[npre - 1])
+    hs, hcs, hcnt, hprio = (_u(sigs[:end], np.uint32), _u(cs[:npre], np.uint64), _u(cnt[:npre], np.uint32),
+                            _u(prio[:npre], np.uint8))
+    keys = np.unique(np.concatenate([hs[int(a): int(a) + int(n)] for a, n in zip(hcs, hcnt)]))
+    fe, fp = O.filter_keys(_u(m0e, np.uint32), _u(m0p, np.int8), keys)
+    _, _, obits, ocnew = O.triage_batch(fe, fp, hs, hcs, hcnt, hprio)
+    np.testing.assert_array_equal(_u(ref_cnew[:npre], np.uint8), ocnew)
+    op = pairs_from_bits(hs, hcs, hcnt, obits)
+    np.testing.assert_array_equal(ref_pairs[ref_pairs < (np.uint64(npre) << np.uint64(32))], op)
+
+
+def test_c5_streaming_skewed_vs_oracle(gpu):
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default(skew=1)
+    P, C, L = 4096, 64, 1024
+    m0e, m0p = gpu.synth_m0(cfg, 1024, 10_000_000)
+    ms = gpu.deserialize(m0e, m0p)
+    ns = S.Signal(None, gpu.eng)
+    oms = O.deserialize(_u(m0e, np.uint32), _u(m0p, np.int8))
+    ons = O.OSig()
+    for batch in range(2):  # the second batch sees the state the first one left
+        sigs, cs, cnt, prio = device_batch(gpu, cfg, batch * P, P, C, L)
+        pairs = torch.full((16 << 20,), -1, dtype=torch.int64, device=gpu.dev)
+        _, cnew, st = gpu.triage(ms, ns, sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
+        hs, hcs, hcnt, hprio = _u(sigs, np.uint32), _u(cs, np.uint64), _u(cnt, np.uint32), _u(prio, np.uint8)
+        ons, obits, ocnew = O.triage_batch_into(oms, hs, hcs, hcnt, hprio, ons)
+        ocnew = ocnew[: hcnt.size]
+        np.testing.assert_array_equal(_u(cnew, np.uint8), ocnew)
+        op = pairs_from_bits(hs, hcs, hcnt, obits[: (hs.size + 31) // 32])
+        assert st["new_pairs"] == op.size
+        np.testing.assert_array_equal(np.sort(_u(pairs[: op.size], np.uint64)), op)
+        assert ms.Len() == oms.Len() and ns.Len() == ons.Len()
+        del sigs, cs, cnt, prio, pairs
+    assert_same_set(ms, oms)
+    assert_same_set(ns, ons)
