@@ -1,5 +1,6 @@
 #!/bin/bash
-# Run bench under several tuning settings (each its own process, own limit).
+# Run bench under several tuning settings (each its own process, own limit);
+# one summary line per setting: ms/step and the K3 stage times.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/sweep
@@ -12,7 +13,7 @@ while read -r envs; do
 	case "$envs" in *" -- "*) extra=${envs#* -- }; envs=${envs%% -- *} ;; esac
 	env $envs timeout -k 10 300 python3 bench.py $ARGS $extra > gpurun_out/sweep/$i.log 2>&1
 	rc=$?
-	echo "$i [$envs $extra] exit $rc $(tail -1 gpurun_out/sweep/$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("ms/step %.2f probe %.2f part %.2f decide %.2f surv %d cand %d" % (d["ms_per_step"], d["stages"]["probe_ms"], d["triage"]["part_ms"], d["stages"]["decide_ms"], d["triage"]["survivors"], d["triage"]["candidates"]))' 2>/dev/null)" | tee -a gpurun_out/sweep/summary.txt
+	echo "$i [$envs $extra] exit $rc $(tail -1 gpurun_out/sweep/$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); s=d["stages"]; print("ms/step %.3f part %.3f agg %.3f fin %.3f edge %.2f parts %d ovf %d" % (d["ms_per_step"], s["part_ms"], s["agg_ms"], s["finalize_ms"], s["edge_ms"], d["triage"]["parts"], d["triage"]["overflow_parts"]))' 2>/dev/null)" | tee -a gpurun_out/sweep/summary.txt
 	[ $rc -gt 1 ] && exit $rc
 done < "${SWEEP_FILE:-scripts/sweep.txt}"
 exit 0

@@ -29,7 +29,7 @@
 //   k_agg_count / k_agg_scan_chunks / k_agg_scan_totals / k_agg_scatter
 //       records -> 4-B packed records grouped by partition, cells in chunk order.
 //   k_agg       one 1024-thread workgroup per partition: an LDS hash table
-//       (residual key + 4 level firsts, 20 B/slot, kAggSlots slots = 155 KiB)
+//       (residual key + 4 level firsts, 20 B/slot, kAggSlots slots = 145 KiB)
 //       absorbs the partition's records -- one ds_read_b128 of the home bucket,
 //       a ds_cmpst on first sight, one ds_min per record; then the distinct
 //       elements are written out compactly.  A partition with more distinct
@@ -50,7 +50,7 @@
 namespace syz {
 
 constexpr uint32_t kAggThreads = 1024;
-constexpr uint32_t kAggSlots = 7936;               // LDS slots per workgroup
+constexpr uint32_t kAggSlots = 7424;               // LDS slots per workgroup (+ 8 KB of first-sight queues)
 constexpr uint32_t kAggBuckets = kAggSlots / 4;    // 4-key buckets (one ds_read_b128 per probe)
 constexpr uint32_t kAggNoSlot = 0xFFFFFFFFu;
 constexpr uint32_t kAggRegion = kAggSlots;         // distinct-list region per partition
@@ -128,10 +128,10 @@ __device__ __forceinline__ uint32_t bucket_first_empty(uint4 B)
 // b, whose snapshot B the caller already read.  Keys only go empty -> key, so
 // a key is always at or before the first empty slot of its probe sequence:
 // an insert is one ds_cmpst at the snapshot's first empty slot, re-reading the
-// bucket only when another lane took that slot first.  Returns the slot, or
-// kAggNoSlot once the table is past its limit (the partition is then redone
-// in HBM).
-__device__ uint32_t agg_find_insert(uint4* kb, uint32_t e, uint32_t b, uint4 B, uint32_t* s_n, uint32_t* s_ovf)
+// bucket only when another lane took that slot first.  Returns the slot
+// (ins incremented if this call inserted e), or kAggNoSlot if the probe sequence ran
+// through the whole table (the partition is then redone in HBM).
+__device__ uint32_t agg_find_insert(uint4* kb, uint32_t e, uint32_t b, uint4 B, uint32_t* s_ovf, uint32_t& ins)
 {
 	uint32_t* keys = reinterpret_cast<uint32_t*>(kb);
 	for (uint32_t step = 0; step < kAggBuckets;) {
@@ -148,8 +148,7 @@ __device__ uint32_t agg_find_insert(uint4* kb, uint32_t e, uint32_t b, uint4 B, 
 		const uint32_t i = b * 4 + j;
 		const uint32_t key = atomicCAS(&keys[i], kAggEmpty, e);
 		if (key == kAggEmpty) {
-			if (atomicAdd(s_n, 1u) >= kAggLimit)
-				lds_flag_set(s_ovf);
+			ins++;
 			return i;
 		}
 		if (key == e)
@@ -441,17 +440,41 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 // LDS counter.  Output: the partition's distinct elements and their level
 // firsts at dist_*[p * kAggRegion ...], cnt[p] = how many, or kAggOverflow
 // when they do not fit the LDS table.
+// U records per lane per batch, D batches in flight ahead of the one absorbed.
+template <uint32_t U, uint32_t D>
 __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict__ recs,
                                                      const uint64_t* __restrict__ rec_base,
                                                      const uint32_t* __restrict__ offsT, uint64_t nchunks, AggGeom g,
-                                                     uint32_t* dist_e, uint4* dist_f, uint32_t* cnt)
+                                                     uint32_t* dist_e, uint4* dist_f, uint32_t* cnt, uint32_t dbg)
 {
-	constexpr uint32_t U = 8;
 	__shared__ uint4 kb[kAggBuckets];  // keys (residuals), 4-slot buckets
 	__shared__ uint32_t fl[4][kAggSlots];
+	// per wave: records whose element was not in its home bucket (first sight,
+	// or a probe chain), gathered across batches and resolved 64 at a time
+	// with every lane busy: (residual, level << 24 | serial)
+	__shared__ uint2 q[kAggThreads / 64][64];
 	__shared__ uint32_t s_n, s_ovf, s_out, s_next;
 	const uint32_t* keys = reinterpret_cast<const uint32_t*>(kb);
 	const uint32_t P = 1u << g.pbits, lane = lane_id();
+	uint2* wq = q[threadIdx.x >> 6];
+	uint32_t qn = 0;  // entries in this wave's queue (uniform)
+	// resolve the queue: find-or-insert each element, then its level first
+	auto flush_queue = [&]() {
+		uint32_t ins = 0;
+		if (lane < qn) {
+			const uint2 e = wq[lane];
+			const uint32_t hb = __umulhi(e.x << g.pbits, kAggBuckets);
+			const uint32_t slot = agg_find_insert(kb, e.x, hb, kb[hb], &s_ovf, ins);
+			if (slot != kAggNoSlot)
+				atomicMin(&fl[e.y >> 24][slot], e.y & 0xFFFFFFu);
+		}
+		// inserts counted per flush (overflow = more than kAggLimit distinct)
+		const uint32_t n_ins = (uint32_t)wave_sum_u64(ins);
+		if (n_ins && lane == 0 && atomicAdd(&s_n, n_ins) + n_ins > kAggLimit)
+			lds_flag_set(&s_ovf);
+		qn = 0;
+		__builtin_amdgcn_wave_barrier();
+	};
 	const uint64_t ngroups = (nchunks + kAggGroup - 1) / kAggGroup;
 	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
 		for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
@@ -478,74 +501,125 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				break;
 			CellGroup cg;
 			cg.load(ot, nchunks, gi);
-			const uint32_t je = cg.bnd[kAggGroup];
-			if (je <= cg.bnd[0])
+			const uint32_t jb = cg.bnd[0], je = cg.bnd[kAggGroup];
+			if (je <= jb)
 				continue;
+			// The group's records through a wave-uniform base (32-bit lane
+			// offsets: saddr loads, no 64-bit address math per record).
+			const uint32_t* gp = pr + jb;
+			const uint32_t n = je - jb, nl = n - 1;
+			const uint32_t chunk0 = (uint32_t)cg.ch0;
 			// Records stream through registers one batch ahead of the LDS work,
-			// ping-ponging between two buffers (a rotating one costs register
-			// moves that wait for the prefetch).  Loads are unconditional (index
+			// ping-ponging between two buffers.  Loads are unconditional (index
 			// clamped): a load under a branch makes the compiler drain vmcnt(0)
 			// at the first use, i.e. wait for the prefetch too.
-			const uint32_t jl = je - 1;
-			auto fetch = [&](uint32_t (&buf)[U], uint32_t j0) {
+			auto fetch = [&](uint32_t (&buf)[U], uint32_t o0) {
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++)
-					buf[u] = __builtin_nontemporal_load(&pr[min(j0 + u * 64 + lane, jl)]);
+					buf[u] = __builtin_nontemporal_load(&gp[min(o0 + u * 64 + lane, nl) & (dbg & 1 ? 0x3FFFu : ~0u)]);
 			};
-			auto absorb = [&](const uint32_t (&buf)[U], uint32_t j0) {
-				uint32_t key[U], lv[U], k[U], hb[U], slot[U];
-				bool ok[U], need[U];
+			// Branch-free per record: the chunk of offset o is the number of cell
+			// boundaries <= o; those at or below the batch start are counted
+			// once per batch on the scalar unit, the (~1-2) inside the batch per
+			// lane, the rest cannot matter.
+			auto absorb = [&](const uint32_t (&buf)[U], uint32_t o0) {
+				if (dbg & 4) {  // timing only: the record stream alone
+					uint32_t x = 0;
+#pragma unroll
+					for (uint32_t u = 0; u < U; u++)
+						x ^= buf[u];
+					if (x == 0x12345679u)
+						lds_flag_set(&s_ovf);
+					return;
+				}
+				uint32_t cbase = chunk0;
+				uint32_t inside = 0;  // bit i: boundary i lies inside this batch
+#pragma unroll
+				for (uint32_t i = 1; i < kAggGroup; i++) {
+					const uint32_t b = cg.bnd[i] - jb;
+					cbase += b <= o0;
+					inside |= (uint32_t)(b > o0 && b < o0 + U * 64) << i;
+				}
+				uint32_t key[U], lv[U], k[U], hb[U], slot[U], c[U];
+				bool ok[U];
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					c[u] = cbase;
+				// a uniform loop over the (0-2 typically) boundaries inside the
+				// batch; each boundary re-read by a scalar load
+				for (uint32_t m = __builtin_amdgcn_readfirstlane(inside); m; m &= m - 1) {
+					const uint32_t b = ot[min<uint64_t>(cg.ch0 + __builtin_ctz(m), nchunks)] - jb;
+#pragma unroll
+					for (uint32_t u = 0; u < U; u++)
+						c[u] += o0 + u * 64 + lane >= b;
+				}
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++) {
-					const uint32_t j = j0 + u * 64 + lane, r = buf[u];
-					ok[u] = j < je;
-					k[u] = cg.serial(j, r, g);
+					const uint32_t o = o0 + u * 64 + lane, r = buf[u];
+					ok[u] = o < n;
+					k[u] = (c[u] << g.cbits()) | g.local(r);
 					key[u] = g.resid(r);
 					lv[u] = g.level(r);
-					hb[u] = agg_home_bucket(key[u], g);
+					hb[u] = __umulhi(r & ~((1u << g.pbits) - 1), kAggBuckets);
 				}
 				// home buckets of all U records in flight together (ds_read_b128 each)
 				uint4 B[U];
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++)
 					B[u] = kb[hb[u]];
+				bool any_need = false;
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++) {
-					need[u] = false;
-					slot[u] = kAggNoSlot;
-					if (!ok[u])
-						continue;
 					const uint32_t f = bucket_find(B[u], key[u]);
-					if (f < 4)
-						slot[u] = hb[u] * 4 + f;
-					else
-						need[u] = true;
+					slot[u] = f < 4 ? hb[u] * 4 + f : kAggNoSlot;
+					any_need |= ok[u] && f >= 4;
 				}
-				// first sight of an element, or a chain past its home bucket
+				// first sight of an element, or a chain past its home bucket: to the
+				// wave's queue (the record's own level first is taken there)
+				if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(any_need) != 0))) {
+#pragma unroll
+					for (uint32_t u = 0; u < U; u++) {
+						const bool nd = ok[u] && slot[u] == kAggNoSlot;
+						const uint64_t m = __ballot(nd);
+						if (!m)
+							continue;
+						const uint32_t c = (uint32_t)__popcll(m);
+						if (qn + c > 64)
+							flush_queue();
+						if (nd)
+							wq[qn + lane_rank(m)] = make_uint2(key[u], (lv[u] << 24) | k[u]);
+						qn += c;
+						ok[u] = ok[u] && !nd;
+					}
+					__builtin_amdgcn_wave_barrier();
+				}
+				if (dbg & 2)  // timing only: no firsts
+					return;
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++)
-					if (need[u])
-						slot[u] = agg_find_insert(kb, key[u], hb[u], B[u], &s_n, &s_ovf);
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++)
-					if (slot[u] != kAggNoSlot)
+					if (ok[u] && slot[u] != kAggNoSlot)
 						atomicMin(&fl[lv[u]][slot[u]], k[u]);
 			};
-			uint32_t ra[U], rb[U];
-			fetch(ra, cg.bnd[0]);
-			for (uint32_t j0 = cg.bnd[0];;) {
-				fetch(rb, j0 + U * 64);
-				absorb(ra, j0);
-				j0 += U * 64;
-				if (j0 >= je || lds_flag(&s_ovf))
-					break;
-				fetch(ra, j0 + U * 64);
-				absorb(rb, j0);
-				j0 += U * 64;
-				if (j0 >= je || lds_flag(&s_ovf))
-					break;
+			// a ring of D + 1 register buffers, rotated by full unrolling (static
+			// indices: no register moves that would wait for the prefetch)
+			uint32_t buf[D + 1][U];
+#pragma unroll
+			for (uint32_t d = 0; d < D; d++)
+				fetch(buf[d], d * U * 64);
+			bool more = true;
+			for (uint32_t o0 = 0; more;) {
+#pragma unroll
+				for (uint32_t t = 0; t <= D; t++) {
+					if (more) {
+						fetch(buf[(t + D) % (D + 1)], o0 + D * U * 64);
+						absorb(buf[t], o0);
+						o0 += U * 64;
+						more = o0 < n && !lds_flag(&s_ovf);
+					}
+				}
 			}
 		}
+		flush_queue();  // every record is absorbed before the barrier
 		__syncthreads();
 		if (s_ovf) {
 			if (threadIdx.x == 0)
@@ -972,8 +1046,19 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
-	k_agg<<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, rec_base, offsT, nchunks, g, (uint32_t*)de, (uint4*)df,
-	                                (uint32_t*)dc);
+	{
+		const uint32_t* r = (const uint32_t*)recs;
+		uint32_t* e = (uint32_t*)de;
+		uint4* f = (uint4*)df;
+		uint32_t* c = (uint32_t*)dc;
+		const uint32_t dbg = ctx->agg_dbg;
+		switch (ctx->agg_variant) {
+		case 1: k_agg<4, 2><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
+		case 2: k_agg<4, 3><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
+		case 3: k_agg<8, 2><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
+		default: k_agg<8, 1><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
+		}
+	}
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));

@@ -35,10 +35,18 @@ namespace syz {
 
 constexpr uint32_t kBinShift = 3;  // 8-slot bins
 constexpr uint32_t kBins = kDedupSize >> kBinShift;
-constexpr uint32_t kEpochMax = 0xFFFFFF;
-constexpr uint32_t kEdgeWaves = 4;
-constexpr uint32_t kEdgeChunk = 64 * kEdgeWaves;  // signals per chunk (one per thread)
-constexpr uint32_t kEdgeDepth = 4;                // chunks in flight per buffer
+constexpr uint32_t kEdgeDepth = 4;  // chunks in flight per buffer
+
+// Geometry of one variant: W waves per program, chunks of 64 * W signals; a
+// conflict stamp is epoch << kPosBits | (chunk - 1 - position).
+template <uint32_t W>
+struct EdgeGeom {
+	static constexpr uint32_t kChunk = 64 * W;
+	static constexpr uint32_t kPosBits = W <= 4 ? 8 : 9;
+	static constexpr uint32_t kPosMask = (1u << kPosBits) - 1;
+	static constexpr uint32_t kEpochMax = (1u << (32 - kPosBits)) - 1;
+	static_assert(kChunk <= (1u << kPosBits), "stamp position field");
+};
 
 // Workgroup barrier that orders LDS only: a plain __syncthreads() is also a
 // release of global memory, i.e. it waits for every global load in flight.
@@ -49,19 +57,24 @@ __device__ __forceinline__ void lds_barrier()
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// stamp s (epoch << 8 | 255 - position) was set by a position before pos this epoch
+// stamp s (epoch << kPosBits | kPosMask - position) was set by a position before pos this epoch
+template <uint32_t W>
 __device__ __forceinline__ bool stamp_earlier(uint32_t s, uint32_t epoch, uint32_t pos)
 {
-	return (s >> 8) == epoch && 255 - (s & 255) < pos;
+	using G = EdgeGeom<W>;
+	return (s >> G::kPosBits) == epoch && G::kPosMask - (s & G::kPosMask) < pos;
 }
 
-__global__ __launch_bounds__(kEdgeChunk) void k_edge_dedup(const uint64_t* __restrict__ pcs, uint64_t npc,
+template <uint32_t W>
+__global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restrict__ pcs, uint64_t npc,
                                                            const uint64_t* __restrict__ call_start,
                                                            const uint32_t* __restrict__ call_len, uint64_t ncalls,
                                                            const uint32_t* __restrict__ prog_call, uint64_t nprog,
                                                            uint32_t* sigs, uint32_t* sig_cnt, uint32_t* completed,
                                                            unsigned long long* cnt)
 {
+	using G = EdgeGeom<W>;
+	constexpr uint32_t kEdgeWaves = W, kEdgeChunk = G::kChunk, kEpochMax = G::kEpochMax;
 	__shared__ uint32_t table[kDedupSize];
 	__shared__ uint32_t stamp[kBins];
 	__shared__ __align__(16) uint32_t s_any[2][kEdgeWaves];
@@ -70,7 +83,7 @@ __global__ __launch_bounds__(kEdgeChunk) void k_edge_dedup(const uint64_t* __res
 	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, pos = threadIdx.x;  // pos: place in a chunk
 	uint32_t seq = 0;
 	// Workgroup OR of a predicate (one barrier): every wave writes its own
-	// flag, one ds_read_b128 reads all four.  Two rows alternate: a row is
+	// flag, ds_read_b128s read them all.  Two rows alternate: a row is
 	// rewritten two calls later, after every wave passed the barrier between.
 	auto wg_any = [&](bool pred) -> bool {
 		uint32_t* row = s_any[seq & 1];
@@ -78,9 +91,14 @@ __global__ __launch_bounds__(kEdgeChunk) void k_edge_dedup(const uint64_t* __res
 		if (lane == 0)
 			row[w] = any;
 		lds_barrier();
-		const uint4 a = *reinterpret_cast<const uint4*>(row);
+		uint32_t o = 0;
+#pragma unroll
+		for (uint32_t i = 0; i < W / 4; i++) {
+			const uint4 a = reinterpret_cast<const uint4*>(row)[i];
+			o |= a.x | a.y | a.z | a.w;
+		}
 		seq++;
-		return (a.x | a.y | a.z | a.w) != 0;
+		return o != 0;
 	};
 	uint64_t err = 0;
 	uint32_t epoch = 0;
@@ -167,7 +185,7 @@ __global__ __launch_bounds__(kEdgeChunk) void k_edge_dedup(const uint64_t* __res
 						lds_barrier();
 					}
 					epoch++;
-					const uint32_t v = (epoch << 8) | (255 - pos);
+					const uint32_t v = (epoch << G::kPosBits) | (G::kPosMask - pos);
 					bool marker = pending && writer, blocked = false;
 					bool mark_now = marker;
 					for (;;) {
@@ -178,7 +196,7 @@ __global__ __launch_bounds__(kEdgeChunk) void k_edge_dedup(const uint64_t* __res
 						}
 						lds_barrier();
 						const uint32_t s0 = stamp[b0], s1 = stamp[b1];
-						blocked = pending && (stamp_earlier(s0, epoch, pos) || stamp_earlier(s1, epoch, pos));
+						blocked = pending && (stamp_earlier<W>(s0, epoch, pos) || stamp_earlier<W>(s1, epoch, pos));
 						mark_now = blocked && !marker;
 						marker = marker || mark_now;
 						if (!wg_any(mark_now))
@@ -268,9 +286,14 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 	if (nprog == 0)
 		return SYZSIG_OK;
 	SYZ_TRY(counters_reset(ctx));
+	// 4 programs per CU (the 32 KB dedup tables bound residency); W waves each
 	const int grid = (int)std::min<uint64_t>(nprog, 256 * 4);
-	k_edge_dedup<<<grid, kEdgeChunk, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call, nprog,
-	                                           d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
+	if (ctx->edge_waves == 8)
+		k_edge_dedup<8><<<grid, 512, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
+		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
+	else
+		k_edge_dedup<4><<<grid, 256, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
+		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
 	SYZ_TRY(counters_fetch(ctx));
 	if (ctx->h_cnt[kCntError])

@@ -103,7 +103,7 @@ def test_triage_agg_auto_vs_oracle(gpu, skew):
     assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
 
 
-AGG_LIMIT = 7936 * 4 // 5  # csrc/agg.hip kAggLimit: distinct elements an LDS partition holds
+AGG_LIMIT = 7424 * 4 // 5  # csrc/agg.hip kAggLimit (kAggSlots * 4 / 5): distinct elements an LDS partition holds
 
 
 def fmix32_inv_np(h):
