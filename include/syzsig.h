@@ -65,6 +65,12 @@ int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable);
  * count of the aggregation path (0 = adaptive, else 8..2048). */
 int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
 
+/* Test knobs that change the code path but never the results:
+ * SYZSIG_DEBUG_FIN_DEFER = the batch finalize sends every element whose probe
+ * sequence leaves its home bucket to the atomic (deferred) path. */
+#define SYZSIG_DEBUG_FIN_DEFER 32u
+int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
+
 /* ---- pkg/signal/signal.go ---- */
 
 /* make(Signal, hint): an empty, non-nil Signal. */

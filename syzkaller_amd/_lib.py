@@ -16,6 +16,7 @@ SYZSIG_ENOMEM = -12
 SYZSIG_EINVAL = -22
 SYZSIG_ERANGE = -34
 SYZSIG_ECORRUPT = -74
+SYZSIG_DEBUG_FIN_DEFER = 32
 
 
 class SyzsigError(RuntimeError):
@@ -64,6 +65,7 @@ SIGNATURES = {
     "syzsig_ctx_stream": (_P, [_P]),
     "syzsig_ctx_set_timing": (c_int, [_P, c_int]),
     "syzsig_ctx_set_agg": (c_int, [_P, c_int, ctypes.c_uint32]),
+    "syzsig_ctx_set_debug": (c_int, [_P, ctypes.c_uint32]),
     "syzsig_set_make": (c_int, [_P, c_uint64, _PP]),
     "syzsig_set_free": (None, [_P]),
     "syzsig_set_clone": (c_int, [_P, _P, _PP]),

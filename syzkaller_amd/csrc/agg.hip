@@ -752,7 +752,8 @@ __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __
                                                               LevelMap lm, uint64_t c0, uint64_t* slots,
                                                               uint64_t bmask, uint64_t* ns_slots, uint64_t ns_bmask,
                                                               uint8_t* call_new, uint64_t* pairs,
-                                                              unsigned long long* npairs, unsigned long long* ctr)
+                                                              unsigned long long* npairs, unsigned long long* ctr,
+                                                              uint32_t dbg)
 {
 	__shared__ uint64_t buf[kFinBuf];
 	__shared__ uint32_t s_n;
@@ -831,7 +832,7 @@ __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __
 					slots[idx] = word;  // one entry per element: no other writer
 				inserted += !present;   // fresh, or an "absent" marker going live
 				changed++;
-				const int rr = tbl_merge_from(ns_slots, ns_bmask, e[k], P, bn[k]);
+				const int rr = (dbg & 8) ? 0 : tbl_merge_from(ns_slots, ns_bmask, e[k], P, bn[k]);  // dbg: timing only
 				ns_ins += rr == 1;
 				ovf += rr < 0;
 				// the staircase: first records of strictly rising level above M0[e]
@@ -863,6 +864,282 @@ __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __
 	block_count(&ctr[kCntInserted], inserted);
 	block_count(&ctr[kCntChanged], changed);
 	block_count(&ctr[kCntAux], ns_ins);
+	block_count(&ctr[kCntOverflow], ovf);
+}
+
+// ---- the finalize without device-scope atomics (the fast path) ----
+// Region r < P is partition r, and the home buckets of its elements form one
+// contiguous slice of maxSignal (and of newSignal) whenever the table has at
+// least P buckets: slice = buckets [r << shift, (r + 1) << shift).  Inside a
+// slice the block is the only writer during this launch, so a found element is
+// updated with a plain store, and an absent one takes the first empty slot of
+// its probe sequence that no other element of the block claimed first -- the
+// claims are LDS compare-and-swaps on the slot's index, not global atomics
+// (measured: device-scope CAS runs at ~20 G/s chip-wide and bounded the
+// atomic finalize).  Probe sequences stop at the slice end: such an element
+// (or one whose claim table is full) is deferred to k_fin_deferred /
+// k_ns_deferred, which run after this launch with the global-atomic code.
+// Correct slot choice: slots only go empty -> key, so an element present at
+// launch start sits before the first slot that was empty then; a slot seen
+// occupied, or claimed by another element, is occupied at launch end, so the
+// occupied-prefix invariant of every probe sequence still holds.
+constexpr uint32_t kFxThreads = 512, kFxIlp = 2, kFxSet = 8192, kFxBuf = 2048, kFxProbe = 64;
+enum : int { kFxTaken = 0, kFxClaimed = 1, kFxFull = 2 };
+
+__device__ __forceinline__ int fx_claim(uint32_t* set, uint32_t tag, uint64_t rel)
+{
+	const uint32_t key = (tag << 31) | (uint32_t)(rel + 1);
+	uint32_t h = fmix32(key) & (kFxSet - 1);
+	for (uint32_t step = 0; step < kFxProbe; step++) {
+		uint32_t v = set[h];
+		if (v == 0) {
+			v = atomicCAS(&set[h], 0u, key);
+			if (v == 0)
+				return kFxClaimed;
+		}
+		if (v == key)
+			return kFxTaken;
+		h = (h + 1) & (kFxSet - 1);
+	}
+	return kFxFull;
+}
+
+// Walk the probe sequence of e inside [b, bend) (B = the home bucket, loaded).
+// Returns the slot index with old = its word (found), or with old = 0 (claimed
+// for e); -1 = defer (slice end, or the claim table is full).
+__device__ __forceinline__ int64_t fx_walk(const uint64_t* tab, uint64_t b, uint64_t bend, uint64_t slice0,
+                                           uint32_t e, Bucket B, uint32_t* set, uint32_t tag, uint64_t& old)
+{
+	for (uint64_t b0 = b; b < bend; b++) {
+		if (b != b0)
+			B = load_bucket(tab + (b << kBucketShift));
+#pragma unroll
+		for (uint32_t i = 0; i < kBucketSlots; i++) {
+			const uint64_t sw = B.s[i], idx = (b << kBucketShift) + i;
+			if (sw != kSlotEmpty) {
+				if (slot_key(sw) == e) {
+					old = sw;
+					return (int64_t)idx;
+				}
+				continue;
+			}
+			const int c = fx_claim(set, tag, idx - slice0);
+			if (c == kFxClaimed) {
+				old = 0;
+				return (int64_t)idx;
+			}
+			if (c == kFxFull)
+				return -1;
+		}
+	}
+	return -1;
+}
+
+__global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
+    const uint32_t* __restrict__ dist_e, const uint4* __restrict__ dist_f, const uint32_t* __restrict__ cnt,
+    uint32_t nregions, LevelMap lm, uint64_t c0, uint64_t* slots, uint64_t bmask, uint32_t ms_shift,
+    uint64_t* ns_slots, uint64_t ns_bmask, uint32_t ns_shift, uint8_t* call_new, uint64_t* pairs,
+    unsigned long long* npairs, unsigned long long* ctr, uint32_t* def_e, uint4* def_f,
+    unsigned long long* def_cnt, uint64_t* def_ns, unsigned long long* def_ns_cnt, uint32_t dbg)
+{
+	__shared__ uint32_t claim[kFxSet];
+	__shared__ uint64_t buf[kFxBuf];
+	__shared__ uint32_t s_n;
+	__shared__ unsigned long long s_base;
+	uint64_t inserted = 0, changed = 0, ns_ins = 0;
+	auto flush = [&](uint32_t nb) {  // every thread; nb = s_n read after a barrier
+		nb = min(nb, kFxBuf);
+		if (threadIdx.x == 0)
+			s_base = atomicAdd(npairs, (unsigned long long)nb);
+		__syncthreads();
+		for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x)
+			pairs[s_base + t] = buf[t];
+		__syncthreads();
+		if (threadIdx.x == 0)
+			s_n = 0;
+		__syncthreads();
+	};
+	auto emit = [&](uint64_t v) {
+		const uint32_t k = atomicAdd(&s_n, 1u);
+		if (k < kFxBuf)
+			buf[k] = v;
+		else
+			pairs[atomicAdd(npairs, 1ull)] = v;
+	};
+	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
+		for (uint32_t i = threadIdx.x; i < kFxSet; i += blockDim.x)
+			claim[i] = 0;
+		if (threadIdx.x == 0)
+			s_n = 0;
+		__syncthreads();
+		const uint64_t ms0 = (uint64_t)r << ms_shift, ms1 = (uint64_t)(r + 1) << ms_shift;
+		const uint64_t ns0 = (uint64_t)r << ns_shift, ns1 = (uint64_t)(r + 1) << ns_shift;
+		const uint32_t n = cnt[r];
+		for (uint32_t i0 = 0; i0 < n; i0 += kFxIlp * kFxThreads) {
+			uint32_t e[kFxIlp];
+			uint4 f4[kFxIlp];
+			int top[kFxIlp];
+#pragma unroll
+			for (uint32_t k = 0; k < kFxIlp; k++) {
+				const uint32_t i = i0 + k * kFxThreads + threadIdx.x;
+				const uint64_t o = (uint64_t)r * kAggRegion + min(i, n - 1);
+				e[k] = dist_e[o];
+				f4[k] = dist_f[o];
+				top[k] = -1;
+				const uint32_t f[4] = {f4[k].x, f4[k].y, f4[k].z, f4[k].w};
+#pragma unroll
+				for (int l = 0; l < 4; l++)
+					if (i < n && l < (int)lm.n && f[l] != kAggNone)
+						top[k] = l;
+			}
+			Bucket bm[kFxIlp], bn[kFxIlp];
+#pragma unroll
+			for (uint32_t k = 0; k < kFxIlp; k++) {
+				if (top[k] >= 0) {
+					bm[k] = load_bucket(slots + (home_bucket(e[k], bmask) << kBucketShift));
+					bn[k] = load_bucket(ns_slots + (home_bucket(e[k], ns_bmask) << kBucketShift));
+				}
+			}
+#pragma unroll
+			for (uint32_t k = 0; k < kFxIlp; k++) {
+				if (top[k] < 0)
+					continue;
+				const uint32_t f[4] = {f4[k].x, f4[k].y, f4[k].z, f4[k].w};
+				const int8_t P = lm.val[top[k]];
+				const uint64_t word = make_slot(e[k], P);
+				uint64_t old = 0;
+				// (dbg & 32, tests: defer every walk that leaves the home bucket)
+				const uint64_t hm = home_bucket(e[k], bmask), hn = home_bucket(e[k], ns_bmask);
+				const int64_t idx = fx_walk(slots, hm, dbg & 32 ? hm + 1 : ms1, ms0 << kBucketShift, e[k], bm[k],
+				                            claim, 0, old);
+				if (idx < 0) {  // the atomic path takes the whole element
+					const uint64_t d = atomicAdd(def_cnt, 1ull);
+					def_e[d] = e[k];
+					def_f[d] = f4[k];
+					continue;
+				}
+				const bool present = slot_live(old);
+				const int p0 = present ? (int)slot_prio(old) : -1000;
+				if ((int)P <= p0)
+					continue;  // (a claimed slot always has P > p0)
+				slots[idx] = word;    // the block's own slice: no other writer
+				inserted += !present; // fresh, or an "absent" marker going live
+				changed++;
+				uint64_t nold = 0;
+				const int64_t nidx = fx_walk(ns_slots, hn, dbg & 32 ? hn + 1 : ns1, ns0 << kBucketShift, e[k], bn[k],
+				                             claim, 1, nold);
+				if (nidx < 0) {
+					def_ns[atomicAdd(def_ns_cnt, 1ull)] = ((uint64_t)e[k] << 32) | prio_biased(P);
+				} else if (nold == 0 || nold < word) {
+					ns_slots[nidx] = word;
+					ns_ins += nold == 0;
+				}
+				// the staircase: first records of strictly rising level above M0[e]
+				uint32_t mk = kAggNone;
+#pragma unroll
+				for (int l = 3; l >= 0; l--) {
+					if (l > top[k] || f[l] == kAggNone)
+						continue;
+					if ((int)lm.val[l] <= p0)
+						break;
+					if (f[l] < mk) {
+						mk = f[l];
+						const uint64_t c = c0 + f[l];
+						call_new[c] = 1;
+						emit((c << 32) | e[k]);
+					}
+				}
+			}
+			__syncthreads();
+			const uint32_t nb = s_n;
+			if (nb > kFxBuf / 2)
+				flush(nb);
+		}
+		__syncthreads();
+		const uint32_t nb = s_n;
+		if (nb)
+			flush(nb);
+	}
+	block_count(&ctr[kCntInserted], inserted);
+	block_count(&ctr[kCntChanged], changed);
+	block_count(&ctr[kCntAux], ns_ins);
+}
+
+// Deferred elements of k_agg_finalize_x, with the global-atomic table code
+// (launched after it: the slices are free for everyone again).
+__global__ __launch_bounds__(256) void k_fin_deferred(const uint32_t* __restrict__ def_e, const uint4* __restrict__ def_f,
+                                                      const unsigned long long* __restrict__ def_cnt, LevelMap lm,
+                                                      uint64_t c0, uint64_t* slots, uint64_t bmask, uint64_t* ns_slots,
+                                                      uint64_t ns_bmask, uint8_t* call_new, uint64_t* pairs,
+                                                      unsigned long long* npairs, unsigned long long* ctr)
+{
+	const uint64_t n = *def_cnt, max_probe = max_probe_for(bmask);
+	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint32_t e = def_e[i];
+		const uint4 f4 = def_f[i];
+		const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
+		int top = -1;
+#pragma unroll
+		for (int l = 0; l < 4; l++)
+			if (l < (int)lm.n && f[l] != kAggNone)
+				top = l;
+		if (top < 0)
+			continue;
+		const int8_t P = lm.val[top];
+		const uint64_t word = make_slot(e, P);
+		uint64_t old = 0;
+		const int64_t idx = tbl_find_or_insert(slots, bmask, e, word, old, max_probe);
+		if (idx < 0) {
+			ovf++;
+			continue;
+		}
+		const bool present = slot_live(old);
+		const int p0 = present ? (int)slot_prio(old) : -1000;
+		if ((int)P <= p0)
+			continue;
+		if (old != 0)
+			slots[idx] = word;
+		inserted += !present;
+		changed++;
+		const int rr = tbl_merge(ns_slots, ns_bmask, e, P);
+		ns_ins += rr == 1;
+		ovf += rr < 0;
+		uint32_t mk = kAggNone;
+#pragma unroll
+		for (int l = 3; l >= 0; l--) {
+			if (l > top || f[l] == kAggNone)
+				continue;
+			if ((int)lm.val[l] <= p0)
+				break;
+			if (f[l] < mk) {
+				mk = f[l];
+				const uint64_t c = c0 + f[l];
+				call_new[c] = 1;
+				pairs[atomicAdd(npairs, 1ull)] = (c << 32) | e;
+			}
+		}
+	}
+	block_count(&ctr[kCntInserted], inserted);
+	block_count(&ctr[kCntChanged], changed);
+	block_count(&ctr[kCntAux], ns_ins);
+	block_count(&ctr[kCntOverflow], ovf);
+}
+
+// Deferred newSignal merges of k_agg_finalize_x: (elem << 32 | prio ^ 0x80).
+__global__ __launch_bounds__(256) void k_ns_deferred(const uint64_t* __restrict__ def_ns,
+                                                     const unsigned long long* __restrict__ def_ns_cnt,
+                                                     uint64_t* ns_slots, uint64_t ns_bmask, unsigned long long* ctr)
+{
+	const uint64_t n = *def_ns_cnt;
+	uint64_t ins = 0, ovf = 0;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t v = def_ns[i];
+		const int r = tbl_merge(ns_slots, ns_bmask, (uint32_t)(v >> 32), (int8_t)((uint8_t)v ^ 0x80u));
+		ins += r == 1;
+		ovf += r < 0;
+	}
+	block_count(&ctr[kCntAux], ins);
 	block_count(&ctr[kCntOverflow], ovf);
 }
 
@@ -1148,6 +1425,7 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	out->dist_f = (const uint4*)dist_f;
 	out->cnt = (const uint32_t*)dc;
 	out->nregions = nregions;
+	out->parts = P;
 	out->D = D;
 	return SYZSIG_OK;
 }
@@ -1181,11 +1459,33 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 	syzsig_set* nsp = *ns;
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
-	if (D)
+	// the slice-exclusive finalize when every region is a partition and both
+	// tables have at least one bucket per partition; else the atomic one
+	const bool fx = D && nsp && a.nregions == a.parts && ms->nbuckets >= a.parts && nsp->nbuckets >= a.parts &&
+	                !(ctx->agg_dbg & 16);
+	if (fx) {
+		const uint32_t pb = 31 - __builtin_clz(a.parts);
+		const uint32_t ms_shift = (63 - __builtin_clzll(ms->nbuckets)) - pb;
+		const uint32_t ns_shift = (63 - __builtin_clzll(nsp->nbuckets)) - pb;
+		void *dd, *dn;
+		SYZ_TRY(ws_get(ctx, 32, D * 20 + 64, &dd));
+		SYZ_TRY(ws_get(ctx, 33, D * 8 + 64, &dn));
+		uint32_t* def_e = (uint32_t*)dd;
+		uint4* def_f = (uint4*)((char*)dd + ((D * 4 + 15) & ~15ull));
+		k_agg_finalize_x<<<a.nregions, kFxThreads, 0, s>>>(
+		    a.dist_e, a.dist_f, a.cnt, a.nregions, lm, c0, ms->slots, ms->nbuckets - 1, ms_shift, nsp->slots,
+		    nsp->nbuckets - 1, ns_shift, b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2], ctx->d_cnt, def_e, def_f,
+		    &ctx->d_cnt[kCntDefer], (uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], ctx->agg_dbg);
+		k_fin_deferred<<<64, 256, 0, s>>>(def_e, def_f, &ctx->d_cnt[kCntDefer], lm, c0, ms->slots, ms->nbuckets - 1, nsp->slots,
+		                                  nsp->nbuckets - 1, b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2],
+		                                  ctx->d_cnt);
+		k_ns_deferred<<<64, 256, 0, s>>>((const uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], nsp->slots, nsp->nbuckets - 1, ctx->d_cnt);
+	} else if (D) {
 		k_agg_finalize<<<a.nregions, kFinThreads, 0, s>>>(
 		    a.dist_e, a.dist_f, a.cnt, a.nregions, lm, c0, ms->slots,
 		    ms->nbuckets - 1, nsp ? nsp->slots : nullptr, nsp ? nsp->nbuckets - 1 : 0, b->call_new, (uint64_t*)pr,
-		    &ctx->d_cnt[kCntAux2], ctx->d_cnt);
+		    &ctx->d_cnt[kCntAux2], ctx->d_cnt, ctx->agg_dbg);
+	}
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[3], s));

@@ -53,6 +53,8 @@ enum Counter : int {
 	kCntChanged,        // triage: slots committed (prio raised or inserted)
 	kCntAux,            // misc (serialize cursor, minimize winners...)
 	kCntAux2,
+	kCntDefer,          // triage finalize: elements deferred to the atomic path
+	kCntDeferNs,        // triage finalize: newSignal merges deferred to the atomic path
 	kNumCounters = 16,
 };
 
@@ -84,8 +86,8 @@ struct syzsig_ctx {
 	// grow-only scratch buffers by role: 0-2 set ops, 3-6 triage candidates and
 	// small state, 7-10 host uploads of minimize, 11-14 triage partitions and
 	// minimize internals and triage pairs (13-15), 16-23 + 30-31 triage aggregation,
-	// 24-29 check_new_signal uploads
-	syz::Workspace ws[32];
+	// 24-29 check_new_signal uploads, 32-34 the finalize's deferred lists
+	syz::Workspace ws[40];
 	bool timing = false;                  // HIP events around triage kernels
 	// tuning knobs (defaults; SYZSIG_* environment overrides read at ctx creation)
 	int part_mode = 1;                    // 0 = never use the aggregation path (agg.hip)
@@ -158,6 +160,7 @@ struct AggOut {
 	const uint4* dist_f;     // their first serial per level (0xFFFFFFFF = none)
 	const uint32_t* cnt;     // per region, device
 	uint32_t nregions;
+	uint32_t parts;          // partitions P; regions [0, P) are partitions (nregions > P: HBM fallback lists)
 	uint64_t D;              // distinct elements in all regions
 };
 int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const LevelMap& lm,

@@ -184,6 +184,15 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts)
 	return SYZSIG_OK;
 }
 
+int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx)
+		return syz::fail(SYZSIG_EINVAL, "ctx_set_debug: ctx is NULL");
+	ctx->agg_dbg = flags & SYZSIG_DEBUG_FIN_DEFER;  // only the result-preserving flags
+	return SYZSIG_OK;
+}
+
 int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable)
 {
 	SYZ_LOCK(ctx);

@@ -41,6 +41,10 @@ class Engine:
         """Large-batch triage path: 0 per-call, 1 auto (default), 2 aggregation always."""
         check(self.L.syzsig_ctx_set_agg(self.h, int(mode), int(parts)))
 
+    def set_debug(self, flags):
+        """Result-preserving code-path knobs (include/syzsig.h SYZSIG_DEBUG_*), for tests."""
+        check(self.L.syzsig_ctx_set_debug(self.h, int(flags)))
+
     def close(self):
         if self.h:
             self.L.syzsig_ctx_destroy(self.h)

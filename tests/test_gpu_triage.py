@@ -106,6 +106,34 @@ def test_triage_agg_auto_vs_oracle(gpu, skew):
 AGG_LIMIT = 7424 * 4 // 5  # csrc/agg.hip kAggLimit (kAggSlots * 4 / 5): distinct elements an LDS partition holds
 
 
+@pytest.mark.parametrize("case", ["tight_tables", "nil_new_signal"])
+def test_triage_finalize_deferred_path(gpu, case):
+    """The finalize's slice-exclusive fast path and its deferred (atomic) path:
+    with SYZSIG_DEBUG_FIN_DEFER every element whose probe sequence leaves its
+    home bucket takes the deferred path; results must equal the oracle's.
+    tight_tables: maxSignal and newSignal loaded close to their growth limit,
+    so probe chains are long and slice ends are reached."""
+    from syzkaller_amd import synth
+    from syzkaller_amd._lib import SYZSIG_DEBUG_FIN_DEFER
+
+    cfg = synth.synth_default()
+    nprog, cpp = 128, 32
+    cl = synth.call_lengths(nprog, cpp, 2048)
+    m0 = synth.m0(cfg, 2048, 700_000 if case == "tight_tables" else 50_000)
+    new0 = None
+    if case == "tight_tables":
+        e = np.unique(np.random.default_rng(5).integers(0, 1 << 32, 300_000, dtype=np.uint64).astype(np.uint32))
+        new0 = (e, np.zeros(e.size, np.int8))
+    for dbg in (0, SYZSIG_DEBUG_FIN_DEFER):
+        gpu.eng.set_debug(dbg)
+        try:
+            st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl), new0=new0,
+                         agg=2)
+        finally:
+            gpu.eng.set_debug(0)
+        assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
+
+
 def fmix32_inv_np(h):
     """Inverse of murmur3 fmix32 (csrc/agg.hip fmix32_inv), on a u32 array."""
     h = np.asarray(h, np.uint32).copy()
