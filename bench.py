@@ -13,7 +13,12 @@ hash-sharded over the ranks (10M elements per rank), each rank owns its own
 4096-program slice of the batch (weak scaling), records are routed to their
 owner with RCCL all-to-all (syzkaller_amd/dist.py).
 
-Prints one JSON line on rank 0.
+Prints one JSON line on rank 0.  Beside the headline K3 line it carries, as
+their own objects with their own roofline, `lines.edge` (K1+K2: KCOV PCs ->
+edge signals, 12 B/PC) and `lines.minimize` (BASELINE config 3: Minimize over
+a 200k-context corpus, 5 B/entry + 4 B/distinct element); `cpu_baseline` is
+the oracle on one core plus `multi_core` (--cpu-threads Procs under one
+rwlock, as syz-fuzzer runs checkNewSignal), with nproc and the CPU model.
 """
 import argparse
 import json
@@ -31,7 +36,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PROBE_BYTES_PER_REC = 12.0  # 4 B element read + 8 B maxSignal slot read
 # the K3 pipeline of one step on one GPU (csrc/agg.hip); roofline.avg_launch_ms is
 # their summed device time (HIP events), roofline.traffic their summed PMC bytes
-K3_KERNELS = "k_agg_count+k_agg_scan_chunks+k_agg_scan_totals+k_agg_scatter+k_agg+k_agg_finalize"
+K3_KERNELS = "k_agg_count+k_agg_scan_chunks+k_agg_scan_totals+k_agg_scatter+k_agg+k_agg_finalize_x+k_fin_deferred+k_ns_deferred"
+EDGE_BYTES_PER_PC = 12.0  # K1+K2: 8 B u64 PC in + 4 B u32 signal out
+MIN_BYTES_PER_ENTRY, MIN_BYTES_PER_DISTINCT = 5.0, 4.0  # Minimize: (elem, prio) entry + covered[e]
 # N > 1: the source's aggregation, then the owner's records-mode triage of the staircases
 K3_DIST_KERNELS = "k_agg_count+k_agg_scan_chunks+k_agg_scan_totals+k_agg_scatter+k_agg+k_probe+k_decide"
 
@@ -53,6 +60,10 @@ def parse():
                          "sharing fewer GPUs (rank r uses GPU r mod device_count)")
     ap.add_argument("--table-hint", type=int, default=0,
                     help="size maxSignal's table for this many entries (default: the library's policy)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the multi-core CPU baseline (the GPU box's CPU share is 16 per GPU)")
+    ap.add_argument("--min-contexts", type=int, default=200_000, help="Minimize line: corpus size (BASELINE config 3)")
+    ap.add_argument("--no-min", action="store_true", help="skip the Minimize line")
     return ap.parse_args()
 
 
@@ -84,10 +95,22 @@ def pmc_traffic(kernel_prefixes, cfg):
     return (best[1], best[2]) if best else (None, None)
 
 
-def cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, calls_per_prog, target_s):
-    """The oracle (single-threaded C restatement of checkNewSignal/pkg/signal,
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, calls_per_prog, target_s, threads):
+    """The oracle (plain-C restatement of checkNewSignal/pkg/signal,
     oracle/oracle.c) on a bounded sample: the first S programs of this batch
-    against the same M0."""
+    against the same M0.  1 core: the sequential loop; N cores: `threads`
+    Procs running fuzzer.go:494-511 concurrently (DiffRaw under the reader
+    lock, Merge under the writer lock, orc_triage_batch_mt)."""
     from oracle import oracle as O
 
     h_cs = cs.cpu().numpy().view(np.uint64)
@@ -97,25 +120,77 @@ def cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, calls_per_prog, target_s):
     p = m0p.cpu().numpy()
     nprog_total = h_cnt.size // calls_per_prog
 
-    def run(nprog):
+    def run(nprog, nthreads):
         nc = nprog * calls_per_prog
         end = int(h_cs[nc - 1]) + int(h_cnt[nc - 1])
         h_sigs = sigs[:end].cpu().numpy().view(np.uint32)
         ms = O.deserialize(e, p)
         t = time.perf_counter()
-        O.triage_batch_into(ms, h_sigs, h_cs[:nc], h_cnt[:nc], h_prio[:nc])
+        if nthreads == 1:
+            O.triage_batch_into(ms, h_sigs, h_cs[:nc], h_cnt[:nc], h_prio[:nc])
+        else:
+            O.triage_batch_mt(ms, h_sigs, h_cs[:nc], h_cnt[:nc], h_prio[:nc], calls_per_prog, nthreads)
         dt = time.perf_counter() - t
         return int(h_cnt[:nc].sum()), dt
 
-    n = 8
-    recs, dt = run(n)
-    est = max(1, min(nprog_total, int(n * target_s / max(dt, 1e-3))))
-    if est > n:
-        n = est
-        recs, dt = run(n)
-    return {"value": recs / dt, "unit": "elems/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} programs ({recs} signal elements) of the same batch vs the same M0, "
-                      f"oracle/oracle.c single thread, {dt:.2f} s"}
+    def sample(nthreads, budget):
+        n = 8
+        recs, dt = run(n, nthreads)
+        est = max(1, min(nprog_total, int(n * budget / max(dt, 1e-3))))
+        if est > n:
+            n = est
+            recs, dt = run(n, nthreads)
+        return n, recs, dt
+
+    n, recs, dt = sample(1, target_s)
+    out = {"value": recs / dt, "unit": "elems/s", "cores": 1, "kind": "port",
+           "sample": f"first {n} programs ({recs} signal elements) of the same batch vs the same M0, "
+                     f"oracle/oracle.c single thread, {dt:.2f} s",
+           "nproc": os.cpu_count(), "cpu_model": cpu_model()}
+    if threads > 1:
+        n2, recs2, dt2 = sample(threads, target_s / 2)
+        out["multi_core"] = {"value": recs2 / dt2, "unit": "elems/s", "cores": threads, "kind": "port",
+                             "sample": f"first {n2} programs ({recs2} signal elements), {threads} threads as Procs "
+                                       f"under one rwlock (fuzzer.go:494-511, oracle.c orc_triage_batch_mt), "
+                                       f"{dt2:.2f} s"}
+    return out
+
+
+def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
+    """BASELINE config 3: signal.Minimize (pkg/signal/signal.go:138-166) over a
+    synthetic n-context corpus (geometric lengths, mean `mean`, elements from a
+    2^22 universe, distinct inside a context, prio 0..3), resident in HBM;
+    device time of syzsig_minimize_dev (HIP events)."""
+    g = torch.Generator(device=dev.dev).manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    lens = torch.as_tensor(np.minimum(rng.geometric(1.0 / mean, size=n), U), dtype=torch.int64, device=dev.dev)
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev.dev)
+    off[1:] = torch.cumsum(lens, 0)
+    N = int(off[-1])
+    base = torch.randint(0, U, (n,), generator=g, device=dev.dev, dtype=torch.int64)
+    stride = torch.randint(0, U // 2, (n,), generator=g, device=dev.dev, dtype=torch.int64) * 2 + 1
+    ctx = torch.repeat_interleave(torch.arange(n, device=dev.dev), lens)
+    k = torch.arange(N, device=dev.dev, dtype=torch.int64) - off[:-1][ctx]
+    elems = ((base[ctx] + k * stride[ctx]) & (U - 1)).to(torch.int32)
+    del ctx, k
+    prios = torch.randint(0, 4, (N,), generator=g, device=dev.dev, dtype=torch.int8)
+    distinct = int(torch.unique(elems).numel())
+    ms = []
+    for _ in range(reps):
+        keep, cnt = dev.minimize(off, elems, prios, hint_distinct=U)
+        ms.append(dev.L.syzsig_ctx_last_ms(dev.eng.h))
+    t = float(np.median(ms))
+    byts = MIN_BYTES_PER_ENTRY * N + MIN_BYTES_PER_DISTINCT * distinct
+    achieved = byts / (t * 1e-3) / 1e9
+    return {"metric": "signal.Minimize corpus entries/sec", "value": N / (t * 1e-3), "unit": "entries/s",
+            "higher_is_better": True, "ms": t, "dtype": "u32",
+            "config": {"workload": f"BASELINE config 3: Minimize over a {n}-program synthetic corpus, 1 GPU",
+                       "contexts": n, "entries": N, "distinct": distinct, "mean_len": mean, "survivors": cnt},
+            "roofline": {"bound": "hbm", "kernel": "k_min_keys+radix sort+k_min_rank+k_min_cover+k_min_winners",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_unit": f"{MIN_BYTES_PER_ENTRY} B/entry + {MIN_BYTES_PER_DISTINCT} B/distinct",
+                         "avg_launch_ms": t}}
 
 
 def frame_regions(sigs, cs, cnt, prio, comp, P, C):
@@ -208,13 +283,14 @@ def main():
     sigs = torch.empty(pcs.numel(), dtype=torch.int32, device=dev.dev)
     cnt = torch.empty(P * C, dtype=torch.int32, device=dev.dev)
     comp = torch.empty(P, dtype=torch.int32, device=dev.dev)
-    edge_ms = []
+    edge_ms, edge_dev_ms = [], []
     for i in range(3):
         torch.cuda.synchronize()
         t = time.perf_counter()
         dev.edge_derive(pcs, cs, cl, pidx, sigs, cnt, comp)
         torch.cuda.synchronize()
         edge_ms.append((time.perf_counter() - t) * 1e3)
+        edge_dev_ms.append(dev.L.syzsig_ctx_last_ms(dev.eng.h))
     npc = pcs.numel()
     del pcs
     nrec = int(cnt.to(torch.int64).sum().item())
@@ -320,7 +396,7 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": probe_units,
                          "avg_launch_ms": k3_ms},
-            "stages": {"edge_ms": float(np.median(edge_ms)), "part_ms": part_ms, "agg_ms": probe_ms,
+            "stages": {"edge_ms": float(np.median(edge_ms)), "edge_dev_ms": float(np.median(edge_dev_ms)), "part_ms": part_ms, "agg_ms": probe_ms,
                        "finalize_ms": decide_ms,
                        "edge_pcs_per_s": npc / (np.median(edge_ms) * 1e-3),
                        "ingest_ms": ingest_ms, "ingest_check": ingest_ok},
@@ -330,8 +406,22 @@ def main():
         traffic, src = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], out["config"])
         out["roofline"]["traffic"] = traffic
         out["roofline"]["traffic_source"] = src
+        # K1+K2 (executor write_coverage_signal on device) as its own line
+        e_ms = float(np.median(edge_dev_ms))
+        e_ach = EDGE_BYTES_PER_PC * npc / (e_ms * 1e-3) / 1e9
+        e_traffic, e_src = pmc_traffic(["syz::k_edge_dedup"], out["config"])
+        out["lines"] = {"edge": {
+            "metric": "KCOV PCs -> edge signals/sec (write_coverage_signal K1 + dedup K2)", "value": npc / (e_ms * 1e-3),
+            "unit": "PCs/s", "higher_is_better": True, "ms": e_ms, "dtype": "u64->u32",
+            "config": {"workload": f"BASELINE config 2 batch: {P} programs x {C} calls x {L} PCs", "pcs": npc,
+                       "signals": nrec},
+            "roofline": {"bound": "hbm", "kernel": "k_edge_dedup", "achieved": e_ach, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": e_ach / HBM_PEAK_GBS, "traffic": e_traffic, "traffic_source": e_src,
+                         "bytes_per_unit": EDGE_BYTES_PER_PC, "units_per_launch": npc, "avg_launch_ms": e_ms}}}
+    if rank == 0 and world == 1 and not a.no_min:
+        out["lines"]["minimize"] = minimize_line(dev, a.min_contexts)
     if rank == 0 and world == 1 and not a.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, C, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, C, a.cpu_seconds, a.cpu_threads)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -42,7 +42,7 @@ extern "C" {
 #define SYZSIG_ERANGE (-34)    /* a size limit of this ABI exceeded */
 #define SYZSIG_ECORRUPT (-74)  /* panic("corrupted Serial"), pkg/signal/signal.go:60-62 */
 
-#define SYZSIG_ABI_VERSION 2
+#define SYZSIG_ABI_VERSION 3
 
 typedef struct syzsig_ctx syzsig_ctx;
 typedef struct syzsig_set syzsig_set;
@@ -59,6 +59,9 @@ int syzsig_ctx_set_stream(syzsig_ctx* ctx, void* stream);
 void* syzsig_ctx_stream(syzsig_ctx* ctx);
 /* Record HIP events around the triage kernels (batch stats probe_ms/decide_ms). */
 int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable);
+/* With timing on: device time (ms, HIP events on the context stream) of the
+ * kernels of the last syzsig_edge_derive_dev / syzsig_minimize_dev call. */
+double syzsig_ctx_last_ms(syzsig_ctx* ctx);
 /* Large-batch triage path selection (tests and tuning; results never depend on it):
  * mode 0 = per-call probe path only, 1 = aggregation path for runs of >= 2^20
  * records (default), 2 = aggregation path always; parts = fixed partition

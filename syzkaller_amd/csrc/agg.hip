@@ -883,7 +883,7 @@ __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __
 // launch start sits before the first slot that was empty then; a slot seen
 // occupied, or claimed by another element, is occupied at launch end, so the
 // occupied-prefix invariant of every probe sequence still holds.
-constexpr uint32_t kFxThreads = 512, kFxIlp = 2, kFxSet = 8192, kFxBuf = 2048, kFxProbe = 64;
+constexpr uint32_t kFxThreads = 512, kFxSet = 8192, kFxBuf = 2048, kFxProbe = 64;
 enum : int { kFxTaken = 0, kFxClaimed = 1, kFxFull = 2 };
 
 __device__ __forceinline__ int fx_claim(uint32_t* set, uint32_t tag, uint64_t rel)
@@ -935,6 +935,7 @@ __device__ __forceinline__ int64_t fx_walk(const uint64_t* tab, uint64_t b, uint
 	return -1;
 }
 
+template <uint32_t kFxIlp>
 __global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
     const uint32_t* __restrict__ dist_e, const uint4* __restrict__ dist_f, const uint32_t* __restrict__ cnt,
     uint32_t nregions, LevelMap lm, uint64_t c0, uint64_t* slots, uint64_t bmask, uint32_t ms_shift,
@@ -1333,7 +1334,7 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 		case 1: k_agg<4, 2><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
 		case 2: k_agg<4, 3><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
 		case 3: k_agg<8, 2><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
-		default: k_agg<8, 1><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
+		default: k_agg<8, 1><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;  // 0, 4, 5
 		}
 	}
 	SYZ_HIP(hipGetLastError());
@@ -1472,7 +1473,9 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 		SYZ_TRY(ws_get(ctx, 33, D * 8 + 64, &dn));
 		uint32_t* def_e = (uint32_t*)dd;
 		uint4* def_f = (uint4*)((char*)dd + ((D * 4 + 15) & ~15ull));
-		k_agg_finalize_x<<<a.nregions, kFxThreads, 0, s>>>(
+		auto fin = ctx->agg_variant == 4 ? k_agg_finalize_x<4> : ctx->agg_variant == 5 ? k_agg_finalize_x<1>
+		                                                                                : k_agg_finalize_x<2>;
+		fin<<<a.nregions, kFxThreads, 0, s>>>(
 		    a.dist_e, a.dist_f, a.cnt, a.nregions, lm, c0, ms->slots, ms->nbuckets - 1, ms_shift, nsp->slots,
 		    nsp->nbuckets - 1, ns_shift, b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2], ctx->d_cnt, def_e, def_f,
 		    &ctx->d_cnt[kCntDefer], (uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], ctx->agg_dbg);

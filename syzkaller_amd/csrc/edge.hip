@@ -288,6 +288,8 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 	SYZ_TRY(counters_reset(ctx));
 	// 4 programs per CU (the 32 KB dedup tables bound residency); W waves each
 	const int grid = (int)std::min<uint64_t>(nprog, 256 * 4);
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
 	if (ctx->edge_waves == 8)
 		k_edge_dedup<8><<<grid, 512, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
@@ -295,7 +297,14 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 		k_edge_dedup<4><<<grid, 256, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
 	SYZ_TRY(counters_fetch(ctx));
+	if (ctx->timing) {
+		float t = 0;
+		SYZ_HIP(hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]));
+		ctx->last_ms = t;
+	}
 	if (ctx->h_cnt[kCntError])
 		return fail(SYZSIG_EINVAL, "edge_derive: malformed program/call ranges or a call with >= 262144 PCs");
 	return SYZSIG_OK;

@@ -97,6 +97,7 @@ struct syzsig_ctx {
 	uint32_t agg_variant = 0;             // k_agg pipeline variant (SYZSIG_AGG_VARIANT; tuning)
 	uint32_t agg_dbg = 0;                 // timing-only experiments (SYZSIG_AGG_DBG; results invalid if set)
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+	double last_ms = 0;                   // device time of the last timed entry point's kernels
 };
 
 struct syzsig_set {

@@ -108,6 +108,8 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* 
 	dk2 = (uint32_t*)dv + nctx;
 	dv2 = (uint32_t*)dk2 + nctx;
 	SYZ_TRY(ws_get(ctx, 14, nctx * 4 + 64, &drank));
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[0], st));
 	k_min_keys<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, nctx, (uint32_t*)dk, (uint32_t*)dv);
 	size_t tmp_bytes = 0;
 	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)dk, (uint32_t*)dk2, (uint32_t*)dv,
@@ -138,8 +140,13 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* 
 				rc = fail(SYZSIG_EIO, "memset keep");
 			k_min_winners<<<grid_for(t->nslots(), 256), 256, 0, st>>>(t->slots, t->nslots(), order, d_keep);
 			k_count_u8<<<grid_for(nctx, 256), 256, 0, st>>>(d_keep, nctx, ctx->d_cnt);
+			if (ctx->timing && hipEventRecord(ctx->ev[1], st) != hipSuccess)
+				rc = fail(SYZSIG_EIO, "event record");
 			if (rc == SYZSIG_OK)
 				rc = counters_fetch(ctx);
+			float t = 0;
+			if (rc == SYZSIG_OK && ctx->timing && hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]) == hipSuccess)
+				ctx->last_ms = t;
 		}
 		syzsig_set_free(t);
 		SYZ_TRY(rc);

@@ -193,6 +193,12 @@ int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags)
 	return SYZSIG_OK;
 }
 
+double syzsig_ctx_last_ms(syzsig_ctx* ctx)
+{
+	SYZ_LOCK(ctx);
+	return ctx ? ctx->last_ms : 0;
+}
+
 int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable)
 {
 	SYZ_LOCK(ctx);

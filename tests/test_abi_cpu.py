@@ -15,7 +15,7 @@ HEADER = os.path.join(ROOT, "include", "syzsig.h")
 
 def declared():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|uint64_t|const char\*|void\*)\s+\**(syzsig_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|double|uint64_t|const char\*|void\*)\s+\**(syzsig_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_symbols_exported_and_bound():
