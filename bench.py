@@ -296,7 +296,7 @@ def main():
     nrec = int(cnt.to(torch.int64).sum().item())
     # ---- M0 (maxSignal before the batch): 10M elements per GPU
     if distributed:
-        from syzkaller_amd.dist import GpuShardOps, ShardedTriage, owner_of_torch
+        from syzkaller_amd.dist import SIGNAL_PRIO_LEVELS, GpuShardOps, ShardedTriage, owner_of_torch
 
         ge, gp = dev.synth_m0(cfg, 2048, a.m0 * world)
         own = owner_of_torch(ge, world) == rank
@@ -318,7 +318,11 @@ def main():
     b, bits, cnew = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
     if distributed:
         ops = GpuShardOps(dev)
+        # the prio levels are agreed once for the workload (signalPrio gives 0..3,
+        # fuzzer.go:513-521), not with a collective every step
         sharded = ShardedTriage(ops, ms, ns)
+        lv = sharded.levels(prio)
+        sharded.fixed_levels = sorted(set(lv) | set(SIGNAL_PRIO_LEVELS)) if len(set(lv) | set(SIGNAL_PRIO_LEVELS)) <= 4 else lv
 
     def step():
         ms.copy_from(pristine)

@@ -22,7 +22,7 @@ serial index carried in every record (see triage.hip).
 import torch
 import torch.distributed as dist
 
-__all__ = ["owner_of_torch", "ShardedTriage", "GpuShardOps"]
+__all__ = ["owner_of_torch", "ShardedTriage", "GpuShardOps", "SIGNAL_PRIO_LEVELS"]
 
 _M32 = 0xFFFFFFFF
 
@@ -54,6 +54,7 @@ class GpuShardOps:
         self.dev = dev
         self.aggregate = aggregate
         self._send = None
+        self._flags = None
         self.last_source_stats = {}
 
     def partition(self, batch, serial_base, levels, nshards):
@@ -72,7 +73,9 @@ class GpuShardOps:
         return send, send_pos, counts
 
     def triage_records(self, shard, new_signal, recs, levels):
-        flags = torch.empty(recs.numel(), dtype=torch.uint8, device=self.dev.dev)
+        if self._flags is None or self._flags.numel() < recs.numel():
+            self._flags = torch.empty(max(recs.numel(), 1) * 5 // 4 + 1, dtype=torch.uint8, device=self.dev.dev)
+        flags = self._flags[: recs.numel()]
         st = self.dev.triage_records(shard, new_signal, recs, levels, flags)
         return flags, st
 
@@ -86,8 +89,22 @@ class GpuShardOps:
         return new_bits, call_new
 
 
+# The prios signalPrio can produce (syz-fuzzer/fuzzer.go:513-521): a fixed
+# level set for batches of real executions, so no collective is needed to
+# agree on one (a superset of the prios present is exact: unused levels are
+# never compared).
+SIGNAL_PRIO_LEVELS = (0, 1, 2, 3)
+
+
 class ShardedTriage:
-    def __init__(self, ops, shard, new_signal, group=None, device=None):
+    """One rank's side of a sharded checkNewSignal step.
+
+    levels: the prio levels of every rank's calls, ascending as int8 (<= 4);
+    None = agree on them with an all_reduce each step.  Per step the only host
+    synchronisation is the exchange of the per-owner record counts (the split
+    sizes all_to_all_single needs); the receive and flag buffers are reused."""
+
+    def __init__(self, ops, shard, new_signal, group=None, device=None, levels=None):
         self.ops = ops
         self.shard = shard            # this rank's maxSignal shard
         self.new_signal = new_signal  # this rank's newSignal shard
@@ -95,15 +112,26 @@ class ShardedTriage:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = device
+        self.fixed_levels = sorted(levels) if levels is not None else None
+        self._recv = None
+        self._back = None
 
     def levels(self, call_prio):
         """Union of the prios of all ranks' calls, ascending as int8."""
+        if self.fixed_levels is not None:
+            return self.fixed_levels
         present = torch.zeros(256, dtype=torch.int32, device=call_prio.device)
         if call_prio.numel():
             present[call_prio.to(torch.int64)] = 1
         dist.all_reduce(present, op=dist.ReduceOp.MAX, group=self.group)
         vals = [v if v < 128 else v - 256 for v in torch.nonzero(present).flatten().tolist()]
         return sorted(vals)
+
+    @staticmethod
+    def _buffer(buf, n, dtype, dev):
+        if buf is None or buf.numel() < n or buf.device != dev:
+            buf = torch.empty(max(n, 1) + max(n, 1) // 4, dtype=dtype, device=dev)
+        return buf
 
     def step(self, batch, call_prio, serial_base):
         """batch = (Batch, new_bits, call_new) for this rank's calls."""
@@ -117,14 +145,17 @@ class ShardedTriage:
         cnt_out = torch.tensor(counts, dtype=torch.int64, device=dev)
         cnt_in = torch.empty_like(cnt_out)
         dist.all_to_all_single(cnt_in, cnt_out, group=self.group)
-        recv_counts = cnt_in.tolist()
-        recv = torch.empty(sum(recv_counts), dtype=torch.int64, device=dev)
+        recv_counts = cnt_in.tolist()  # the step's one host sync: split sizes
+        nrecv = sum(recv_counts)
+        self._recv = self._buffer(self._recv, nrecv, torch.int64, dev)
+        recv = self._recv[:nrecv]
         dist.all_to_all_single(recv, send, recv_counts, counts, group=self.group)
         flags, st = self.ops.triage_records(self.shard, self.new_signal, recv, levels)
-        back = torch.empty(send.numel(), dtype=torch.uint8, device=dev)
+        self._back = self._buffer(self._back, send.numel(), torch.uint8, dev)
+        back = self._back[: send.numel()]
         dist.all_to_all_single(back, flags, counts, recv_counts, group=self.group)
         new_bits, call_new = self.ops.unpartition(batch, token, back)
         st = dict(st)
         st["sent"] = int(send.numel())
-        st["received"] = int(recv.numel())
+        st["received"] = int(nrecv)
         return new_bits, call_new, st

@@ -1,0 +1,110 @@
+"""GPU, world_size 2 over gloo with both ranks on cuda:0: the sharded step of
+syzkaller_amd/dist.py driving the real kernels (GpuShardOps: the staircase
+aggregation of agg.hip, records-mode triage of triage.hip) -- the N>1 path of
+bench.py with gloo standing in for RCCL (RCCL refuses two ranks on one GPU).
+Two consecutive batches per rank (the shards carry their state), compared
+with sequential checkNewSignal (oracle) over the whole rank-major batch.
+
+Reference: syz-fuzzer/fuzzer.go:494-511; SURVEY.md 8(e).
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+NPROG, CPP, L, NM0, KNOWN = 24, 32, 2048, 100_000, 1024
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+    from syzkaller_amd.device import Device
+    from syzkaller_amd.dist import GpuShardOps, ShardedTriage, owner_of_torch
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dev = Device(0)
+    cfg = synth.synth_default(skew=1)
+    ge, gp = dev.synth_m0(cfg, KNOWN, NM0)
+    own = owner_of_torch(ge, world) == rank
+    ms = dev.deserialize(ge[own].contiguous(), gp[own].contiguous())
+    ns = S.Signal(None, dev.eng)
+    ops = GpuShardOps(dev)
+    sh = ShardedTriage(ops, ms, ns)  # first step: levels agreed by all_reduce
+    out = {}
+    for step in range(2):
+        # batch `step`, rank r's programs: a contiguous range of the global, rank-major order
+        p0 = (step * world + rank) * NPROG
+        cl = torch.full((NPROG * CPP,), L, dtype=torch.int32)
+        pcs, cs, cl, prio = dev.synth_traces(cfg, p0, NPROG, CPP, cl)
+        pidx = torch.arange(NPROG + 1, dtype=torch.int32, device=dev.dev) * CPP
+        sigs, cnt, _ = dev.edge_derive(pcs, cs, cl, pidx)
+        b, bits, cnew = dev.batch(sigs, cs, cnt, prio, want_bits=True)
+        bits, cnew, st = sh.step((b, bits, cnew), prio, rank * NPROG * CPP)
+        if step == 0:
+            sh.fixed_levels = sh.levels(prio)  # later steps: no collective
+        torch.cuda.synchronize()
+        out[f"bits{step}"] = bits.cpu().numpy().view(np.uint32)
+        out[f"cnew{step}"] = cnew.cpu().numpy()
+        out[f"sent{step}"] = np.array([st["sent"], st["received"]])
+    se = ms.Serialize()
+    out["ms_e"], out["ms_p"] = se.Elems, se.Prios
+    sn = ns.Serialize() if not ns.is_nil() else S.Serial()
+    out["ns_e"], out["ns_p"] = sn.Elems, sn.Prios
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gpu_sharded_step_gloo_two_ranks():
+    from syzkaller_amd import synth
+
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(worker, args=(world, _port(), d), nprocs=world, start_method="spawn")
+        res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
+    cfg = synth.synth_default(skew=1)
+    m0e, m0p = synth.m0(cfg, KNOWN, NM0)
+    oms = O.deserialize(m0e, m0p)
+    ons = O.OSig()
+    cl = synth.call_lengths(NPROG, CPP, L)
+    pidx = synth.prog_call_index(NPROG, CPP)
+    for step in range(2):
+        for r in range(world):  # serial order: batch by batch, rank-major inside a batch
+            pcs, cs, prio = synth.traces(cfg, (step * world + r) * NPROG, NPROG, CPP, cl)
+            sigs, cnt, _ = O.exec_batch(pcs, cs, cl, pidx)
+            ons, obits, ocnew = O.triage_batch_into(oms, sigs, cs, cnt, prio, ons)
+            np.testing.assert_array_equal(res[r][f"cnew{step}"], ocnew[: cnt.size])
+            np.testing.assert_array_equal(res[r][f"bits{step}"], obits[: (sigs.size + 31) // 32])
+    assert sum(int(x[f"sent{s}"][0]) for x in res for s in range(2)) == \
+        sum(int(x[f"sent{s}"][1]) for x in res for s in range(2))
+    ge = np.concatenate([x["ms_e"] for x in res])
+    gpr = np.concatenate([x["ms_p"] for x in res])
+    oe, op = oms.Serialize()
+    o1, o2 = np.argsort(ge), np.argsort(oe)
+    np.testing.assert_array_equal(ge[o1], oe[o2])
+    np.testing.assert_array_equal(gpr[o1], op[o2])
+    ne = np.concatenate([x["ns_e"] for x in res])
+    npr = np.concatenate([x["ns_p"] for x in res])
+    oe, op = ons.Serialize()
+    o1, o2 = np.argsort(ne), np.argsort(oe)
+    np.testing.assert_array_equal(ne[o1], oe[o2])
+    np.testing.assert_array_equal(npr[o1], op[o2])
