@@ -128,6 +128,33 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, const uint32
                         const int8_t* d_prios, uint64_t nctx, uint64_t hint_distinct, uint8_t* d_keep,
                         uint64_t* n_out);
 
+/* ---- syz-manager/manager.go:1027-1052 Manager.Poll, over a batch of polls ----
+ * Poll i (arrival order) comes from fuzzer poll_fuzzer[i] (< nfuzzers) with the
+ * Serial a.MaxSignal = elems/prios[poll_off[i] .. poll_off[i+1]) (Deserialize
+ * rules, signal.go:59-71: a later duplicate overwrites).  The result is the
+ * reference's sequential loop over the polls:
+ *   newMax := maxSignal.Diff(Deserialize(a.MaxSignal)); maxSignal.Merge(newMax);
+ *   every other fuzzer's newMaxSignal.Merge(newMax);
+ *   reply = the polling fuzzer's newMaxSignal, which becomes nil.
+ * new_max[g] = fuzzer g's newMaxSignal (NULL = nil): a polling fuzzer's set is
+ * freed (nil) and may be replaced by a new one.  replies[i] = poll i's
+ * r.MaxSignal as a set (NULL = empty Serial) for the caller to Serialize and
+ * free.  Host arrays (the RPC payloads). */
+int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_max, uint32_t nfuzzers,
+                              const uint32_t* poll_fuzzer, const uint64_t* poll_off, const uint32_t* elems,
+                              const int8_t* prios, uint32_t npolls, syzsig_set** replies);
+
+/* Minimize sharded by element (one process per GPU): shard `shard` of
+ * `nshards` takes only the entries whose element it owns (owner_of, as the
+ * sharded maxSignal) over the whole corpus description (same ctx_off order on
+ * every shard); d_keep[i] = 1 iff context i wins one of the shard's elements.
+ * The OR (max) of d_keep over the shards is syzsig_minimize_dev's d_keep:
+ * an element's winner depends on that element's entries only.  *n_out = the
+ * shard's count. */
+int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, const uint32_t* d_elems,
+                              const int8_t* d_prios, uint64_t nctx, uint32_t nshards, uint32_t shard,
+                              uint64_t hint_distinct, uint8_t* d_keep, uint64_t* n_out);
+
 /* ---- pkg/cover/cover.go:7-30: type Cover map[uint32]struct{} ----
  * A Cover is a syzsig_set whose entries all carry prio 0.  Merge(raw)
  * (cover.go:9-18) allocates a NULL *cov even when n == 0, then inserts every

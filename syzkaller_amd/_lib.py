@@ -83,12 +83,14 @@ SIGNATURES = {
     "syzsig_diff_raw": (c_int, [_P, _P, _P, c_uint64, c_uint8, _PP]),
     "syzsig_intersection": (c_int, [_P, _P, _P, _PP]),
     "syzsig_merge": (c_int, [_P, _PP, _P]),
+    "syzsig_manager_poll_batch": (c_int, [_P, _PP, _P, c_uint32, _P, _P, _P, _P, c_uint32, _P]),
     "syzsig_cover_merge": (c_int, [_P, _PP, _P, c_uint64]),
     "syzsig_cover_merge_dev": (c_int, [_P, _PP, _P, c_uint64]),
     "syzsig_triage_runs_dev": (c_int, [_P, _P, c_uint64, _P, _P, _P, ctypes.c_uint32, _P, _P, _P, _P, _P, _P, _P]),
     "syzsig_minimize_pred_dev": (c_int, [_P, _P, c_uint64, _P, _P, _P, ctypes.c_uint32, _P, _P, _P, _P, _P, _P]),
     "syzsig_minimize": (c_int, [_P, _P, _P, _P, c_uint64, c_uint64, _P, POINTER(c_uint64)]),
     "syzsig_minimize_dev": (c_int, [_P, _P, _P, _P, c_uint64, c_uint64, _P, POINTER(c_uint64)]),
+    "syzsig_minimize_shard_dev": (c_int, [_P, _P, _P, _P, c_uint64, c_uint32, c_uint32, c_uint64, _P, POINTER(c_uint64)]),
     "syzsig_check_new_signal": (c_int, [_P, _PP, _PP, _P, c_uint64, _P, _P, _P, c_uint32, _P,
                                         POINTER(c_uint32), _P]),
     "syzsig_triage_batch": (c_int, [_P, _P, _PP, POINTER(Batch), POINTER(BatchStats)]),

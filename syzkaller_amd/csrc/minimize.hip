@@ -32,11 +32,14 @@ __global__ void k_min_rank(const uint32_t* __restrict__ order, uint64_t n, uint3
 		rank_of[order[r]] = (uint32_t)r;
 }
 
-// one wave per context
+// one wave per context; with nshards > 1 only the entries whose element this
+// shard owns (syz::owner_of) -- the winner of an element depends on that
+// element's entries alone, so shards of the element space are independent
+// (Minimize sharded by element)
 __global__ __launch_bounds__(256) void k_min_cover(uint64_t* slots, uint64_t bmask, const uint64_t* __restrict__ off,
                                                    const uint32_t* __restrict__ elems, const int8_t* __restrict__ prios,
                                                    const uint32_t* __restrict__ rank_of, uint64_t n,
-                                                   unsigned long long* cnt)
+                                                   uint32_t nshards, uint32_t shard, unsigned long long* cnt)
 {
 	const uint32_t lane = lane_id();
 	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -46,6 +49,8 @@ __global__ __launch_bounds__(256) void k_min_cover(uint64_t* slots, uint64_t bma
 		const uint32_t low_rank = 0xFFFFFFu - rank_of[c];
 		for (uint64_t j = off[c] + lane; j < off[c + 1]; j += 64) {
 			const uint32_t e = elems[j];
+			if (nshards > 1 && owner_of(e, nshards) != shard)
+				continue;
 			const uint64_t v = ((uint64_t)e << 32) | ((uint64_t)prio_biased(prios[j]) << 24) | low_rank;
 			uint64_t old;
 			const int64_t s = tbl_find_or_insert(slots, bmask, e, v, old, maxp);
@@ -84,10 +89,13 @@ using namespace syz;
 
 extern "C" {
 
-int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
-                        uint64_t nctx, uint64_t hint_distinct, uint8_t* d_keep, uint64_t* n_out)
+int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
+                              uint64_t nctx, uint32_t nshards, uint32_t shard, uint64_t hint_distinct, uint8_t* d_keep,
+                              uint64_t* n_out)
 {
 	SYZ_LOCK(ctx);
+	if (nshards == 0 || shard >= nshards)
+		return fail(SYZSIG_EINVAL, "minimize_shard: shard must be < nshards");
 	if (!ctx || !n_out || (nctx && (!d_off || !d_keep)))
 		return fail(SYZSIG_EINVAL, "minimize: NULL argument");
 	*n_out = 0;
@@ -126,7 +134,8 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* 
 		SYZ_TRY(set_alloc(ctx, nb, &t));
 		SYZ_TRY(counters_reset(ctx));
 		k_min_cover<<<grid_for(nctx * 64, 256, 4096), 256, 0, st>>>(t->slots, nb - 1, d_off, d_elems, d_prios,
-		                                                             (const uint32_t*)drank, nctx, ctx->d_cnt);
+		                                                             (const uint32_t*)drank, nctx, nshards, shard,
+		                                                             ctx->d_cnt);
 		hipError_t e = hipGetLastError();
 		int rc = e == hipSuccess ? counters_fetch(ctx) : hip_fail(e, "k_min_cover", __FILE__, __LINE__);
 		if (rc == SYZSIG_OK && ctx->h_cnt[kCntOverflow]) {
@@ -153,6 +162,12 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* 
 		*n_out = ctx->h_cnt[kCntAux];
 		return SYZSIG_OK;
 	}
+}
+
+int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
+                        uint64_t nctx, uint64_t hint_distinct, uint8_t* d_keep, uint64_t* n_out)
+{
+	return syzsig_minimize_shard_dev(ctx, d_off, d_elems, d_prios, nctx, 1, 0, hint_distinct, d_keep, n_out);
 }
 
 int syzsig_minimize(syzsig_ctx* ctx, const uint64_t* ctx_off, const uint32_t* elems, const int8_t* prios,

@@ -1,0 +1,337 @@
+// poll.hip -- syz-manager/manager.go:1027-1052 Manager.Poll over a batch of
+// polls, on device.
+//
+// Reference, per poll (in arrival order) of fuzzer f with a.MaxSignal s:
+//   newMax := mgr.maxSignal.Diff(s.Deserialize())
+//   if !newMax.Empty(): mgr.maxSignal.Merge(newMax); for every f1 != f: f1.newMaxSignal.Merge(newMax)
+//   if !f.newMaxSignal.Empty(): reply = f.newMaxSignal.Serialize(); f.newMaxSignal = nil
+//
+// Batch restatement.  For element e let p_i = Deserialize(s_i)[e] (the last
+// entry of e in s_i).  e is in newMax_i  <=>  p_i > max(M0[e], p_j for every
+// earlier poll j carrying e) -- the same strictly-greater running maximum as
+// checkNewSignal -- so newMax over the batch is a list of "events" (e, i, p)
+// whose prios rise with i for each e.  Fan-out: an event of poll i reaches
+// fuzzer g != f_i in g's next poll after i (its reply), or g's newMaxSignal
+// after the batch if g does not poll again; g's newMaxSignal from before the
+// batch goes into the reply of g's first poll.  Merge is max-prio, so every
+// target (a reply, or a fuzzer's final newMaxSignal) is the max-merge of the
+// (e, p) routed to it:
+//   k_poll_keys / radix sort   records by (e, poll), input order kept
+//   k_poll_walk                one thread per element: the events, and
+//                              maxSignal.Merge of the element's final max
+//   k_poll_fanout              (target, e, p) of every event for every other
+//                              fuzzer into one max-table keyed by (target, e)
+//   k_poll_pre                 pre-batch newMaxSignal of polling fuzzers
+//   k_poll_count / k_poll_scatter   the table into the target sets
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "internal.h"
+
+namespace syz {
+
+constexpr uint64_t kPollEmpty = ~0ull;
+constexpr uint32_t kPollMaxTargets = (1u << 24) - 2;  // targets < 2^24 - 1 keep a word != kPollEmpty
+
+// target-table word: target << 40 | elem << 8 | prio ^ 0x80 (key = the top 56 bits)
+__device__ __forceinline__ uint64_t poll_word(uint32_t t, uint32_t e, uint32_t pb)
+{
+	return ((uint64_t)t << 40) | ((uint64_t)e << 8) | pb;
+}
+
+__device__ __forceinline__ uint64_t poll_hash(uint64_t k)
+{
+	k ^= k >> 33;
+	k *= 0xff51afd7ed558ccdull;
+	k ^= k >> 33;
+	k *= 0xc4ceb9fe1a85ec53ull;
+	k ^= k >> 33;
+	return k;
+}
+
+// max-insert into the target table (C a power of two, sized >= 2 * entries)
+__device__ __forceinline__ void poll_put(uint64_t* T, uint64_t C, uint64_t w)
+{
+	const uint64_t key = w >> 8;
+	uint64_t h = poll_hash(key) & (C - 1);
+	for (uint64_t step = 0; step < C; step++) {
+		uint64_t s = T[h];
+		if (s == kPollEmpty) {
+			s = atomicCAS((unsigned long long*)&T[h], kPollEmpty, (unsigned long long)w);
+			if (s == kPollEmpty)
+				return;
+		}
+		if ((s >> 8) == key) {
+			if (s < w)
+				atomicMax((unsigned long long*)&T[h], (unsigned long long)w);
+			return;
+		}
+		h = (h + 1) & (C - 1);
+	}
+}
+
+__global__ void k_poll_keys(const uint32_t* __restrict__ elems, const uint32_t* __restrict__ rec_poll, uint64_t n,
+                            uint64_t* keys, uint32_t* vals)
+{
+	for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+		keys[r] = ((uint64_t)elems[r] << 32) | rec_poll[r];
+		vals[r] = (uint32_t)r;
+	}
+}
+
+// One thread per element run of the sorted records: M0[e], then the polls in
+// order, each poll's last entry of e (Deserialize: a later duplicate wins).
+__global__ void k_poll_walk(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint64_t n,
+                            const int8_t* __restrict__ prios, uint64_t* ms, uint64_t ms_bmask, uint64_t* ev,
+                            unsigned long long* nev, unsigned long long* ctr)
+{
+	uint64_t ins = 0, ovf = 0, changed = 0;
+	for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+		const uint32_t e = (uint32_t)(sk[r] >> 32);
+		if (r > 0 && (uint32_t)(sk[r - 1] >> 32) == e)
+			continue;  // not the head of e's run
+		uint64_t v = 0;
+		int m = -1000;  // absent: below every prio (signal.go:79-81)
+		if (tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v))
+			m = slot_prio(v);
+		const int m0 = m;
+		for (uint64_t q = r; q < n && (uint32_t)(sk[q] >> 32) == e; q++) {
+			if (q + 1 < n && sk[q + 1] == sk[q])
+				continue;  // an earlier duplicate inside one Serial
+			const int p = prios[sv[q]];
+			if (p > m) {
+				ev[atomicAdd(nev, 1ull)] = ((uint64_t)e << 32) | ((sk[q] & 0xFFFFFFull) << 8) | prio_biased((int8_t)p);
+				m = p;
+			}
+		}
+		if (m > m0) {
+			const int rr = tbl_merge(ms, ms_bmask, e, (int8_t)m);
+			ins += rr == 1;
+			ovf += rr < 0;
+			changed++;
+		}
+	}
+	block_count(&ctr[kCntInserted], ins);
+	block_count(&ctr[kCntOverflow], ovf);
+	block_count(&ctr[kCntChanged], changed);
+}
+
+// every event of poll i, for every fuzzer g != f_i: target next_target[i * F + g]
+__global__ void k_poll_fanout(const uint64_t* __restrict__ ev, const unsigned long long* __restrict__ nev,
+                              const uint32_t* __restrict__ poll_fuzzer, const uint32_t* __restrict__ next_target,
+                              uint32_t F, uint64_t* T, uint64_t C)
+{
+	const uint64_t n = *nev * F;
+	for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < n; x += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t w = ev[x / F];
+		const uint32_t g = (uint32_t)(x % F), i = (uint32_t)(w >> 8) & 0xFFFFFF;
+		if (poll_fuzzer[i] == g)
+			continue;
+		poll_put(T, C, poll_word(next_target[(uint64_t)i * F + g], (uint32_t)(w >> 32), (uint32_t)w & 0xFF));
+	}
+}
+
+// a polling fuzzer's newMaxSignal from before the batch -> its first reply
+__global__ void k_poll_pre(const uint64_t* __restrict__ slots, uint64_t nslots, uint32_t target, uint64_t* T,
+                           uint64_t C)
+{
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nslots;
+	     i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t s = slots[i];
+		if (slot_live(s))
+			poll_put(T, C, poll_word(target, slot_key(s), (uint32_t)s & 0xFF));
+	}
+}
+
+__global__ void k_poll_count(const uint64_t* __restrict__ T, uint64_t C, unsigned int* tcount)
+{
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < C; i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t w = T[i];
+		if (w != kPollEmpty)
+			atomicAdd(&tcount[w >> 40], 1u);
+	}
+}
+
+struct PollTarget {
+	uint64_t* slots;
+	uint64_t bmask;
+};
+
+__global__ void k_poll_scatter(const uint64_t* __restrict__ T, uint64_t C, const PollTarget* __restrict__ tg,
+                               unsigned int* tins, unsigned long long* ctr)
+{
+	uint64_t ovf = 0;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < C; i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t w = T[i];
+		if (w == kPollEmpty)
+			continue;
+		const uint32_t t = (uint32_t)(w >> 40);
+		const int r = tbl_merge(tg[t].slots, tg[t].bmask, (uint32_t)(w >> 8), (int8_t)((uint8_t)w ^ 0x80u));
+		if (r == 1)
+			atomicAdd(&tins[t], 1u);
+		ovf += r < 0;
+	}
+	block_count(&ctr[kCntOverflow], ovf);
+}
+
+static uint64_t pow2_ge(uint64_t x)
+{
+	uint64_t p = 1;
+	while (p < x)
+		p <<= 1;
+	return p;
+}
+
+}  // namespace syz
+
+using namespace syz;
+
+extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_max,
+                                         uint32_t nfuzzers, const uint32_t* poll_fuzzer, const uint64_t* poll_off,
+                                         const uint32_t* elems, const int8_t* prios, uint32_t npolls,
+                                         syzsig_set** replies)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !max_signal || (nfuzzers && !new_max) || (npolls && (!poll_fuzzer || !poll_off || !replies)))
+		return fail(SYZSIG_EINVAL, "manager_poll_batch: NULL argument");
+	if ((uint64_t)npolls + nfuzzers > kPollMaxTargets)
+		return fail(SYZSIG_ERANGE, "manager_poll_batch: too many polls + fuzzers");
+	for (uint32_t i = 0; i < npolls; i++) {
+		replies[i] = nullptr;
+		if (poll_fuzzer[i] >= nfuzzers || poll_off[i + 1] < poll_off[i])
+			return fail(SYZSIG_EINVAL, "manager_poll_batch: bad poll_fuzzer or poll_off");
+	}
+	if (npolls == 0)
+		return SYZSIG_OK;
+	const uint64_t n = poll_off[npolls] - poll_off[0];
+	if (n && (!elems || !prios))
+		return fail(SYZSIG_EINVAL, "manager_poll_batch: NULL Serial arrays");
+	const uint32_t F = nfuzzers, K = npolls;
+	const hipStream_t s = ctx->stream;
+	// next target of (poll i, fuzzer g): g's next poll after i, else K + g (its final newMaxSignal)
+	std::vector<uint32_t> next((uint64_t)K * F), rec_poll(n), last(F);
+	for (uint32_t g = 0; g < F; g++)
+		last[g] = K + g;
+	for (uint32_t i = K; i-- > 0;) {
+		std::copy(last.begin(), last.end(), next.begin() + (uint64_t)i * F);
+		last[poll_fuzzer[i]] = i;
+	}
+	for (uint32_t i = 0; i < K; i++)
+		for (uint64_t r = poll_off[i]; r < poll_off[i + 1]; r++)
+			rec_poll[r - poll_off[0]] = i;
+	const bool fresh_ms = !*max_signal;  // Merge allocates a nil maxSignal only for a non-empty newMax
+	if (fresh_ms)
+		SYZ_TRY(syzsig_set_make(ctx, n, max_signal));
+	syzsig_set* ms = *max_signal;
+	SYZ_TRY(set_reserve(ms, n));
+	// uploads and scratch: records, sorted records, events, the target table
+	void *de, *dp, *drp, *dk, *dv, *dk2, *dv2, *dev, *dnext, *dtmp = nullptr;
+	SYZ_TRY(ws_get(ctx, 40, n * 4 + 64, &de));
+	SYZ_TRY(ws_get(ctx, 41, n + 64, &dp));
+	SYZ_TRY(ws_get(ctx, 42, n * 4 + 64, &drp));
+	SYZ_TRY(ws_get(ctx, 43, n * 24 + 64, &dk));
+	dk2 = (uint64_t*)dk + n;
+	dv = (uint64_t*)dk2 + n;
+	dv2 = (uint32_t*)dv + n;
+	SYZ_TRY(ws_get(ctx, 44, n * 8 + ((uint64_t)K * F + K) * 4 + 64, &dev));
+	dnext = (uint64_t*)dev + n;
+	uint32_t* dpf = (uint32_t*)dnext + (uint64_t)K * F;
+	if (n) {
+		SYZ_HIP(hipMemcpyAsync(de, elems + poll_off[0], n * 4, hipMemcpyHostToDevice, s));
+		SYZ_HIP(hipMemcpyAsync(dp, prios + poll_off[0], n, hipMemcpyHostToDevice, s));
+		SYZ_HIP(hipMemcpyAsync(drp, rec_poll.data(), n * 4, hipMemcpyHostToDevice, s));
+	}
+	if ((uint64_t)K * F)
+		SYZ_HIP(hipMemcpyAsync(dnext, next.data(), (uint64_t)K * F * 4, hipMemcpyHostToDevice, s));
+	SYZ_HIP(hipMemcpyAsync(dpf, poll_fuzzer, (uint64_t)K * 4, hipMemcpyHostToDevice, s));
+	SYZ_TRY(counters_reset(ctx));
+	unsigned long long* nev = &ctx->d_cnt[kCntAux];
+	if (n) {
+		k_poll_keys<<<grid_for(n, 256), 256, 0, s>>>((const uint32_t*)de, (const uint32_t*)drp, n, (uint64_t*)dk,
+		                                             (uint32_t*)dv);
+		size_t tmp_bytes = 0;
+		SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint64_t*)dk, (uint64_t*)dk2, (uint32_t*)dv,
+		                                           (uint32_t*)dv2, (int)n, 0, 64, s));
+		SYZ_TRY(ws_get(ctx, 45, tmp_bytes + 64, &dtmp));
+		SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, (uint64_t*)dk, (uint64_t*)dk2, (uint32_t*)dv,
+		                                           (uint32_t*)dv2, (int)n, 0, 64, s));
+		k_poll_walk<<<grid_for(n, 256), 256, 0, s>>>((const uint64_t*)dk2, (const uint32_t*)dv2, n,
+		                                             (const int8_t*)dp, ms->slots, ms->nbuckets - 1, (uint64_t*)dev,
+		                                             nev, ctx->d_cnt);
+		SYZ_HIP(hipGetLastError());
+	}
+	SYZ_TRY(counters_fetch(ctx));
+	if (ctx->h_cnt[kCntOverflow])
+		return fail(SYZSIG_EIO, "manager_poll_batch: maxSignal overflow after reserve (internal error)");
+	ms->len += ctx->h_cnt[kCntInserted];
+	const uint64_t E = ctx->h_cnt[kCntAux];
+	if (fresh_ms && !E) {
+		syzsig_set_free(ms);
+		*max_signal = nullptr;
+	}
+	// the target table: every event for every other fuzzer + pre-batch sets of polling fuzzers
+	uint64_t entries = E * (F ? F - 1 : 0);
+	for (uint32_t g = 0; g < F; g++)
+		if (last[g] < K)
+			entries += syzsig_len(new_max[g]);
+	const uint64_t C = pow2_ge(std::max<uint64_t>(2 * entries, 1024));
+	void *dT, *dtc;
+	SYZ_TRY(ws_get(ctx, 46, C * 8 + 64, &dT));
+	SYZ_TRY(ws_get(ctx, 47, ((uint64_t)K + F) * 8 + 64, &dtc));
+	unsigned int* tcount = (unsigned int*)dtc;
+	unsigned int* tins = tcount + K + F;
+	SYZ_HIP(hipMemsetAsync(dT, 0xff, C * 8, s));
+	SYZ_HIP(hipMemsetAsync(dtc, 0, ((uint64_t)K + F) * 8, s));
+	if (E && F > 1)
+		k_poll_fanout<<<grid_for(E * F, 256, 8192), 256, 0, s>>>((const uint64_t*)dev, nev, dpf,
+		                                                         (const uint32_t*)dnext, F, (uint64_t*)dT, C);
+	for (uint32_t g = 0; g < F; g++)
+		if (last[g] < K && syzsig_len(new_max[g]))
+			k_poll_pre<<<grid_for(new_max[g]->nslots(), 256), 256, 0, s>>>(new_max[g]->slots, new_max[g]->nslots(),
+			                                                               last[g], (uint64_t*)dT, C);
+	k_poll_count<<<grid_for(C, 256, 8192), 256, 0, s>>>((const uint64_t*)dT, C, tcount);
+	SYZ_HIP(hipGetLastError());
+	std::vector<unsigned int> hc((uint64_t)K + F);
+	SYZ_HIP(hipMemcpyAsync(hc.data(), tcount, ((uint64_t)K + F) * 4, hipMemcpyDeviceToHost, s));
+	SYZ_HIP(hipStreamSynchronize(s));
+	// the polling fuzzers' newMaxSignal is nil after their poll (manager.go:1049-1052)
+	for (uint32_t g = 0; g < F; g++) {
+		if (last[g] < K && new_max[g]) {
+			syzsig_set_free(new_max[g]);
+			new_max[g] = nullptr;
+		}
+	}
+	// target sets: the replies, then every fuzzer's newMaxSignal after the batch
+	std::vector<PollTarget> tg((uint64_t)K + F, PollTarget{nullptr, 0});
+	for (uint64_t t = 0; t < (uint64_t)K + F; t++) {
+		if (!hc[t])
+			continue;
+		syzsig_set** sp = t < K ? &replies[t] : &new_max[t - K];
+		if (!*sp)
+			SYZ_TRY(syzsig_set_make(ctx, hc[t], sp));
+		else
+			SYZ_TRY(set_reserve(*sp, hc[t]));
+		tg[t] = PollTarget{(*sp)->slots, (*sp)->nbuckets - 1};
+	}
+	void* dtg;
+	SYZ_TRY(ws_get(ctx, 39, ((uint64_t)K + F) * sizeof(PollTarget) + 64, &dtg));
+	SYZ_HIP(hipMemcpyAsync(dtg, tg.data(), ((uint64_t)K + F) * sizeof(PollTarget), hipMemcpyHostToDevice, s));
+	SYZ_TRY(counters_reset(ctx));
+	k_poll_scatter<<<grid_for(C, 256, 8192), 256, 0, s>>>((const uint64_t*)dT, C, (const PollTarget*)dtg, tins,
+	                                                      ctx->d_cnt);
+	SYZ_HIP(hipGetLastError());
+	std::vector<unsigned int> hi((uint64_t)K + F);
+	SYZ_HIP(hipMemcpyAsync(hi.data(), tins, ((uint64_t)K + F) * 4, hipMemcpyDeviceToHost, s));
+	SYZ_TRY(counters_fetch(ctx));  // (synchronizes: hi and tg are consumed)
+	if (ctx->h_cnt[kCntOverflow])
+		return fail(SYZSIG_EIO, "manager_poll_batch: target overflow after reserve (internal error)");
+	for (uint64_t t = 0; t < (uint64_t)K + F; t++) {
+		if (!hc[t])
+			continue;
+		syzsig_set* st = t < K ? replies[t] : new_max[t - K];
+		st->len += hi[t];
+	}
+	return SYZSIG_OK;
+}

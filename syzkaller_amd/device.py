@@ -190,6 +190,18 @@ class Device:
                                          int(hint_distinct), _p(keep), ctypes.byref(cnt)))
         return keep, int(cnt.value)
 
+    def minimize_shard(self, ctx_off, elems, prios, nshards, shard, hint_distinct=0):
+        """Minimize over the elements this shard owns (owner_of); OR the keep
+        arrays of all shards for the corpus result (see dist.sharded_minimize)."""
+        self._check_dev(ctx_off, elems, prios)
+        n = ctx_off.numel() - 1
+        keep = torch.empty(max(n, 0), dtype=torch.uint8, device=self.dev)
+        cnt = ctypes.c_uint64()
+        check(self.L.syzsig_minimize_shard_dev(self.eng.h, _p(ctx_off), _p(elems), _p(prios), max(n, 0),
+                                               int(nshards), int(shard), int(hint_distinct), _p(keep),
+                                               ctypes.byref(cnt)))
+        return keep, int(cnt.value)
+
     # ---------------------------------------------------------------- sharding
     def shard_partition(self, b, serial_base, levels, nshards, send, send_pos):
         lv = (ctypes.c_int8 * len(levels))(*levels)

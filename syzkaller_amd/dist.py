@@ -22,7 +22,7 @@ serial index carried in every record (see triage.hip).
 import torch
 import torch.distributed as dist
 
-__all__ = ["owner_of_torch", "ShardedTriage", "GpuShardOps", "SIGNAL_PRIO_LEVELS"]
+__all__ = ["owner_of_torch", "ShardedTriage", "GpuShardOps", "SIGNAL_PRIO_LEVELS", "sharded_minimize"]
 
 _M32 = 0xFFFFFFFF
 
@@ -159,3 +159,16 @@ class ShardedTriage:
         st["sent"] = int(send.numel())
         st["received"] = int(nrecv)
         return new_bits, call_new, st
+
+
+def sharded_minimize(minimize_shard, ctx_off, elems, prios, group=None, hint_distinct=0):
+    """signal.Minimize (pkg/signal/signal.go:138-166) sharded by element over
+    the ranks of `group`: every rank holds the corpus
+    description; rank r resolves the winners of the elements it owns
+    (minimize_shard(ctx_off, elems, prios, world, r, hint) -> (keep u8[nctx], n),
+    e.g. Device.minimize_shard) and the per-context keep flags are OR-reduced
+    (all_reduce MAX of 0/1 bytes).  Returns (keep, survivors)."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    keep, _ = minimize_shard(ctx_off, elems, prios, world, rank, hint_distinct // max(world, 1))
+    dist.all_reduce(keep, op=dist.ReduceOp.MAX, group=group)
+    return keep, int(keep.to(torch.int64).sum().item())

@@ -21,7 +21,7 @@ from . import _lib
 from ._lib import check
 
 __all__ = ["Engine", "engine", "Signal", "Cover", "Serial", "Context", "FromRaw", "Minimize", "signal_prio",
-           "check_new_signal"]
+           "check_new_signal", "manager_poll"]
 
 
 class Engine:
@@ -310,3 +310,36 @@ def check_new_signal(max_signal, new_signal, calls, eng=None, want_bits=False):
         new_signal._h = nh
     idx = [int(i) for i in out[: n.value]]
     return (idx, bits[: (sigs.size + 31) // 32]) if want_bits else idx
+
+
+def manager_poll(max_signal, new_max, polls, eng=None):
+    """syz-manager/manager.go:1027-1052 Manager.Poll for a batch of polls, in
+    order: polls = [(fuzzer index, Serial a.MaxSignal)], new_max = every
+    fuzzer's newMaxSignal (Signal objects, updated in place; a polling
+    fuzzer's becomes nil).  max_signal is merged (a nil one is allocated).
+    Returns each poll's reply r.MaxSignal as a Serial (empty if none)."""
+    eng = eng or max_signal._e
+    F, K = len(new_max), len(polls)
+    pf = np.array([int(f) for f, _ in polls], dtype=np.uint32)
+    lens = np.array([np.asarray(s.Elems).size for _, s in polls], dtype=np.uint64)
+    for _, s in polls:
+        if np.asarray(s.Elems).size != np.asarray(s.Prios).size:
+            raise _lib.CorruptedSerial(_lib.SYZSIG_ECORRUPT, "corrupted Serial")  # signal.go:60-62
+    off = np.zeros(K + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    elems = np.concatenate([np.asarray(s.Elems, np.uint32) for _, s in polls]) if off[-1] else np.empty(0, np.uint32)
+    prios = np.concatenate([np.asarray(s.Prios, np.int8) for _, s in polls]) if off[-1] else np.empty(0, np.int8)
+    nm = (ctypes.c_void_p * max(F, 1))(*[s.handle.value or 0 for s in new_max])
+    rep = (ctypes.c_void_p * max(K, 1))()
+    mh = ctypes.c_void_p(max_signal.handle.value or 0)
+    check(eng.L.syzsig_manager_poll_batch(eng.h, ctypes.byref(mh), nm, F, _ptr(pf), _ptr(off), _ptr(elems),
+                                          _ptr(prios), K, rep))
+    if mh.value and max_signal.is_nil():
+        max_signal._h = mh
+    for g, s in enumerate(new_max):
+        s._h = ctypes.c_void_p(nm[g]) if nm[g] else None  # the library freed or replaced polled sets
+    out = []
+    for i in range(K):
+        r = Signal(ctypes.c_void_p(rep[i]) if rep[i] else None, eng)
+        out.append(r.Serialize() if not r.is_nil() else Serial())
+    return out

@@ -181,3 +181,71 @@ def test_sharded_step_equals_sequential_checknewsignal(seed, stair):
     sent = sum(r["stats"]["sent"] for r in res)
     assert sent == sum(r["stats"]["received"] for r in res)
     assert sent < sigs.size if stair else sent == sigs.size
+
+
+# ---- Minimize sharded by element (dist.sharded_minimize) ----
+
+def _owner_np(e, n):
+    """syz::owner_of (csrc/common.h) over a u32 array."""
+    h = (np.asarray(e, np.uint64) * np.uint64(0x9E3779B1) + np.uint64(0x7F4A7C15)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    return ((h * np.uint64(n)) >> np.uint64(32)).astype(np.int64)
+
+
+def numpy_minimize_shard(off, elems, prios, nshards, shard):
+    """Restatement of one shard's part of signal.Minimize (signal.go:138-166):
+    contexts ordered by (Len desc, index asc); for every element this shard
+    owns the winner is the earliest context of the highest prio."""
+    n = off.size - 1
+    lens = np.diff(off.astype(np.int64))
+    order = np.lexsort((np.arange(n), -lens))
+    rank = np.empty(n, np.int64)
+    rank[order] = np.arange(n)
+    ctx = np.repeat(np.arange(n), lens)
+    own = _owner_np(elems, nshards) == shard
+    e, p, r = elems[own].astype(np.int64), prios[own].astype(np.int64), rank[ctx[own]]
+    keep = np.zeros(n, np.uint8)
+    if e.size:
+        o = np.lexsort((r, -p, e))
+        first = np.ones(o.size, bool)
+        first[1:] = e[o][1:] != e[o][:-1]
+        keep[order[r[o][first]]] = 1
+    return torch.from_numpy(keep), int(keep.sum())
+
+
+def _corpus(seed, n=300, U=2000):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 60, size=n)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    elems = np.concatenate([rng.choice(U, size=int(L), replace=False) for L in lens]).astype(np.uint32)
+    prios = rng.integers(0, 4, size=elems.size).astype(np.int8)
+    return off, elems, prios
+
+
+def minimize_worker(rank, world, port, outdir, seed):
+    from syzkaller_amd.dist import sharded_minimize
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    off, elems, prios = _corpus(seed)
+    keep, n = sharded_minimize(lambda o, e, p, w, r, h: numpy_minimize_shard(o, e, p, w, r), off, elems, prios)
+    json.dump({"keep": keep.tolist(), "n": n}, open(os.path.join(outdir, f"m{rank}.json"), "w"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_sharded_minimize_equals_minimize(seed):
+    from oracle import oracle as O
+
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(minimize_worker, args=(world, free_port(), d, seed), nprocs=world, start_method="spawn")
+        res = [json.load(open(os.path.join(d, f"m{r}.json"))) for r in range(world)]
+    off, elems, prios = _corpus(seed)
+    exp = O.minimize(off, elems, prios)
+    for r in res:  # every rank holds the reduced result
+        assert np.nonzero(np.array(r["keep"]))[0].tolist() == exp and r["n"] == len(exp)

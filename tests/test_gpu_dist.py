@@ -108,3 +108,47 @@ def test_gpu_sharded_step_gloo_two_ranks():
     o1, o2 = np.argsort(ne), np.argsort(oe)
     np.testing.assert_array_equal(ne[o1], oe[o2])
     np.testing.assert_array_equal(npr[o1], op[o2])
+
+
+def minimize_worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+
+    from syzkaller_amd.device import Device
+    from syzkaller_amd.dist import sharded_minimize
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dev = Device(0)
+    off, e, p = _min_corpus()
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).to(dev.dev)  # noqa: E731
+    keep, n = sharded_minimize(dev.minimize_shard, t(off, np.int64), t(e, np.int32), t(p, np.int8))
+    np.save(os.path.join(outdir, f"m{rank}.npy"), keep.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _min_corpus():
+    rng = np.random.default_rng(77)
+    lens = rng.geometric(1 / 200, size=5000)
+    off = np.zeros(lens.size + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    U = 1 << 16
+    base = rng.integers(0, U, size=lens.size)
+    stride = rng.integers(0, U // 2, size=lens.size) * 2 + 1
+    ctx = np.repeat(np.arange(lens.size), lens)
+    k = np.arange(int(off[-1])) - off[:-1].astype(np.int64)[ctx]
+    e = ((base[ctx] + k * stride[ctx]) & (U - 1)).astype(np.uint32)
+    p = rng.integers(0, 4, size=e.size).astype(np.int8)
+    return off, e, p
+
+
+def test_gpu_sharded_minimize_gloo_two_ranks():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(minimize_worker, args=(world, _port(), d), nprocs=world, start_method="spawn")
+        keeps = [np.load(os.path.join(d, f"m{r}.npy")) for r in range(world)]
+    off, e, p = _min_corpus()
+    exp = O.minimize(off, e, p)
+    for k in keeps:
+        assert np.nonzero(k)[0].tolist() == exp

@@ -174,3 +174,23 @@ def _owner(e, n):
         return h
     h = fmix((e * 0x9E3779B1 + 0x7F4A7C15) & 0xFFFFFFFF)
     return (h * n) >> 32
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_minimize_sharded_by_element_equals_unsharded(gpu, nshards):
+    """G element shards on one GPU (syzsig_minimize_shard_dev): the OR of
+    their keep flags equals unsharded Minimize and the oracle."""
+    rng = np.random.default_rng(40 + nshards)
+    off, e, p = corpus(rng, 3000, 120, 20000)
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).to(gpu.dev)  # noqa: E731
+    doff, de, dp = t(off, np.int64), t(e, np.int32), t(p, np.int8)
+    keep1, n1 = gpu.minimize(doff, de, dp)
+    acc = torch.zeros_like(keep1)
+    tot = 0
+    for g in range(nshards):
+        k, n = gpu.minimize_shard(doff, de, dp, nshards, g)
+        acc = torch.maximum(acc, k)
+        tot += n
+    assert torch.equal(acc, keep1)
+    assert tot >= n1
+    assert np.nonzero(acc.cpu().numpy())[0].tolist() == O.minimize(off, e, p)

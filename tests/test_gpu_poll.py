@@ -1,0 +1,55 @@
+"""GPU: the manager's Poll over a batch of polls (csrc/poll.hip,
+syzsig_manager_poll_batch) against the reference's sequential loop restated
+over the oracle's Signal ops (oracle.poll: syz-manager/manager.go:1027-1052)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _serial(rng, n, U, dup=True):
+    e = rng.integers(0, U, size=n).astype(np.uint32)  # duplicates inside a Serial: the later one wins
+    if not dup:
+        e = np.unique(e)
+    p = rng.integers(-3, 5, size=e.size).astype(np.int8)
+    return e, p
+
+
+@pytest.mark.parametrize("seed,F,K,U,n", [(0, 5, 40, 3000, 400), (1, 1, 8, 500, 100), (2, 16, 200, 50_000, 3000),
+                                          (3, 3, 30, 200, 50)])
+def test_poll_batch_vs_sequential_oracle(gpu, seed, F, K, U, n):
+    from syzkaller_amd import signal as S
+
+    rng = np.random.default_rng(seed)
+    m0 = _serial(rng, 4 * n, U, dup=False)
+    pre = [None if rng.random() < 0.3 else _serial(rng, int(rng.integers(0, n)), U, dup=False) for _ in range(F)]
+    polls = [(int(rng.integers(0, F)), _serial(rng, int(rng.integers(0, 2 * n)), U)) for _ in range(K)]
+    # device
+    ms = S.Serial(*m0).Deserialize(gpu.eng)
+    nm = [S.Serial(*p).Deserialize(gpu.eng) if p is not None else S.Signal(None, gpu.eng) for p in pre]
+    replies = S.manager_poll(ms, nm, [(f, S.Serial(e, p)) for f, (e, p) in polls], gpu.eng)
+    # oracle: one poll after the other
+    oms = O.deserialize(*m0)
+    onm = [O.deserialize(*p) if p is not None else O.OSig() for p in pre]
+    for i, (f, ser) in enumerate(polls):
+        re, rp = O.poll(oms, onm, f, ser)
+        got = dict(zip(replies[i].Elems.tolist(), replies[i].Prios.tolist()))
+        assert got == dict(zip(re.tolist(), rp.tolist())), f"reply {i}"
+    assert ms.to_dict() == oms.to_dict()
+    for g in range(F):
+        assert (nm[g].to_dict() if not nm[g].is_nil() else {}) == onm[g].to_dict(), f"fuzzer {g}"
+        assert nm[g].is_nil() == onm[g].is_nil() or onm[g].Len() == 0
+
+
+def test_poll_batch_empty_and_nil_max(gpu):
+    from syzkaller_amd import signal as S
+
+    ms = S.Signal(None, gpu.eng)
+    nm = [S.Signal(None, gpu.eng) for _ in range(3)]
+    rep = S.manager_poll(ms, nm, [(0, S.Serial()), (1, S.Serial([7, 8, 7], [1, 2, 0])), (0, S.Serial())], gpu.eng)
+    assert [r.Elems.size for r in rep] == [0, 0, 2]
+    assert dict(zip(rep[2].Elems.tolist(), rep[2].Prios.tolist())) == {7: 0, 8: 2}
+    assert ms.to_dict() == {7: 0, 8: 2}
+    assert nm[0].is_nil() and nm[1].is_nil() and nm[2].to_dict() == {7: 0, 8: 2}
