@@ -57,13 +57,9 @@ __device__ __forceinline__ void lds_barrier()
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// stamp s (epoch << kPosBits | kPosMask - position) was set by a position before pos this epoch
-template <uint32_t W>
-__device__ __forceinline__ bool stamp_earlier(uint32_t s, uint32_t epoch, uint32_t pos)
-{
-	using G = EdgeGeom<W>;
-	return (s >> G::kPosBits) == epoch && G::kPosMask - (s & G::kPosMask) < pos;
-}
+// A bin's stamp is the max of epoch << kPosBits | (kPosMask - position) over
+// this epoch's markers (older epochs compare lower): it was set by a position
+// before mine this epoch  <=>  stamp > my own v = epoch << kPosBits | (kPosMask - pos).
 
 template <uint32_t W>
 __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restrict__ pcs, uint64_t npc,
@@ -196,7 +192,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						}
 						lds_barrier();
 						const uint32_t s0 = stamp[b0], s1 = stamp[b1];
-						blocked = pending && (stamp_earlier<W>(s0, epoch, pos) || stamp_earlier<W>(s1, epoch, pos));
+						blocked = pending && (s0 > v || s1 > v);
 						mark_now = blocked && !marker;
 						marker = marker || mark_now;
 						if (!wg_any(mark_now))
