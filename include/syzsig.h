@@ -70,8 +70,11 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
 
 /* Test knobs that change the code path but never the results:
  * SYZSIG_DEBUG_FIN_DEFER = the batch finalize sends every element whose probe
- * sequence leaves its home bucket to the atomic (deferred) path. */
+ * sequence leaves its home bucket to the atomic (deferred) path;
+ * SYZSIG_DEBUG_MIN_ATOMIC = Minimize takes its per-entry atomicMax path instead
+ * of the aggregation path. */
 #define SYZSIG_DEBUG_FIN_DEFER 32u
+#define SYZSIG_DEBUG_MIN_ATOMIC 64u
 int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
 
 /* ---- pkg/signal/signal.go ---- */

@@ -17,6 +17,7 @@ SYZSIG_EINVAL = -22
 SYZSIG_ERANGE = -34
 SYZSIG_ECORRUPT = -74
 SYZSIG_DEBUG_FIN_DEFER = 32
+SYZSIG_DEBUG_MIN_ATOMIC = 64
 
 
 class SyzsigError(RuntimeError):

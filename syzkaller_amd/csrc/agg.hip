@@ -53,7 +53,7 @@ constexpr uint32_t kAggThreads = 1024;
 constexpr uint32_t kAggSlots = 7424;               // LDS slots per workgroup (+ 8 KB of first-sight queues)
 constexpr uint32_t kAggBuckets = kAggSlots / 4;    // 4-key buckets (one ds_read_b128 per probe)
 constexpr uint32_t kAggNoSlot = 0xFFFFFFFFu;
-constexpr uint32_t kAggRegion = kAggSlots;         // distinct-list region per partition
+static_assert(kAggRegion == kAggSlots, "distinct-list region per partition (internal.h)");
 constexpr uint32_t kAggLimit = kAggSlots * 4 / 5;  // distinct elements before a partition overflows
 constexpr double kAggTargetLoad = 0.4;             // partitions are sized for this LDS load
 constexpr uint32_t kAggEmpty = 0xFFFFFFFFu;        // empty key (LDS keys are residuals < 2^29)
@@ -81,8 +81,10 @@ __host__ __device__ __forceinline__ uint32_t fmix32_inv(uint32_t h)
 // Partition geometry of one run (see the header).
 struct AggGeom {
 	uint32_t pbits;  // P = 2^pbits partitions
+	uint32_t ibits;  // partitioning work items of 2^ibits calls (<= cbits): a chunk is 2^(cbits-ibits) items
 	__host__ __device__ uint32_t rbits() const { return 32 - pbits; }
 	__host__ __device__ uint32_t cbits() const { return pbits - 2; }
+	__host__ __device__ uint32_t items_per_chunk_log2() const { return cbits() - ibits; }
 	__host__ __device__ uint32_t part(uint32_t h) const { return h >> (32 - pbits); }
 	__host__ __device__ uint32_t meta(uint32_t level, uint64_t serial) const
 	{
@@ -182,14 +184,20 @@ struct CellGroup {
 };
 
 // ---------------------------------------------------------------- partitioning
-// Calls of the run [c0, c1) in chunks of 2^cbits; counts[chunk][p].
+// Calls of the run [c0, c1) in work items of 2^ibits; counts[item][p].  kShard:
+// only the records whose element shard x.shard of x.nshards owns (owner_of).
+template <bool kShard>
 __global__ __launch_bounds__(kAggThreads) void k_agg_count(const uint32_t* __restrict__ sigs,
                                                            const uint64_t* __restrict__ call_start,
                                                            const uint32_t* __restrict__ call_len, uint64_t c0,
-                                                           uint64_t c1, AggGeom g, uint32_t* counts)
+                                                           uint64_t c1, AggGeom g, AggSrc x, uint32_t* counts)
 {
 	__shared__ uint32_t h[kAggMaxParts];
-	const uint32_t P = 1u << g.pbits, cb = g.cbits();
+	auto add = [&](uint32_t e) {
+		if (!kShard || owner_of(e, x.nshards) == x.shard)
+			atomicAdd(&h[g.part(fmix32(e))], 1u);
+	};
+	const uint32_t P = 1u << g.pbits, cb = g.ibits;  // per work item of 2^ibits calls
 	const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = lane_id();
 	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << cb) - 1) >> cb;
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
@@ -204,13 +212,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_count(const uint32_t* __res
 			for (; j + 192 < len; j += 256) {
 				const uint32_t a = sigs[start + j], b = sigs[start + j + 64], d = sigs[start + j + 128],
 				               f = sigs[start + j + 192];
-				atomicAdd(&h[g.part(fmix32(a))], 1u);
-				atomicAdd(&h[g.part(fmix32(b))], 1u);
-				atomicAdd(&h[g.part(fmix32(d))], 1u);
-				atomicAdd(&h[g.part(fmix32(f))], 1u);
+				add(a);
+				add(b);
+				add(d);
+				add(f);
 			}
 			for (; j < len; j += 64)
-				atomicAdd(&h[g.part(fmix32(sigs[start + j]))], 1u);
+				add(sigs[start + j]);
 		}
 		__syncthreads();
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
@@ -244,23 +252,26 @@ __device__ __forceinline__ uint32_t block_excl_scan_1k(uint32_t v, uint32_t* out
 	return tot;
 }
 
-// block p: exclusive scan over chunks of counts[.][p] -> offs[.][p]
-// (chunk-major, for the scatter) and offsT[p][.] (partition-major, the
-// partition's total at [nchunks], for k_agg); totals[p]
-__global__ __launch_bounds__(1024) void k_agg_scan_chunks(const uint32_t* counts, uint64_t nchunks, uint32_t P,
-                                                          uint32_t* offs, uint32_t* offsT, uint64_t* totals)
+// block p: exclusive scan over work items of counts[.][p] -> offs[.][p]
+// (item-major, for the scatter) and, at every chunk's first item, offsT[p][.]
+// (partition-major by chunk, the partition's total at [nchunks], for k_agg);
+// totals[p].  An item is 2^ilog items of a chunk (ilog = 0: items are chunks).
+__global__ __launch_bounds__(1024) void k_agg_scan_chunks(const uint32_t* counts, uint64_t nitems, uint32_t ilog,
+                                                          uint32_t P, uint32_t* offs, uint32_t* offsT, uint64_t* totals)
 {
 	const uint32_t p = blockIdx.x;
+	const uint64_t nchunks = (nitems + (1ull << ilog) - 1) >> ilog;
 	uint32_t* ot = offsT + (uint64_t)p * (nchunks + 1);
 	uint64_t run = 0;
-	for (uint64_t b0 = 0; b0 < nchunks; b0 += blockDim.x) {
+	for (uint64_t b0 = 0; b0 < nitems; b0 += blockDim.x) {
 		const uint64_t b = b0 + threadIdx.x;
-		const uint32_t v = b < nchunks ? counts[b * P + p] : 0;
+		const uint32_t v = b < nitems ? counts[b * P + p] : 0;
 		uint32_t ex;
 		const uint32_t tot = block_excl_scan_1k(v, &ex);
-		if (b < nchunks) {
+		if (b < nitems) {
 			offs[b * P + p] = (uint32_t)(run + ex);
-			ot[b] = (uint32_t)(run + ex);
+			if ((b & ((1ull << ilog) - 1)) == 0)
+				ot[b >> ilog] = (uint32_t)(run + ex);
 		}
 		run += tot;
 	}
@@ -297,13 +308,17 @@ __global__ __launch_bounds__(1024) void k_agg_scan_totals(const uint64_t* totals
 // partition; the runs of one chunk's consecutive tiles continue each other.
 // The next tile's loads are issued before the write-out of the current one,
 // so HBM reads overlap the stores instead of following them.
+// kEntry (Minimize): the level comes from each record's own prio
+// (x.elem_prio, parallel to sigs) instead of its call's, and only the records
+// whose element shard x.shard owns are kept.
 constexpr uint32_t kScatChunkMax = 1u << (kAggMaxBits - 2);  // calls per chunk (cbits <= 9)
 
+template <bool kEntry>
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __restrict__ sigs,
                                                              const uint64_t* __restrict__ call_start,
                                                              const uint32_t* __restrict__ call_len,
                                                              const uint8_t* __restrict__ call_prio, LevelMap lm,
-                                                             uint64_t c0, uint64_t c1, AggGeom g,
+                                                             uint64_t c0, uint64_t c1, AggGeom g, AggSrc x,
                                                              const uint32_t* __restrict__ offs,
                                                              const uint64_t* __restrict__ rec_base, uint32_t* recs)
 {
@@ -316,14 +331,18 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 	__shared__ uint64_t c_start[kScatChunkMax];  // the chunk's calls
 	__shared__ uint32_t c_len[kScatChunkMax];
 	__shared__ uint16_t c_meta[kScatChunkMax];
-	__shared__ uint32_t tile_n;
-	const uint32_t P = 1u << g.pbits, cb = g.cbits();
+	__shared__ uint8_t s_lvl[kEntry ? 256 : 1];
+	const uint32_t P = 1u << g.pbits, cb = g.cbits(), ib = g.ibits;
+	if (kEntry) {
+		for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
+			s_lvl[i] = lm.lvl[i];
+	}
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << cb) - 1) >> cb;
+	const uint64_t ncalls = c1 - c0, nitems = (ncalls + (1ull << ib) - 1) >> ib;
 	const uint32_t per_t = (P + blockDim.x - 1) / blockDim.x;
-	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-		const uint64_t cbeg = ch << cb;
-		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << cb);
+	for (uint64_t ch = blockIdx.x; ch < nitems; ch += gridDim.x) {  // ch: work item (of 2^ibits calls)
+		const uint64_t cbeg = ch << ib;
+		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
 			cur[i] = rec_base[i] + offs[ch * P + i];
 			hist[i] = 0;
@@ -332,10 +351,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 			const uint64_t c = c0 + cbeg + i;
 			c_start[i] = call_start[c];
 			c_len[i] = call_len[c];
-			c_meta[i] = (uint16_t)g.meta(lm.lvl[call_prio[c]], cbeg + i);
+			c_meta[i] = (uint16_t)g.meta(kEntry ? 0 : lm.lvl[call_prio[c]], cbeg + i);
 		}
-		if (threadIdx.x == 0)
-			tile_n = 0;
 		__syncthreads();
 		// this wave's walk: local call wc (then +kWaves), offset wo inside it
 		uint32_t wc = w, wo = 0;
@@ -343,6 +360,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 		// (calls hold < 2^24 records, batch validation); the wave's j-th call
 		// is local call w + j * kWaves (j < 2^cbits / kWaves <= 32).
 		uint32_t ev[kPer], loc[kPer];
+		int8_t pv[kEntry ? kPer : 1];
 		// issue the loads of this wave's next quota; returns how many records it has
 		auto fetch = [&]() -> uint32_t {
 			uint32_t q = 0;
@@ -368,28 +386,35 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 			}
 			if (q) {
 #pragma unroll
-				for (uint32_t u = 0; u < kPer; u++)
-					ev[u] = __builtin_nontemporal_load(&sigs[c_start[w + (loc[u] >> 24) * kWaves] + (loc[u] & 0xFFFFFFu)]);
+				for (uint32_t u = 0; u < kPer; u++) {
+					const uint64_t a = c_start[w + (loc[u] >> 24) * kWaves] + (loc[u] & 0xFFFFFFu);
+					ev[u] = __builtin_nontemporal_load(&sigs[a]);
+					if (kEntry)
+						pv[kEntry ? u : 0] = __builtin_nontemporal_load(&x.elem_prio[a]);
+				}
 			}
 			return q;
 		};
 		uint32_t n = fetch();
 		for (;;) {
-			// stage: partition and rank of every record of the tile
-			if (lane == 0 && n)
-				atomicAdd(&tile_n, n);
+			// stage: partition and rank of every record of the tile (loc = ~0: not kept)
 #pragma unroll
 			for (uint32_t u = 0; u < kPer; u++) {
 				const uint32_t i = u * 64 + lane;
-				if (i < n) {
+				const bool keep = i < n && (!kEntry || x.nshards == 1 || owner_of(ev[u], x.nshards) == x.shard);
+				if (keep) {
 					const uint32_t h = fmix32(ev[u]), p = g.part(h);
 					const uint32_t r = atomicAdd(&hist[p], 1u);
-					ev[u] = g.rec(h, c_meta[w + (loc[u] >> 24) * kWaves]);
+					uint32_t meta = c_meta[w + (loc[u] >> 24) * kWaves];
+					if (kEntry)
+						meta |= (uint32_t)s_lvl[(uint8_t)pv[kEntry ? u : 0]] << cb;
+					ev[u] = g.rec(h, meta);
 					loc[u] = p | (r << 16);
+				} else {
+					loc[u] = ~0u;
 				}
 			}
 			__syncthreads();
-			const uint32_t nt = tile_n;
 			// exclusive scan of hist; pos[p] = the partition's first sorted position
 			uint32_t hsum = 0;
 			for (uint32_t q = 0; q < per_t; q++) {
@@ -397,7 +422,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 				hsum += i < P ? hist[i] : 0;
 			}
 			uint32_t ex;
-			block_excl_scan_1k(hsum, &ex);
+			const uint32_t nt = block_excl_scan_1k(hsum, &ex);  // records kept in the tile
 			for (uint32_t q = 0; q < per_t; q++) {
 				const uint32_t i = threadIdx.x * per_t + q;
 				if (i < P) {
@@ -409,8 +434,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 			__syncthreads();
 #pragma unroll
 			for (uint32_t u = 0; u < kPer; u++) {
-				const uint32_t i = u * 64 + lane;
-				if (i < n) {
+				if (loc[u] != ~0u) {
 					const uint32_t p = loc[u] & 0xFFFFu, d = pos[p] + (loc[u] >> 16);
 					t_rec[d] = ev[u];
 					t_part[d] = (uint16_t)p;
@@ -427,8 +451,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 				cur[i] += pos[i] + hist[i];  // advance by the run
 				hist[i] = 0;
 			}
-			if (threadIdx.x == 0)
-				tile_n = 0;
 			if (!__syncthreads_or(n != 0))
 				break;
 		}
@@ -1272,17 +1294,18 @@ static uint64_t pow2_at_least(uint64_t x)
 	return p;
 }
 
-static AggGeom agg_geom_for(syzsig_ctx* ctx, uint64_t nrec)
+static AggGeom agg_geom_for(syzsig_ctx* ctx, uint64_t nrec, double distinct_hint)
 {
 	AggGeom g;
 	if (ctx->agg_parts) {
 		g.pbits = 31 - __builtin_clz(ctx->agg_parts);  // validated power of two in [8, 2048]
 		return g;
 	}
-	// expected distinct elements: the ratio seen on the previous large batch
-	// (1/32 before the first); big runs keep >= 256 partitions (one per CU)
+	// expected distinct elements: the caller's hint, else the ratio seen on the
+	// previous large batch (1/32 before the first); big runs keep >= 256
+	// partitions (one per CU)
 	const double ratio = ctx->agg_distinct_ratio > 0 ? ctx->agg_distinct_ratio : 1.0 / 32;
-	const double d = ratio * (double)nrec;
+	const double d = distinct_hint > 0 ? distinct_hint : ratio * (double)nrec;
 	uint32_t pb = nrec >= (1ull << 24) ? 8 : kAggMinBits;
 	while (pb < kAggMaxBits && d > kAggTargetLoad * kAggSlots * (double)(1u << pb))
 		pb++;
@@ -1294,29 +1317,47 @@ static AggGeom agg_geom_for(syzsig_ctx* ctx, uint64_t nrec)
 // [c0, c1) with level map lm: every distinct element of the run with its level
 // firsts (run serials), in regions of kAggRegion entries.
 int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const LevelMap& lm,
-                  uint64_t run_recs, syzsig_batch_stats* st, AggOut* out)
+                  uint64_t run_recs, syzsig_batch_stats* st, AggOut* out, const AggSrc* xp)
 {
-	const AggGeom g = agg_geom_for(ctx, run_recs);
+	const AggSrc x = xp ? *xp : AggSrc{nullptr, 1, 0, 0};
+	const bool entry = xp != nullptr;
+	AggGeom g = agg_geom_for(ctx, run_recs, x.distinct_hint);
 	const uint32_t P = 1u << g.pbits;
 	const uint64_t nchunks = (c1 - c0 + (1ull << g.cbits()) - 1) >> g.cbits();
+	// Work items of the count/scatter: whole chunks for a batch (its calls are
+	// alike), smaller ones for Minimize, whose calls (contexts in Len-desc
+	// order) make the first chunks far heavier than the last: >= ~2048 items.
+	g.ibits = g.cbits();
+	if (entry)
+		while (g.ibits > 0 && ((c1 - c0) >> g.ibits) < 2048)
+			g.ibits--;
+	const uint32_t ilog = g.items_per_chunk_log2();
+	const uint64_t nitems = (c1 - c0 + (1ull << g.ibits) - 1) >> g.ibits;
 	void *recs, *cm, *pm, *de, *df, *dc;
 	SYZ_TRY(ws_get(ctx, 16, run_recs * 4 + 64, &recs));
-	SYZ_TRY(ws_get(ctx, 17, (2 * nchunks * P + (uint64_t)P * (nchunks + 1)) * 4 + 64, &cm));
+	SYZ_TRY(ws_get(ctx, 17, (2 * nitems * P + (uint64_t)P * (nchunks + 1)) * 4 + 64, &cm));
 	SYZ_TRY(ws_get(ctx, 18, (kAggMaxParts + 1) * 8 * 2, &pm));
 	uint32_t* counts = (uint32_t*)cm;
-	uint32_t* offs = counts + nchunks * P;
-	uint32_t* offsT = offs + nchunks * P;
+	uint32_t* offs = counts + nitems * P;
+	uint32_t* offsT = offs + nitems * P;
 	uint64_t* totals = (uint64_t*)pm;
 	uint64_t* rec_base = totals + kAggMaxParts + 1;
 	const hipStream_t s = ctx->stream;
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
-	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
-	k_agg_count<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1, g, counts);
-	k_agg_scan_chunks<<<P, 1024, 0, s>>>(counts, nchunks, P, offs, offsT, totals);
+	const int pg = (int)std::min<uint64_t>(nitems, 2048);
+	if (x.nshards > 1)
+		k_agg_count<true><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1, g, x, counts);
+	else
+		k_agg_count<false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1, g, x, counts);
+	k_agg_scan_chunks<<<P, 1024, 0, s>>>(counts, nitems, ilog, P, offs, offsT, totals);
 	k_agg_scan_totals<<<1, 1024, 0, s>>>(totals, P, rec_base);
-	k_agg_scatter<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, g, offs,
-	                                         rec_base, (uint32_t*)recs);
+	if (entry)
+		k_agg_scatter<true><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1,
+		                                               g, x, offs, rec_base, (uint32_t*)recs);
+	else
+		k_agg_scatter<false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1,
+		                                                g, x, offs, rec_base, (uint32_t*)recs);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
@@ -1421,7 +1462,8 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	st->distinct += D;
 	st->parts = P;
 	st->survivors += D;
-	ctx->agg_distinct_ratio = run_recs ? (double)D / (double)run_recs : 0;
+	if (!entry)
+		ctx->agg_distinct_ratio = run_recs ? (double)D / (double)run_recs : 0;
 	out->dist_e = (const uint32_t*)dist_e;
 	out->dist_f = (const uint4*)dist_f;
 	out->cnt = (const uint32_t*)dc;

@@ -156,6 +156,7 @@ constexpr uint32_t kSerialMask = 0xFFFFFF;  // 24-bit serial index inside a run
 int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm);
 
 // aggregation path (agg.hip)
+constexpr uint32_t kAggRegion = 7424;  // distinct-list region per partition (= LDS slots of k_agg)
 struct AggOut {
 	const uint32_t* dist_e;  // distinct elements; region r at [r * kAggRegion, + cnt[r])
 	const uint4* dist_f;     // their first serial per level (0xFFFFFFFF = none)
@@ -164,8 +165,15 @@ struct AggOut {
 	uint32_t parts;          // partitions P; regions [0, P) are partitions (nregions > P: HBM fallback lists)
 	uint64_t D;              // distinct elements in all regions
 };
+// Per-record extras of an aggregation run, for Minimize (minimize.hip); triage
+// passes none.
+struct AggSrc {
+	const int8_t* elem_prio;  // per-record prio, parallel to sigs (level lm.lvl[prio]); nullptr = the call's
+	uint32_t nshards, shard;  // keep only the records whose element this shard owns (owner_of)
+	double distinct_hint;     // expected distinct elements (0: the batch-ratio policy)
+};
 int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const LevelMap& lm,
-                  uint64_t run_recs, syzsig_batch_stats* st, AggOut* out);
+                  uint64_t run_recs, syzsig_batch_stats* st, AggOut* out, const AggSrc* x = nullptr);
 // validates a batch's call ranges (SYZSIG_EINVAL) and sums its records (triage.hip)
 int batch_total_records(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t* total, uint32_t prio_mask[8]);
 int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,

@@ -8,6 +8,15 @@
 //   argmax over entries of (prio, -rank)
 // which one atomicMax per entry computes on the slot word
 //   e << 32 | (prio ^ 0x80) << 24 | (0xFFFFFF - rank)        (rank < 2^24 - 1).
+//
+// The main path does it without device-scope atomics: the contexts in rank
+// order are a "batch" whose call r is context order[r], and its entries go
+// through the aggregation pipeline of agg.hip (partition by element, LDS hash
+// per partition) with each entry's own prio as its level.  Per element that
+// yields first[l] = the smallest rank with an entry at level l, so the winner
+// is first[top level present] -- argmax (prio, -rank) again.  The atomic form
+// above remains the fallback for more than 4 distinct prios (the records
+// carry 2 level bits) or a context of >= 2^24 entries.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -75,6 +84,78 @@ __global__ void k_min_winners(const uint64_t* __restrict__ slots, uint64_t nslot
 	}
 }
 
+// the virtual batch: call r = context order[r] (call_len 0 + bad for a
+// context too long for the aggregation records)
+__global__ void k_min_calls(const uint64_t* __restrict__ off, const uint32_t* __restrict__ order, uint64_t n,
+                            uint64_t* cstart, uint32_t* clen, unsigned long long* bad)
+{
+	uint64_t nb = 0;
+	for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+		const uint32_t c = order[r];
+		const uint64_t s = off[c], len = off[c + 1] - s;
+		cstart[r] = s;
+		clen[r] = len < (1ull << 24) ? (uint32_t)len : 0;
+		nb += len >= (1ull << 24);
+	}
+	block_count(bad, nb);
+}
+
+// prios present among the entries (256-bit mask, by u8 value): a per-lane
+// mask of 0..31 on the fast path, the full 8 words only when a wave sees one
+// outside it
+__global__ __launch_bounds__(256) void k_min_prio_mask(const uint8_t* __restrict__ prios, uint64_t n, uint32_t* mask)
+{
+	uint32_t lo = 0, m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	auto add_slow = [&](uint32_t u) {
+#pragma unroll
+		for (uint32_t k = 0; k < 8; k++)
+			m[k] |= (u >> 5) == k ? 1u << (u & 31) : 0u;
+	};
+	const uint64_t n16 = ((uintptr_t)prios & 15) ? 0 : n / 16;
+	const uint4* p16 = reinterpret_cast<const uint4*>(prios);
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint4 v = p16[i];
+		const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+		if (((v.x | v.y | v.z | v.w) & 0xE0E0E0E0u) == 0) {  // every byte < 32
+#pragma unroll
+			for (uint32_t k = 0; k < 16; k++)
+				lo |= 1u << ((w[k >> 2] >> ((k & 3) * 8)) & 31);
+		} else {
+#pragma unroll
+			for (uint32_t k = 0; k < 16; k++)
+				add_slow((w[k >> 2] >> ((k & 3) * 8)) & 0xFF);
+		}
+	}
+	for (uint64_t i = n16 * 16 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+	     i += (uint64_t)gridDim.x * blockDim.x)
+		add_slow(prios[i]);
+	m[0] |= lo;
+#pragma unroll
+	for (uint32_t k = 0; k < 8; k++) {
+		uint32_t r = m[k];
+		for (int d = 32; d >= 1; d >>= 1)
+			r |= __shfl_xor(r, d, 64);
+		if (lane_id() == 0 && r)
+			atomicOr(&mask[k], r);
+	}
+}
+
+// winners: per distinct element, the rank of its first entry at the top level
+// present -> keep[that context]
+__global__ __launch_bounds__(256) void k_min_from_dist(const uint4* __restrict__ dist_f,
+                                                       const uint32_t* __restrict__ cnt, uint32_t nregions,
+                                                       const uint32_t* __restrict__ order, uint8_t* keep)
+{
+	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
+		const uint32_t n = cnt[r];
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+			const uint4 f = dist_f[(uint64_t)r * kAggRegion + i];
+			const uint32_t rank = f.w != 0xFFFFFFFFu ? f.w : f.z != 0xFFFFFFFFu ? f.z : f.y != 0xFFFFFFFFu ? f.y : f.x;
+			keep[order[rank]] = 1;
+		}
+	}
+}
+
 __global__ void k_count_u8(const uint8_t* __restrict__ a, uint64_t n, unsigned long long* cnt)
 {
 	uint64_t c = 0;
@@ -86,6 +167,58 @@ __global__ void k_count_u8(const uint8_t* __restrict__ a, uint64_t n, unsigned l
 }  // namespace syz
 
 using namespace syz;
+
+// The aggregation path (header).  *used = false: the atomic path must run
+// (more than 4 distinct prios, or a context of >= 2^24 entries).
+static int minimize_agg(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
+                        uint64_t nctx, uint64_t total, uint32_t nshards, uint32_t shard, uint64_t hint,
+                        const uint32_t* order, uint8_t* d_keep, bool* used)
+{
+	*used = false;
+	hipStream_t st = ctx->stream;
+	void* vb;
+	SYZ_TRY(ws_get(ctx, 34, nctx * 12 + 128, &vb));
+	uint32_t* dmask = (uint32_t*)vb;
+	uint64_t* cstart = (uint64_t*)((char*)vb + 64);
+	uint32_t* clen = (uint32_t*)(cstart + nctx);
+	SYZ_TRY(counters_reset(ctx));
+	SYZ_HIP(hipMemsetAsync(dmask, 0, 32, st));
+	k_min_calls<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, order, nctx, cstart, clen, &ctx->d_cnt[kCntAux]);
+	k_min_prio_mask<<<grid_for(total / 16 + 1, 256, 2048), 256, 0, st>>>((const uint8_t*)d_prios, total, dmask);
+	SYZ_HIP(hipGetLastError());
+	uint32_t* hmask = (uint32_t*)(ctx->h_pin + kPinMask);
+	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 32, hipMemcpyDeviceToHost, st));
+	SYZ_TRY(counters_fetch(ctx));  // synchronizes the stream
+	if (ctx->h_cnt[kCntAux])
+		return SYZSIG_OK;
+	int8_t levels[4];
+	uint32_t nl = 0;
+	for (int v = -128; v <= 127; v++) {
+		const uint8_t u = (uint8_t)(int8_t)v;
+		if ((hmask[u >> 5] >> (u & 31)) & 1) {
+			if (nl == 4)
+				return SYZSIG_OK;
+			levels[nl++] = (int8_t)v;
+		}
+	}
+	LevelMap lm;
+	SYZ_TRY(level_map_from_levels(levels, nl, &lm));
+	syzsig_batch b = {};
+	b.sigs = d_elems;
+	b.call_start = cstart;
+	b.call_len = clen;
+	b.ncalls = nctx;
+	b.nrec = total;
+	const AggSrc x{d_prios, nshards, shard, (double)(hint ? hint : total)};  // distinct <= entries
+	syzsig_batch_stats bst = {};
+	AggOut a;
+	SYZ_TRY(agg_aggregate(ctx, &b, 0, nctx, lm, total, &bst, &a, &x));
+	SYZ_HIP(hipMemsetAsync(d_keep, 0, nctx, st));
+	k_min_from_dist<<<std::min<uint32_t>(a.nregions, 8192), 256, 0, st>>>(a.dist_f, a.cnt, a.nregions, order, d_keep);
+	SYZ_HIP(hipGetLastError());
+	*used = true;
+	return SYZSIG_OK;
+}
 
 extern "C" {
 
@@ -117,7 +250,7 @@ int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint
 	dv2 = (uint32_t*)dk2 + nctx;
 	SYZ_TRY(ws_get(ctx, 14, nctx * 4 + 64, &drank));
 	if (ctx->timing)
-		SYZ_HIP(hipEventRecord(ctx->ev[0], st));
+		SYZ_HIP(hipEventRecord(ctx->ev[3], st));
 	k_min_keys<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, nctx, (uint32_t*)dk, (uint32_t*)dv);
 	size_t tmp_bytes = 0;
 	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)dk, (uint32_t*)dk2, (uint32_t*)dv,
@@ -126,6 +259,23 @@ int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint
 	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, (uint32_t*)dk, (uint32_t*)dk2, (uint32_t*)dv,
 	                                           (uint32_t*)dv2, (int)nctx, 0, 32, st));
 	const uint32_t* order = (const uint32_t*)dv2;
+	bool used = false;
+	if (total && !(ctx->agg_dbg & SYZSIG_DEBUG_MIN_ATOMIC))
+		SYZ_TRY(minimize_agg(ctx, d_off, d_elems, d_prios, nctx, total, nshards, shard, hint_distinct, order, d_keep,
+		                     &used));
+	if (used) {
+		SYZ_TRY(counters_reset(ctx));
+		k_count_u8<<<grid_for(nctx, 256), 256, 0, st>>>(d_keep, nctx, ctx->d_cnt);
+		SYZ_HIP(hipGetLastError());
+		if (ctx->timing)
+			SYZ_HIP(hipEventRecord(ctx->ev[0], st));
+		SYZ_TRY(counters_fetch(ctx));
+		float t = 0;
+		if (ctx->timing && hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[0]) == hipSuccess)
+			ctx->last_ms = t;
+		*n_out = ctx->h_cnt[kCntAux];
+		return SYZSIG_OK;
+	}
 	k_min_rank<<<grid_for(nctx, 256), 256, 0, st>>>(order, nctx, (uint32_t*)drank);
 	// 2. per-element argmax of (prio, -rank)
 	uint64_t nb = buckets_for(hint_distinct ? hint_distinct : std::max<uint64_t>(total, 1));
@@ -154,7 +304,7 @@ int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint
 			if (rc == SYZSIG_OK)
 				rc = counters_fetch(ctx);
 			float t = 0;
-			if (rc == SYZSIG_OK && ctx->timing && hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]) == hipSuccess)
+			if (rc == SYZSIG_OK && ctx->timing && hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[1]) == hipSuccess)
 				ctx->last_ms = t;
 		}
 		syzsig_set_free(t);

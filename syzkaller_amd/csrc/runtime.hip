@@ -189,7 +189,7 @@ int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags)
 	SYZ_LOCK(ctx);
 	if (!ctx)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_debug: ctx is NULL");
-	ctx->agg_dbg = flags & SYZSIG_DEBUG_FIN_DEFER;  // only the result-preserving flags
+	ctx->agg_dbg = flags & (SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC);  // only the result-preserving flags
 	return SYZSIG_OK;
 }
 

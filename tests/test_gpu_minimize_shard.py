@@ -21,16 +21,62 @@ def corpus(rng, n, mean, universe, distinct_len=False):
     return off, elems, prios
 
 
+@pytest.mark.parametrize("path", ["agg", "atomic"])
 @pytest.mark.parametrize("seed,n,mean,U,distinct", [(0, 300, 50, 4000, True), (1, 2000, 200, 100000, False),
                                                      (2, 5000, 30, 500, False)])
-def test_minimize_vs_oracle(gpu, seed, n, mean, U, distinct):
+def test_minimize_vs_oracle(gpu, seed, n, mean, U, distinct, path):
+    """Both K5 paths: the aggregation path (default: entries partitioned by
+    element, LDS winners per partition) and the per-entry atomicMax path."""
+    from syzkaller_amd._lib import SYZSIG_DEBUG_MIN_ATOMIC
+
     rng = np.random.default_rng(seed)
     off, e, p = corpus(rng, n, mean, U, distinct)
     exp = O.minimize(off, e, p)
     t = lambda a, dt: torch.from_numpy(a.view(dt)).to(gpu.dev)  # noqa: E731
-    keep, cnt = gpu.minimize(t(off, np.int64), t(e, np.int32), t(p, np.int8))
+    gpu.eng.set_debug(SYZSIG_DEBUG_MIN_ATOMIC if path == "atomic" else 0)
+    try:
+        keep, cnt = gpu.minimize(t(off, np.int64), t(e, np.int32), t(p, np.int8))
+    finally:
+        gpu.eng.set_debug(0)
     got = np.nonzero(keep.cpu().numpy())[0].tolist()
     assert got == exp and cnt == len(exp)
+
+
+def test_minimize_many_prios_takes_atomic_path(gpu):
+    """8 distinct prios (incl. negative ones) exceed the aggregation records'
+    2 level bits: the atomic path runs, same result as the oracle."""
+    rng = np.random.default_rng(11)
+    off, e, _ = corpus(rng, 1500, 80, 30000)
+    p = rng.integers(-4, 4, size=e.size).astype(np.int8)
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).to(gpu.dev)  # noqa: E731
+    keep, cnt = gpu.minimize(t(off, np.int64), t(e, np.int32), t(p, np.int8))
+    assert np.nonzero(keep.cpu().numpy())[0].tolist() == O.minimize(off, e, p)
+
+
+def test_minimize_negative_prios_agg_path(gpu):
+    """4 prios spanning the sign (signed order -2 < -1 < 0 < 3) on the
+    aggregation path."""
+    rng = np.random.default_rng(12)
+    off, e, _ = corpus(rng, 1500, 80, 30000)
+    p = rng.choice(np.array([-2, -1, 0, 3], np.int8), size=e.size)
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).to(gpu.dev)  # noqa: E731
+    keep, cnt = gpu.minimize(t(off, np.int64), t(e, np.int32), t(p, np.int8))
+    assert np.nonzero(keep.cpu().numpy())[0].tolist() == O.minimize(off, e, p)
+
+
+def test_minimize_agg_partition_overflow(gpu):
+    """8 fixed partitions for ~98k distinct elements: every partition overflows
+    its LDS table and is aggregated in the HBM fallback table."""
+    rng = np.random.default_rng(13)
+    off, e, p = corpus(rng, 2000, 200, 100000)
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).to(gpu.dev)  # noqa: E731
+    gpu.eng.set_agg(1, 8)
+    try:
+        keep, cnt = gpu.minimize(t(off, np.int64), t(e, np.int32), t(p, np.int8))
+    finally:
+        gpu.eng.set_agg(1, 0)
+    exp = O.minimize(off, e, p)
+    assert np.nonzero(keep.cpu().numpy())[0].tolist() == exp and cnt == len(exp)
 
 
 def test_minimize_host_api(gpu):
