@@ -38,6 +38,10 @@ PROBE_BYTES_PER_REC = 12.0  # 4 B element read + 8 B maxSignal slot read (SURVEY
 # their summed device time (HIP events), roofline.traffic their summed PMC bytes
 K3_KERNELS = "k_agg_count+k_agg_scan_chunks+k_agg_scan_totals+k_agg_scatter+k_agg+k_agg_finalize_x+k_fin_deferred+k_ns_deferred"
 EDGE_BYTES_PER_PC = 12.0  # K1+K2: 8 B u64 PC in + 4 B u32 signal out
+# Minimize's chain on its aggregation path (csrc/minimize.hip header); the
+# keys sort and k_min_calls are negligible (200k contexts)
+MIN_KERNELS = ("k_min_prio_mask+k_agg_count+k_agg_scan_chunks+k_agg_scan_totals+k_agg_scatter+k_agg"
+               "+k_min_from_dist+k_count_u8")
 MIN_BYTES_PER_ENTRY, MIN_BYTES_PER_DISTINCT = 5.0, 4.0  # Minimize: (elem, prio) entry + covered[e]
 # N > 1: the source's aggregation, then the owner's records-mode triage of the staircases
 K3_DIST_KERNELS = "k_agg_count+k_agg_scan_chunks+k_agg_scan_totals+k_agg_scatter+k_agg+k_probe+k_decide"
@@ -67,14 +71,18 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_prefixes, cfg):
+TRIAGE_KEYS = ("programs_per_gpu", "calls", "pcs_per_call", "m0_per_gpu", "skew", "parallelism")
+MIN_KEYS = ("workload", "contexts", "entries", "mean_len")
+
+
+def pmc_traffic(kernel_prefixes, cfg, keys=TRIAGE_KEYS):
     """HBM bytes per launch of the dominant kernel from the newest committed
     rocprofv3 PMC summary (profiles/*/summary.json, written by
     scripts/summarize_prof.py from separate FETCH_SIZE / WRITE_SIZE passes of
-    this same bench command) whose workload matches; None if there is none."""
+    this same workload: scripts/profile.sh) whose workload matches; None if
+    there is none."""
     import glob
 
-    keys = ("programs_per_gpu", "calls", "pcs_per_call", "m0_per_gpu", "skew")
     best = None
     for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
         try:
@@ -82,7 +90,7 @@ def pmc_traffic(kernel_prefixes, cfg):
         except (OSError, ValueError):
             continue
         bc = d.get("bench_config") or {}
-        if any(bc.get(k) != cfg.get(k) for k in keys) or bc.get("parallelism") != cfg.get("parallelism"):
+        if any(bc.get(k) != cfg.get(k) for k in keys):
             continue
         tot, hit = 0.0, False
         for name, e in d.get("kernels", {}).items():
@@ -181,14 +189,16 @@ def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
         ms.append(dev.L.syzsig_ctx_last_ms(dev.eng.h))
     t = float(np.median(ms))
     byts = MIN_BYTES_PER_ENTRY * N + MIN_BYTES_PER_DISTINCT * distinct
+    cfg = {"workload": f"BASELINE config 3: Minimize over a {n}-program synthetic corpus, 1 GPU",
+           "contexts": n, "entries": N, "distinct": distinct, "mean_len": mean, "survivors": cnt}
+    traffic, src = pmc_traffic(["syz::" + k for k in MIN_KERNELS.split("+")], cfg, MIN_KEYS)
     achieved = byts / (t * 1e-3) / 1e9
     return {"metric": "signal.Minimize corpus entries/sec", "value": N / (t * 1e-3), "unit": "entries/s",
             "higher_is_better": True, "ms": t, "dtype": "u32",
-            "config": {"workload": f"BASELINE config 3: Minimize over a {n}-program synthetic corpus, 1 GPU",
-                       "contexts": n, "entries": N, "distinct": distinct, "mean_len": mean, "survivors": cnt},
-            "roofline": {"bound": "hbm", "kernel": "k_min_keys+radix sort+k_min_rank+k_min_cover+k_min_winners",
+            "config": cfg,
+            "roofline": {"bound": "hbm", "kernel": MIN_KERNELS,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
                          "bytes_per_unit": f"{MIN_BYTES_PER_ENTRY} B/entry + {MIN_BYTES_PER_DISTINCT} B/distinct",
                          "avg_launch_ms": t}}
 
