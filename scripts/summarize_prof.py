@@ -29,15 +29,16 @@ def short(name):
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
-    shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
     out = collections.OrderedDict()
-    for r in csv.DictReader(open(stats)):
-        out[short(r["Name"])] = {"launches": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
-                                 "pct": float(r["Percentage"])}
+    if os.path.exists(stats):  # a counter-only run (scripts/pmc_sq.sh) has no trace
+        shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+        for r in csv.DictReader(open(stats)):
+            out[short(r["Name"])] = {"launches": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                                     "pct": float(r["Percentage"])}
     pmc = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in sorted(os.listdir(src)):
         f = os.path.join(src, d, "run_counter_collection.csv")
-        if not d.startswith("pmc_") or not os.path.exists(f):
+        if not d.startswith("pmc") or not os.path.exists(f):
             continue
         for r in csv.DictReader(open(f)):
             pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -50,6 +51,13 @@ def main(src, dst):
             e["write_bytes"] = avg["WRITE_SIZE"] * 1024
         if "read_bytes" in e and "write_bytes" in e:
             e["traffic_bytes"] = e["read_bytes"] + e["write_bytes"]
+        if "SQ_WAVE_CYCLES" in avg and avg["SQ_WAVE_CYCLES"]:
+            # quad-cycle counters (MI355X_MICROARCH.md): shares of wave time
+            wc = avg["SQ_WAVE_CYCLES"]
+            e["sq_shares"] = {c: avg[c] / wc for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                                                        "SQ_WAIT_INST_LDS") if c in avg}
+        if "SQ_LDS_IDX_ACTIVE" in avg and avg["SQ_LDS_IDX_ACTIVE"] and "SQ_LDS_BANK_CONFLICT" in avg:
+            e["lds_bank_conflict_share"] = avg["SQ_LDS_BANK_CONFLICT"] / avg["SQ_LDS_IDX_ACTIVE"]
         if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
             t = avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"]
             e["l2_hit"] = avg["TCC_HIT_sum"] / t if t else None

@@ -108,3 +108,28 @@ def test_oracle_minimize_matches_literal_python():
                     covered[e] = (p, si)
         exp = sorted(order[si] for si in {v[1] for v in covered.values()})
         assert sorted(OracleImpl().minimize(ctxs)) == exp
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_oracle_mt_baseline_matches_sequential(threads):
+    """orc_triage_batch_mt (the bench's nproc-core CPU baseline: Procs under
+    one rwlock, fuzzer.go:494-511) ends in the same maxSignal and newSignal
+    as sequential checkNewSignal; which calls report new signal depends on the
+    thread interleaving, so only its bounds are checked."""
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default(skew=1)
+    nprog, cpp = 24, 16
+    cl = synth.call_lengths(nprog, cpp, 600)
+    pidx = synth.prog_call_index(nprog, cpp)
+    pcs, cs, prio = synth.traces(cfg, 0, nprog, cpp, cl)
+    sigs, cnt, _ = O.exec_batch(pcs, cs, cl, pidx)
+    m0e, m0p = synth.m0(cfg, 64, 20000)
+    ms, ns, _, cnew = O.triage_batch(m0e, m0p, sigs, cs, cnt, prio)
+    ms2 = O.deserialize(m0e, m0p)
+    ns2, ncalls = O.triage_batch_mt(ms2, sigs, cs, cnt, prio, cpp, threads)
+    assert ms2.to_dict() == ms.to_dict()
+    assert ns2.to_dict() == ns.to_dict()
+    assert 0 < ncalls <= cnt.size
+    if threads == 1:
+        assert ncalls == int(cnew.sum())
