@@ -562,8 +562,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 					cbase += b <= o0;
 					inside |= (uint32_t)(b > o0 && b < o0 + U * 64) << i;
 				}
+				// Lanes past the group's end re-read its last record (clamped
+				// index): a second copy of a record changes nothing (min is
+				// idempotent; its serial, counted past trailing empty cells, is
+				// only ever larger), so no lane needs a validity test.
 				uint32_t key[U], lv[U], k[U], hb[U], slot[U], c[U];
-				bool ok[U];
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++)
 					c[u] = cbase;
@@ -577,8 +580,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				}
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++) {
-					const uint32_t o = o0 + u * 64 + lane, r = buf[u];
-					ok[u] = o < n;
+					const uint32_t r = buf[u];
 					k[u] = (c[u] << g.cbits()) | g.local(r);
 					key[u] = g.resid(r);
 					lv[u] = g.level(r);
@@ -594,14 +596,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				for (uint32_t u = 0; u < U; u++) {
 					const uint32_t f = bucket_find(B[u], key[u]);
 					slot[u] = f < 4 ? hb[u] * 4 + f : kAggNoSlot;
-					any_need |= ok[u] && f >= 4;
+					any_need |= f >= 4;
 				}
 				// first sight of an element, or a chain past its home bucket: to the
 				// wave's queue (the record's own level first is taken there)
 				if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(any_need) != 0))) {
 #pragma unroll
 					for (uint32_t u = 0; u < U; u++) {
-						const bool nd = ok[u] && slot[u] == kAggNoSlot;
+						const bool nd = slot[u] == kAggNoSlot;
 						const uint64_t m = __ballot(nd);
 						if (!m)
 							continue;
@@ -611,7 +613,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 						if (nd)
 							wq[qn + lane_rank(m)] = make_uint2(key[u], (lv[u] << 24) | k[u]);
 						qn += c;
-						ok[u] = ok[u] && !nd;
 					}
 					__builtin_amdgcn_wave_barrier();
 				}
@@ -619,7 +620,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 					return;
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++)
-					if (ok[u] && slot[u] != kAggNoSlot)
+					if (slot[u] != kAggNoSlot)
 						atomicMin(&fl[lv[u]][slot[u]], k[u]);
 			};
 			// a ring of D + 1 register buffers, rotated by full unrolling (static
