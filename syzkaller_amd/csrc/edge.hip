@@ -75,26 +75,29 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 	__shared__ uint32_t stamp[kBins];
 	__shared__ __align__(16) uint32_t s_any[2][kEdgeWaves];
 	__shared__ uint32_t s_carry[2][kEdgeWaves];
-	__shared__ uint32_t s_wcnt[kEdgeWaves];
 	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, pos = threadIdx.x;  // pos: place in a chunk
 	uint32_t seq = 0;
 	// Workgroup OR of a predicate (one barrier): every wave writes its own
 	// flag, ds_read_b128s read them all.  Two rows alternate: a row is
 	// rewritten two calls later, after every wave passed the barrier between.
-	auto wg_any = [&](bool pred) -> bool {
-		uint32_t* row = s_any[seq & 1];
+	// A wave may publish a payload with its flag (row[w] = payload << 1 | flag,
+	// readable in `row` until the next call but one).
+	const uint32_t* row = s_any[0];
+	auto wg_any = [&](bool pred, uint32_t payload) -> bool {
+		uint32_t* r = s_any[seq & 1];
 		const uint32_t any = __ballot(pred) != 0;
 		if (lane == 0)
-			row[w] = any;
+			r[w] = payload << 1 | any;
 		lds_barrier();
 		uint32_t o = 0;
 #pragma unroll
 		for (uint32_t i = 0; i < W / 4; i++) {
-			const uint4 a = reinterpret_cast<const uint4*>(row)[i];
+			const uint4 a = reinterpret_cast<const uint4*>(r)[i];
 			o |= a.x | a.y | a.z | a.w;
 		}
 		seq++;
-		return o != 0;
+		row = r;
+		return (o & 1) != 0;
 	};
 	uint64_t err = 0;
 	uint32_t epoch = 0;
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 					s_carry[q & 1][w] = h;
 				// cover_check (executor_linux.cc:196-204): doexit(0), this call and
 				// the rest of the program publish nothing
-				if (wg_any(valid && !cover_check(pc)))
+				if (wg_any(valid && !cover_check(pc), 0))
 					return false;
 				if (lane == 0)
 					up = w == 0 ? carry : s_carry[q & 1][w - 1];
@@ -159,7 +162,10 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 				const uint32_t home = sig & (kDedupSize - 1);
 				const uint32_t b0 = home >> kBinShift, b1 = ((home + 3) & (kDedupSize - 1)) >> kBinShift;
 				bool pending = valid, emit = false;
-				while (wg_any(pending)) {
+				// rounds until no lane is pending (a chunk always has a valid lane, so
+				// the first round needs no test); the test after the last round also
+				// publishes every wave's emit count for the output below
+				for (;;) {
 					// 1. evaluate dedup() (executor.h:692-706) on the current table,
 					// branch-free: the first probe i with T[h+i] == sig (duplicate)
 					// or T[h+i] == 0 (insert there), else the forced overwrite at h
@@ -195,7 +201,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						blocked = pending && (s0 > v || s1 > v);
 						mark_now = blocked && !marker;
 						marker = marker || mark_now;
-						if (!wg_any(mark_now))
+						if (!wg_any(mark_now, 0))
 							break;
 					}
 					// 3. final lanes commit (visible after the next round's barrier)
@@ -204,16 +210,15 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						table[wpos] = sig;
 					emit = emit || fin_w;
 					pending = pending && blocked;
+					if (!wg_any(pending, (uint32_t)__popcll(__ballot(emit))))
+						break;
 				}
 				// write_output order == trace order: waves in order, lanes in order
 				const uint64_t m = __ballot(emit);
-				if (lane == 0)
-					s_wcnt[w] = (uint32_t)__popcll(m);
-				lds_barrier();
 				uint32_t base = nsig, tot = 0;
 #pragma unroll
 				for (uint32_t i = 0; i < kEdgeWaves; i++) {
-					const uint32_t x = s_wcnt[i];
+					const uint32_t x = row[i] >> 1;
 					base += i < w ? x : 0;
 					tot += x;
 				}
