@@ -281,25 +281,35 @@ __global__ __launch_bounds__(1024) void k_agg_scan_chunks(const uint32_t* counts
 	}
 }
 
-// totals -> rec_base[P + 1] (one block; P <= 2048)
+// totals -> rec_base[P + 1] (one block of 1024 threads, P <= 2048: two
+// partitions per thread, a wave scan, then the 16 wave sums)
 __global__ __launch_bounds__(1024) void k_agg_scan_totals(const uint64_t* totals, uint32_t P, uint64_t* rec_base)
 {
-	__shared__ uint64_t s[kAggMaxParts];
-	for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
-		s[i] = totals[i];
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		uint64_t r = 0;
-		for (uint32_t p = 0; p < P; p++) {
-			const uint64_t t = s[p];
-			s[p] = r;
-			r += t;
-		}
-		rec_base[P] = r;
+	__shared__ uint64_t wsum[16];
+	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, i0 = threadIdx.x * 2;
+	const uint64_t a = i0 < P ? totals[i0] : 0, b = i0 + 1 < P ? totals[i0 + 1] : 0;
+	uint64_t x = a + b;  // inclusive wave scan of the pair sums
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint64_t y = __shfl_up(x, o, 64);
+		if (lane >= (uint32_t)o)
+			x += y;
 	}
+	if (lane == 63)
+		wsum[w] = x;
 	__syncthreads();
-	for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
-		rec_base[i] = s[i];
+	uint64_t pre = 0, tot = 0;
+	for (uint32_t k = 0; k < 16; k++) {
+		pre += k < w ? wsum[k] : 0;
+		tot += wsum[k];
+	}
+	const uint64_t ex = pre + x - (a + b);
+	if (i0 < P)
+		rec_base[i0] = ex;
+	if (i0 + 1 < P)
+		rec_base[i0 + 1] = ex + a;
+	if (threadIdx.x == 0)
+		rec_base[P] = tot;
 }
 
 // Records of each chunk -> their cells (fixed by the scan, so no global
@@ -900,8 +910,9 @@ __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __
 // claims are LDS compare-and-swaps on the slot's index, not global atomics
 // (measured: device-scope CAS runs at ~20 G/s chip-wide and bounded the
 // atomic finalize).  Probe sequences stop at the slice end: such an element
-// (or one whose claim table is full) is deferred to k_fin_deferred /
-// k_ns_deferred, which run after this launch with the global-atomic code.
+// (or one whose claim table is full) is deferred, and so is a newSignal merge
+// that leaves its slice: k_fin_deferred takes both lists after this launch,
+// with the global-atomic code.
 // Correct slot choice: slots only go empty -> key, so an element present at
 // launch start sits before the first slot that was empty then; a slot seen
 // occupied, or claimed by another element, is occupied at launch end, so the
@@ -1091,15 +1102,16 @@ __global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
 
 // Deferred elements of k_agg_finalize_x, with the global-atomic table code
 // (launched after it: the slices are free for everyone again).
-__global__ __launch_bounds__(256) void k_fin_deferred(const uint32_t* __restrict__ def_e, const uint4* __restrict__ def_f,
+__device__ void fin_deferred(const uint32_t* __restrict__ def_e, const uint4* __restrict__ def_f,
                                                       const unsigned long long* __restrict__ def_cnt, LevelMap lm,
                                                       uint64_t c0, uint64_t* slots, uint64_t bmask, uint64_t* ns_slots,
                                                       uint64_t ns_bmask, uint8_t* call_new, uint64_t* pairs,
-                                                      unsigned long long* npairs, unsigned long long* ctr)
+                                                      unsigned long long* npairs, unsigned long long* ctr,
+                                                      uint32_t nblocks, uint32_t block)
 {
 	const uint64_t n = *def_cnt, max_probe = max_probe_for(bmask);
 	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0;
-	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+	for (uint64_t i = block * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)nblocks * blockDim.x) {
 		const uint32_t e = def_e[i];
 		const uint4 f4 = def_f[i];
 		const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
@@ -1151,13 +1163,13 @@ __global__ __launch_bounds__(256) void k_fin_deferred(const uint32_t* __restrict
 }
 
 // Deferred newSignal merges of k_agg_finalize_x: (elem << 32 | prio ^ 0x80).
-__global__ __launch_bounds__(256) void k_ns_deferred(const uint64_t* __restrict__ def_ns,
-                                                     const unsigned long long* __restrict__ def_ns_cnt,
-                                                     uint64_t* ns_slots, uint64_t ns_bmask, unsigned long long* ctr)
+__device__ void ns_deferred(const uint64_t* __restrict__ def_ns, const unsigned long long* __restrict__ def_ns_cnt,
+                            uint64_t* ns_slots, uint64_t ns_bmask, unsigned long long* ctr, uint32_t nblocks,
+                            uint32_t block)
 {
 	const uint64_t n = *def_ns_cnt;
 	uint64_t ins = 0, ovf = 0;
-	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+	for (uint64_t i = block * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)nblocks * blockDim.x) {
 		const uint64_t v = def_ns[i];
 		const int r = tbl_merge(ns_slots, ns_bmask, (uint32_t)(v >> 32), (int8_t)((uint8_t)v ^ 0x80u));
 		ins += r == 1;
@@ -1165,6 +1177,25 @@ __global__ __launch_bounds__(256) void k_ns_deferred(const uint64_t* __restrict_
 	}
 	block_count(&ctr[kCntAux], ins);
 	block_count(&ctr[kCntOverflow], ovf);
+}
+
+// Both deferred lists in one launch: the first kDeferBlocks blocks take the
+// elements, the rest the newSignal merges (both sides only ever max-merge
+// newSignal with atomics, so they commute).
+constexpr uint32_t kDeferBlocks = 64;
+__global__ __launch_bounds__(256) void k_fin_deferred(const uint32_t* __restrict__ def_e, const uint4* __restrict__ def_f,
+                                                      const unsigned long long* __restrict__ def_cnt, LevelMap lm,
+                                                      uint64_t c0, uint64_t* slots, uint64_t bmask, uint64_t* ns_slots,
+                                                      uint64_t ns_bmask, uint8_t* call_new, uint64_t* pairs,
+                                                      unsigned long long* npairs, unsigned long long* ctr,
+                                                      const uint64_t* __restrict__ def_ns,
+                                                      const unsigned long long* __restrict__ def_ns_cnt)
+{
+	if (blockIdx.x < kDeferBlocks)
+		fin_deferred(def_e, def_f, def_cnt, lm, c0, slots, bmask, ns_slots, ns_bmask, call_new, pairs, npairs, ctr,
+		             kDeferBlocks, blockIdx.x);
+	else
+		ns_deferred(def_ns, def_ns_cnt, ns_slots, ns_bmask, ctr, gridDim.x - kDeferBlocks, blockIdx.x - kDeferBlocks);
 }
 
 // ---------------------------------------------------------------- new bits
@@ -1522,10 +1553,10 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 		    a.dist_e, a.dist_f, a.cnt, a.nregions, lm, c0, ms->slots, ms->nbuckets - 1, ms_shift, nsp->slots,
 		    nsp->nbuckets - 1, ns_shift, b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2], ctx->d_cnt, def_e, def_f,
 		    &ctx->d_cnt[kCntDefer], (uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], ctx->agg_dbg);
-		k_fin_deferred<<<64, 256, 0, s>>>(def_e, def_f, &ctx->d_cnt[kCntDefer], lm, c0, ms->slots, ms->nbuckets - 1, nsp->slots,
-		                                  nsp->nbuckets - 1, b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2],
-		                                  ctx->d_cnt);
-		k_ns_deferred<<<64, 256, 0, s>>>((const uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], nsp->slots, nsp->nbuckets - 1, ctx->d_cnt);
+		k_fin_deferred<<<2 * kDeferBlocks, 256, 0, s>>>(def_e, def_f, &ctx->d_cnt[kCntDefer], lm, c0, ms->slots,
+		                                                ms->nbuckets - 1, nsp->slots, nsp->nbuckets - 1, b->call_new,
+		                                                (uint64_t*)pr, &ctx->d_cnt[kCntAux2], ctx->d_cnt,
+		                                                (const uint64_t*)dn, &ctx->d_cnt[kCntDeferNs]);
 	} else if (D) {
 		k_agg_finalize<<<a.nregions, kFinThreads, 0, s>>>(
 		    a.dist_e, a.dist_f, a.cnt, a.nregions, lm, c0, ms->slots,
