@@ -72,9 +72,15 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
  * SYZSIG_DEBUG_FIN_DEFER = the batch finalize sends every element whose probe
  * sequence leaves its home bucket to the atomic (deferred) path;
  * SYZSIG_DEBUG_MIN_ATOMIC = Minimize takes its per-entry atomicMax path instead
- * of the aggregation path. */
+ * of the aggregation path;
+ * SYZSIG_DEBUG_EXACT_CELLS = large triage runs partition records into counted
+ * cells (count pass + scan) instead of capped cells;
+ * SYZSIG_DEBUG_CAP_SPILL = capped cells of 64 records, so that dense runs
+ * overflow them and take the redo with counted cells. */
 #define SYZSIG_DEBUG_FIN_DEFER 32u
 #define SYZSIG_DEBUG_MIN_ATOMIC 64u
+#define SYZSIG_DEBUG_EXACT_CELLS 128u
+#define SYZSIG_DEBUG_CAP_SPILL 256u
 int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
 
 /* ---- pkg/signal/signal.go ---- */

@@ -18,6 +18,8 @@ SYZSIG_ERANGE = -34
 SYZSIG_ECORRUPT = -74
 SYZSIG_DEBUG_FIN_DEFER = 32
 SYZSIG_DEBUG_MIN_ATOMIC = 64
+SYZSIG_DEBUG_EXACT_CELLS = 128
+SYZSIG_DEBUG_CAP_SPILL = 256
 
 
 class SyzsigError(RuntimeError):

@@ -62,7 +62,10 @@ constexpr uint32_t kAggOverflow = 0xFFFFFFFFu;     // partition count marker
 constexpr uint32_t kAggMinBits = 3, kAggMaxBits = 11;
 constexpr uint32_t kAggMaxParts = 1u << kAggMaxBits;
 constexpr uint32_t kAggTile = 18432;  // records per scatter tile (18 per lane; 6 B of LDS each)
-constexpr uint32_t kAggGroup = 8;     // cells per wave work item of k_agg
+#ifndef SYZ_AGG_GROUP
+#define SYZ_AGG_GROUP 8
+#endif
+constexpr uint32_t kAggGroup = SYZ_AGG_GROUP;  // cells per wave work item of k_agg (<= 64)
 
 static_assert(0x85ebca6bu * 0xa5cb9243u == 1u, "fmix32_inv multiplier");
 static_assert(0xc2b2ae35u * 0x7ed1b41du == 1u, "fmix32_inv multiplier");
@@ -323,21 +326,37 @@ __global__ __launch_bounds__(1024) void k_agg_scan_totals(const uint64_t* totals
 // whose element shard x.shard owns are kept.
 constexpr uint32_t kScatChunkMax = 1u << (kAggMaxBits - 2);  // calls per chunk (cbits <= 9)
 
-template <bool kEntry>
+// Capped cells (the count-free layout of a triage run):
+// chunk c's cells are consecutive regions of cap[c] records (a multiple of 64)
+// from base[c], partition after partition; the scatter writes cnt[p][c] and
+// raises *ovf when a cell receives more than its capacity (the run is then
+// redone with counted cells).
+struct CapCells {
+	const uint64_t* base;  // [nchunks] first record of chunk c's cells
+	const uint32_t* cap;   // [nchunks] records per cell of chunk c
+	uint32_t* cnt;         // [P][nchunks] records in cell (c, p)
+	uint32_t* ovf;         // set to 1 by a cell overflow
+	uint64_t nchunks;
+};
+
+template <bool kEntry, bool kCap>
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __restrict__ sigs,
                                                              const uint64_t* __restrict__ call_start,
                                                              const uint32_t* __restrict__ call_len,
                                                              const uint8_t* __restrict__ call_prio, LevelMap lm,
                                                              uint64_t c0, uint64_t c1, AggGeom g, AggSrc x,
                                                              const uint32_t* __restrict__ offs,
-                                                             const uint64_t* __restrict__ rec_base, uint32_t* recs)
+                                                             const uint64_t* __restrict__ rec_base, CapCells cc,
+                                                             uint32_t* recs)
 {
 	constexpr uint32_t kWaves = kAggThreads / 64, kQuota = kAggTile / kWaves, kPer = kQuota / 64;
 	static_assert(kQuota % 64 == 0, "tile quota per wave");
+	static_assert(!(kEntry && kCap), "capped cells are for whole-chunk work items");
 	__shared__ uint32_t t_rec[kAggTile];   // sorted by partition: packed records
 	__shared__ uint16_t t_part[kAggTile];  // ... and their partitions
 	__shared__ uint64_t cur[kAggMaxParts];
 	__shared__ uint32_t hist[kAggMaxParts], pos[kAggMaxParts];
+	__shared__ uint32_t room[kCap ? kAggMaxParts : 1];  // capped: free records left in the cell
 	__shared__ uint64_t c_start[kScatChunkMax];  // the chunk's calls
 	__shared__ uint32_t c_len[kScatChunkMax];
 	__shared__ uint16_t c_meta[kScatChunkMax];
@@ -350,11 +369,18 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
 	const uint64_t ncalls = c1 - c0, nitems = (ncalls + (1ull << ib) - 1) >> ib;
 	const uint32_t per_t = (P + blockDim.x - 1) / blockDim.x;
+	bool spilled = false;
 	for (uint64_t ch = blockIdx.x; ch < nitems; ch += gridDim.x) {  // ch: work item (of 2^ibits calls)
 		const uint64_t cbeg = ch << ib;
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-			cur[i] = rec_base[i] + offs[ch * P + i];
+			if (kCap) {
+				const uint32_t cap = cc.cap[ch];
+				cur[i] = cc.base[ch] + (uint64_t)i * cap;
+				room[kCap ? i : 0] = cap;
+			} else {
+				cur[i] = rec_base[i] + offs[ch * P + i];
+			}
 			hist[i] = 0;
 		}
 		for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
@@ -454,30 +480,112 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 			n = fetch();
 			__syncthreads();
 			// consecutive threads write consecutive records of one partition's run
-			for (uint32_t d = threadIdx.x; d < nt; d += blockDim.x)
-				recs[cur[t_part[d]] + d] = t_rec[d];
+			for (uint32_t d = threadIdx.x; d < nt; d += blockDim.x) {
+				const uint32_t p = t_part[d];
+				if (!kCap || d - pos[p] < room[kCap ? p : 0])
+					recs[cur[p] + d] = t_rec[d];
+				else
+					spilled = true;
+			}
 			__syncthreads();
 			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
 				cur[i] += pos[i] + hist[i];  // advance by the run
+				if (kCap)
+					room[kCap ? i : 0] -= min(room[kCap ? i : 0], hist[i]);
 				hist[i] = 0;
 			}
 			if (!__syncthreads_or(n != 0))
 				break;
 		}
+		if (kCap) {
+			const uint32_t cap = cc.cap[ch];
+			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
+				cc.cnt[(uint64_t)i * cc.nchunks + ch] = cap - room[kCap ? i : 0];
+			__syncthreads();  // room is reset by the next item
+		}
+	}
+	if (kCap && spilled)
+		*cc.ovf = 1u;
+}
+
+// Capped cells of a run: records per chunk -> cell capacity and chunk base.
+// cap = m + sd * sqrt(m) + 64 rounded up to 64, m = the chunk's records / P
+// (the cells of a uniformly hashed chunk hold m +- sqrt(m)); the host reserves
+// 1.25 * records + nchunks * P * (sd^2 + 128), an upper bound of the sum
+// (sd * sqrt(m) <= m / 4 + sd^2).
+__global__ __launch_bounds__(256) void k_chunk_sizes(const uint32_t* __restrict__ call_len, uint64_t c0, uint64_t c1,
+                                                     uint32_t cbits, uint64_t* sizes)
+{
+	const uint64_t ch = blockIdx.x, cbeg = c0 + (ch << cbits), cend = min<uint64_t>(c1, cbeg + (1ull << cbits));
+	uint64_t s = 0;
+	for (uint64_t c = cbeg + threadIdx.x; c < cend; c += blockDim.x)
+		s += call_len[c];
+	s = wave_sum_u64(s);
+	__shared__ uint64_t ws[4];
+	if (lane_id() == 0)
+		ws[threadIdx.x >> 6] = s;
+	__syncthreads();
+	if (threadIdx.x == 0)
+		sizes[ch] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(1024) void k_cell_plan(const uint64_t* __restrict__ sizes, uint64_t nchunks, uint32_t P,
+                                                    float sd, uint64_t* base, uint32_t* cap)
+{
+	__shared__ uint64_t wsum[16];
+	uint64_t run = 0;
+	for (uint64_t b0 = 0; b0 < nchunks; b0 += blockDim.x) {
+		const uint64_t c = b0 + threadIdx.x;
+		uint64_t v = 0;
+		if (c < nchunks) {
+			const float m = (float)sizes[c] / (float)P;
+			const uint32_t k = sd < 0 ? 64u : ((uint32_t)(m + sd * sqrtf(m)) + 64 + 63) & ~63u;  // sd < 0: tests
+			cap[c] = k;
+			v = (uint64_t)k * P;
+		}
+		// exclusive block scan of v
+		uint64_t xs = v;
+		const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint64_t y = __shfl_up(xs, o, 64);
+			if (lane >= (uint32_t)o)
+				xs += y;
+		}
+		if (lane == 63)
+			wsum[w] = xs;
+		__syncthreads();
+		uint64_t pre = 0, tot = 0;
+		for (uint32_t i = 0; i < 16; i++) {
+			pre += i < w ? wsum[i] : 0;
+			tot += wsum[i];
+		}
+		if (c < nchunks)
+			base[c] = run + pre + xs - v;
+		run += tot;
+		__syncthreads();
 	}
 }
 
 // ---------------------------------------------------------------- aggregation
-// One workgroup per partition.  Waves take groups of kAggGroup cells from an
-// LDS counter.  Output: the partition's distinct elements and their level
-// firsts at dist_*[p * kAggRegion ...], cnt[p] = how many, or kAggOverflow
-// when they do not fit the LDS table.
-// U records per lane per batch, D batches in flight ahead of the one absorbed.
-template <uint32_t U, uint32_t D>
+// One workgroup per partition.  Waves take groups of kAggGroup cells (chunks)
+// from an LDS counter and stream them as 64-record slices: a slice lies in one
+// cell, so its chunk -- and the serial's high bits -- is uniform (scalar).
+// Cell (c, p): counted layout, the partition's records from rec_base[p] with
+// cell offsets offsT[p][.]; capped layout (kCap), cap[c] records from
+// base[c] + p * cap[c] of which cnt[p][c] are written.  Output: the
+// partition's distinct elements and their level firsts at
+// dist_*[p * kAggRegion ...], cnt[p] = how many, or kAggOverflow when they do
+// not fit the LDS table.
+// U slices per lane per batch, D batches in flight ahead of the one absorbed.
+template <uint32_t U, uint32_t D, bool kCap>
 __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict__ recs,
                                                      const uint64_t* __restrict__ rec_base,
-                                                     const uint32_t* __restrict__ offsT, uint64_t nchunks, AggGeom g,
-                                                     uint32_t* dist_e, uint4* dist_f, uint32_t* cnt, uint32_t dbg)
+                                                     const uint32_t* __restrict__ offsT,
+                                                     const uint64_t* __restrict__ cap_base,
+                                                     const uint32_t* __restrict__ cap_len,
+                                                     const uint32_t* __restrict__ cap_cnt, uint64_t nchunks, AggGeom g,
+                                                     uint32_t* dist_e, uint4* dist_f, uint32_t* cnt)
 {
 	__shared__ uint4 kb[kAggBuckets];  // keys (residuals), 4-slot buckets
 	__shared__ uint32_t fl[4][kAggSlots];
@@ -521,7 +629,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 			s_next = 0;
 		}
 		__syncthreads();
-		const uint32_t* pr = recs + rec_base[p];
 		const uint32_t* ot = offsT + (uint64_t)p * (nchunks + 1);
 		// no barrier inside: a wave leaves early once overflow is flagged
 		for (;;) {
@@ -531,62 +638,89 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 			gi = __builtin_amdgcn_readfirstlane(__shfl(gi, 0, 64));
 			if (gi >= ngroups || lds_flag(&s_ovf))
 				break;
-			CellGroup cg;
-			cg.load(ot, nchunks, gi);
-			const uint32_t jb = cg.bnd[0], je = cg.bnd[kAggGroup];
-			if (je <= jb)
-				continue;
-			// The group's records through a wave-uniform base (32-bit lane
-			// offsets: saddr loads, no 64-bit address math per record).
-			const uint32_t* gp = pr + jb;
-			const uint32_t n = je - jb, nl = n - 1;
-			const uint32_t chunk0 = (uint32_t)cg.ch0;
-			// Records stream through registers one batch ahead of the LDS work,
-			// ping-ponging between two buffers.  Loads are unconditional (index
-			// clamped): a load under a branch makes the compiler drain vmcnt(0)
-			// at the first use, i.e. wait for the prefetch too.
-			auto fetch = [&](uint32_t (&buf)[U], uint32_t o0) {
+			// the group's cells, one per lane 0..kAggGroup-1: first record and
+			// records.  The group is walked as one virtual run, cell after cell:
+			// virtual offset v of cell i is record recs[v + delta_i].
+			const uint64_t ch0 = (uint64_t)gi * kAggGroup;
+			uint64_t lbase = 0;
+			uint32_t llen = 0;
+			{
+				const uint64_t c = ch0 + lane;
+				if (lane < kAggGroup && c < nchunks) {
+					if (kCap) {
+						lbase = cap_base[c] + (uint64_t)p * cap_len[c];
+						llen = cap_cnt[(uint64_t)p * nchunks + c];
+					} else {
+						lbase = rec_base[p] + ot[c];
+						llen = ot[c + 1] - ot[c];
+					}
+				}
+			}
+			uint32_t lvs = llen;  // inclusive scan over lanes 0..kAggGroup-1, then exclusive
 #pragma unroll
-				for (uint32_t u = 0; u < U; u++)
-					buf[u] = __builtin_nontemporal_load(&gp[min(o0 + u * 64 + lane, nl) & (dbg & 1 ? 0x3FFFu : ~0u)]);
+			for (uint32_t o = 1; o < kAggGroup; o <<= 1) {
+				const uint32_t y = __shfl_up(lvs, o, 64);
+				if (lane >= o)
+					lvs += y;
+			}
+			const uint32_t n = __builtin_amdgcn_readlane(lvs, kAggGroup - 1);
+			if (n == 0)
+				continue;
+			lvs -= llen;
+			const uint64_t ldelta = lbase - lvs;
+			const uint32_t nl = n - 1;
+			// Per batch [o0, o0 + U * 64): the cell of o0 (the last cell starting
+			// at or before it: a non-empty one, as an empty cell shares its
+			// successor's start) and the cells starting inside the batch.
+			auto cells = [&](uint32_t o0, uint32_t& c0, uint32_t& inside) {
+				c0 = (uint32_t)__popcll(__ballot(lane < kAggGroup && lvs <= o0)) - 1;
+				inside = (uint32_t)__ballot(lane < kAggGroup && lvs > o0 && lvs < o0 + U * 64);
 			};
-			// Branch-free per record: the chunk of offset o is the number of cell
-			// boundaries <= o; those at or below the batch start are counted
-			// once per batch on the scalar unit, the (~1-2) inside the batch per
-			// lane, the rest cannot matter.
-			auto absorb = [&](const uint32_t (&buf)[U], uint32_t o0) {
-				if (dbg & 4) {  // timing only: the record stream alone
-					uint32_t x = 0;
+			auto delta_of = [&](uint32_t i) -> uint64_t {
+				const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)ldelta, i);
+				const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(ldelta >> 32), i);
+				return (uint64_t)hi << 32 | lo;
+			};
+			// Records stream through registers one batch ahead of the LDS work,
+			// ping-ponging between register buffers.  Loads are unconditional:
+			// lanes past the group re-read its last record -- a second copy of a
+			// record changes nothing (min is idempotent), so no lane needs a
+			// validity test.
+			auto fetch = [&](uint32_t (&buf)[U], uint32_t o0) {
+				uint32_t c0, inside;
+				cells(min(o0, nl), c0, inside);  // a prefetch past the group reads its last record
+				const uint64_t d0 = delta_of(c0);
+				uint32_t v[U];
+				uint64_t d[U];
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++) {
+					v[u] = min(o0 + u * 64 + lane, nl);
+					d[u] = d0;
+				}
+				for (uint32_t m = __builtin_amdgcn_readfirstlane(inside); m; m &= m - 1) {
+					const uint32_t j = __builtin_ctz(m), vs = __builtin_amdgcn_readlane(lvs, j);
+					const uint64_t dj = delta_of(j);
 #pragma unroll
 					for (uint32_t u = 0; u < U; u++)
-						x ^= buf[u];
-					if (x == 0x12345679u)
-						lds_flag_set(&s_ovf);
-					return;
+						d[u] = v[u] >= vs ? dj : d[u];
 				}
-				uint32_t cbase = chunk0;
-				uint32_t inside = 0;  // bit i: boundary i lies inside this batch
 #pragma unroll
-				for (uint32_t i = 1; i < kAggGroup; i++) {
-					const uint32_t b = cg.bnd[i] - jb;
-					cbase += b <= o0;
-					inside |= (uint32_t)(b > o0 && b < o0 + U * 64) << i;
-				}
-				// Lanes past the group's end re-read its last record (clamped
-				// index): a second copy of a record changes nothing (min is
-				// idempotent; its serial, counted past trailing empty cells, is
-				// only ever larger), so no lane needs a validity test.
+				for (uint32_t u = 0; u < U; u++)
+					buf[u] = __builtin_nontemporal_load(&recs[v[u] + d[u]]);
+			};
+			auto absorb = [&](const uint32_t (&buf)[U], uint32_t o0) {
+				uint32_t c0, inside;
+				cells(o0, c0, inside);
 				uint32_t key[U], lv[U], k[U], hb[U], slot[U], c[U];
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++)
-					c[u] = cbase;
-				// a uniform loop over the (0-2 typically) boundaries inside the
-				// batch; each boundary re-read by a scalar load
+					c[u] = (uint32_t)ch0 + c0;
+				// a uniform loop over the (0-2 typically) cells starting inside the batch
 				for (uint32_t m = __builtin_amdgcn_readfirstlane(inside); m; m &= m - 1) {
-					const uint32_t b = ot[min<uint64_t>(cg.ch0 + __builtin_ctz(m), nchunks)] - jb;
+					const uint32_t vs = __builtin_amdgcn_readlane(lvs, __builtin_ctz(m));
 #pragma unroll
 					for (uint32_t u = 0; u < U; u++)
-						c[u] += o0 + u * 64 + lane >= b;
+						c[u] += min(o0 + u * 64 + lane, nl) >= vs;
 				}
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++) {
@@ -626,8 +760,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 					}
 					__builtin_amdgcn_wave_barrier();
 				}
-				if (dbg & 2)  // timing only: no firsts
-					return;
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++)
 					if (slot[u] != kAggNoSlot)
@@ -1345,9 +1477,96 @@ static AggGeom agg_geom_for(syzsig_ctx* ctx, uint64_t nrec, double distinct_hint
 	return g;
 }
 
+// The count-free attempt of a triage run: scatter into capped cells (no count
+// pass, no scan), then aggregate.  *done = false when the run must be redone
+// with counted cells: a cell overflowed (the slack is doubled for the next run,
+// and capped cells are given up past kCapSdMax), or a partition overflowed the
+// LDS table (its HBM fallback reads counted cells).
+constexpr float kCapSdMax = 24.0f;
+static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const LevelMap& lm,
+                      uint64_t run_recs, const AggGeom& g, syzsig_batch_stats* st, AggOut* out, bool* done)
+{
+	*done = false;
+	const uint32_t P = 1u << g.pbits;
+	const uint64_t nchunks = (c1 - c0 + (1ull << g.cbits()) - 1) >> g.cbits();
+	const bool tight = ctx->agg_dbg & SYZSIG_DEBUG_CAP_SPILL;
+	const float sd = tight ? 0.0f : ctx->cap_sd;
+	// upper bound of sum_c P * cap[c] (k_cell_plan): 1.25 records + per cell sd^2 + 128
+	const uint64_t bound = run_recs + run_recs / 4 + nchunks * P * (uint64_t)(sd * sd + 128.0f) + 64;
+	void *recs, *cm, *de, *df, *dc;
+	SYZ_TRY(ws_get(ctx, 16, bound * 4, &recs));
+	SYZ_TRY(ws_get(ctx, 17, nchunks * 20 + (uint64_t)P * nchunks * 4 + 256, &cm));
+	uint64_t* sizes = (uint64_t*)cm;
+	uint64_t* cbase = sizes + nchunks;
+	uint32_t* ccap = (uint32_t*)(cbase + nchunks);
+	uint32_t* ccnt = ccap + nchunks;
+	uint32_t* ovf = ccnt + (uint64_t)P * nchunks;
+	SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
+	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
+	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
+	const hipStream_t s = ctx->stream;
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
+	SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
+	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.cbits(), sizes);
+	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, P, tight ? -1.0f : sd, cbase, ccap);
+	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks};
+	const AggSrc x{nullptr, 1, 0, 0};
+	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
+	k_agg_scatter<false, true><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
+	                                                      c1, g, x, nullptr, nullptr, cc, (uint32_t*)recs);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
+	k_agg<8, 1, true><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks,
+	                                            g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
+	uint32_t* hov = (uint32_t*)(ctx->h_pin + kPinCounts);
+	uint32_t* hcp = hov + 16;
+	SYZ_HIP(hipMemcpyAsync(hcp, dc, P * 4, hipMemcpyDeviceToHost, s));
+	SYZ_HIP(hipMemcpyAsync(hov, ovf, 4, hipMemcpyDeviceToHost, s));
+	SYZ_HIP(hipStreamSynchronize(s));
+	if (ctx->timing) {
+		float t0 = 0, t1 = 0;
+		SYZ_HIP(hipEventElapsedTime(&t0, ctx->ev[0], ctx->ev[1]));
+		SYZ_HIP(hipEventElapsedTime(&t1, ctx->ev[1], ctx->ev[2]));
+		st->part_ms += t0;
+		st->probe_ms += t1;
+	}
+	if (*hov) {
+		st->retries++;
+		if (!tight)
+			ctx->cap_sd = ctx->cap_sd * 2 > kCapSdMax ? 0.0f : ctx->cap_sd * 2;
+		return SYZSIG_OK;
+	}
+	uint64_t D = 0;
+	for (uint32_t p = 0; p < P; p++) {
+		if (hcp[p] == kAggOverflow) {
+			st->retries++;
+			return SYZSIG_OK;
+		}
+		D += hcp[p];
+	}
+	st->distinct += D;
+	st->parts = P;
+	st->survivors += D;
+	ctx->agg_distinct_ratio = run_recs ? (double)D / (double)run_recs : 0;
+	out->dist_e = (const uint32_t*)de;
+	out->dist_f = (const uint4*)df;
+	out->cnt = (const uint32_t*)dc;
+	out->nregions = P;
+	out->parts = P;
+	out->D = D;
+	*done = true;
+	return SYZSIG_OK;
+}
+
 // Count, scatter and aggregate (plus the HBM fallback) one run of calls
 // [c0, c1) with level map lm: every distinct element of the run with its level
-// firsts (run serials), in regions of kAggRegion entries.
+// firsts (run serials), in regions of kAggRegion entries.  A triage run tries
+// capped cells first (agg_capped), counted cells are the exact path.
 int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const LevelMap& lm,
                   uint64_t run_recs, syzsig_batch_stats* st, AggOut* out, const AggSrc* xp)
 {
@@ -1363,6 +1582,13 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	if (entry)
 		while (g.ibits > 0 && ((c1 - c0) >> g.ibits) < 2048)
 			g.ibits--;
+	if (!entry && (ctx->cap_sd > 0 || (ctx->agg_dbg & SYZSIG_DEBUG_CAP_SPILL)) &&
+	    !(ctx->agg_dbg & SYZSIG_DEBUG_EXACT_CELLS)) {
+		bool done = false;
+		SYZ_TRY(agg_capped(ctx, b, c0, c1, lm, run_recs, g, st, out, &done));
+		if (done)
+			return SYZSIG_OK;
+	}
 	const uint32_t ilog = g.items_per_chunk_log2();
 	const uint64_t nitems = (c1 - c0 + (1ull << g.ibits) - 1) >> g.ibits;
 	void *recs, *cm, *pm, *de, *df, *dc;
@@ -1384,12 +1610,13 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 		k_agg_count<false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1, g, x, counts);
 	k_agg_scan_chunks<<<P, 1024, 0, s>>>(counts, nitems, ilog, P, offs, offsT, totals);
 	k_agg_scan_totals<<<1, 1024, 0, s>>>(totals, P, rec_base);
+	const CapCells nocap{nullptr, nullptr, nullptr, nullptr, 0};
 	if (entry)
-		k_agg_scatter<true><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1,
-		                                               g, x, offs, rec_base, (uint32_t*)recs);
+		k_agg_scatter<true, false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
+		                                                      c1, g, x, offs, rec_base, nocap, (uint32_t*)recs);
 	else
-		k_agg_scatter<false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1,
-		                                                g, x, offs, rec_base, (uint32_t*)recs);
+		k_agg_scatter<false, false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
+		                                                       c1, g, x, offs, rec_base, nocap, (uint32_t*)recs);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
@@ -1397,19 +1624,8 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
-	{
-		const uint32_t* r = (const uint32_t*)recs;
-		uint32_t* e = (uint32_t*)de;
-		uint4* f = (uint4*)df;
-		uint32_t* c = (uint32_t*)dc;
-		const uint32_t dbg = ctx->agg_dbg;
-		switch (ctx->agg_variant) {
-		case 1: k_agg<4, 2><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
-		case 2: k_agg<4, 3><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
-		case 3: k_agg<8, 2><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;
-		default: k_agg<8, 1><<<P, kAggThreads, 0, s>>>(r, rec_base, offsT, nchunks, g, e, f, c, dbg); break;  // 0, 4, 5
-		}
-	}
+	k_agg<8, 1, false><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr,
+	                                             nchunks, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));

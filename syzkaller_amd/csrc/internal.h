@@ -63,6 +63,9 @@ struct Workspace {
 	size_t size = 0;
 };
 
+// capped cells of the aggregation path (agg.hip): default slack, in standard deviations
+constexpr float kCapSdDefault = 6.0f;
+
 // ctx->h_pin layout
 constexpr size_t kPinMask = 0, kPinPairs = 64, kPinCounts = 1024, kPinBytes = 64 * 1024;
 
@@ -93,6 +96,7 @@ struct syzsig_ctx {
 	int part_mode = 1;                    // 0 = never use the aggregation path (agg.hip)
 	uint32_t agg_parts = 0;               // fixed partition count of the aggregation path (0 = adaptive)
 	double agg_distinct_ratio = 0;        // distinct/records of the last aggregated run (sizes the next)
+	float cap_sd = syz::kCapSdDefault;    // capped-cell slack in standard deviations (agg.hip; 0 = counted cells)
 	uint32_t edge_waves = 4;              // waves per program of k_edge_dedup (4 or 8; SYZSIG_EDGE_WAVES)
 	uint32_t agg_variant = 0;             // k_agg pipeline variant (SYZSIG_AGG_VARIANT; tuning)
 	uint32_t agg_dbg = 0;                 // timing-only experiments (SYZSIG_AGG_DBG; results invalid if set)

@@ -181,6 +181,7 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_agg: mode must be 0..2 and parts 0 or a power of two in 8..2048");
 	ctx->part_mode = mode;
 	ctx->agg_parts = parts;
+	ctx->cap_sd = syz::kCapSdDefault;  // capped cells again, with the default slack
 	return SYZSIG_OK;
 }
 
@@ -189,7 +190,8 @@ int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags)
 	SYZ_LOCK(ctx);
 	if (!ctx)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_debug: ctx is NULL");
-	ctx->agg_dbg = flags & (SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC);  // only the result-preserving flags
+	ctx->agg_dbg = flags & (SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS |
+	                        SYZSIG_DEBUG_CAP_SPILL);  // only the result-preserving flags
 	return SYZSIG_OK;
 }
 

@@ -43,8 +43,9 @@ def oracle_pairs(hs, hcs, hcnt, obits):
     return np.unique((call << np.uint64(32)) | hs[r].astype(np.uint64))
 
 
-def compare(gpu, m0, hb, db, new0=None, ms_hint=None, agg=1, parts=0):
-    """agg: 0 = per-call path, 1 = auto, 2 = aggregation path (parts fixed if > 0)."""
+def compare(gpu, m0, hb, db, new0=None, ms_hint=None, agg=1, parts=0, reset=True):
+    """agg: 0 = per-call path, 1 = auto, 2 = aggregation path (parts fixed if > 0).
+    reset=False keeps the engine's path settings (and its adaptive state) as they are."""
     from syzkaller_amd import signal as S
 
     hs, hcs, hcnt, hprio = hb
@@ -54,11 +55,13 @@ def compare(gpu, m0, hb, db, new0=None, ms_hint=None, agg=1, parts=0):
     ms = S.Serial(*m0).Deserialize(gpu.eng) if m0[0].size else S.Signal.make(ms_hint or 0, gpu.eng)
     ns = S.Serial(*new0).Deserialize(gpu.eng) if new0 is not None else S.Signal(None, gpu.eng)
     pairs = torch.full((int(hcnt.sum()) + 1,), -1, dtype=torch.int64, device=gpu.dev)
-    gpu.eng.set_agg(agg, parts)
+    if reset:
+        gpu.eng.set_agg(agg, parts)
     try:
         bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio, new_pairs=pairs)
     finally:
-        gpu.eng.set_agg(1, 0)
+        if reset:
+            gpu.eng.set_agg(1, 0)
     oms, ons, obits, ocnew = O.triage_batch(m0[0], m0[1], hs, hcs, hcnt, hprio, new0)
     np.testing.assert_array_equal(_u(cnew, np.uint8), ocnew)
     np.testing.assert_array_equal(_u(bits, np.uint32), obits)
@@ -132,6 +135,53 @@ def test_triage_finalize_deferred_path(gpu, case):
         finally:
             gpu.eng.set_debug(0)
         assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
+
+
+@pytest.mark.parametrize("mode", ["capped", "counted", "spill", "hot"])
+def test_triage_cell_layouts(gpu, mode):
+    """Both record layouts of the aggregation path against the oracle: capped
+    cells (default), counted cells (SYZSIG_DEBUG_EXACT_CELLS), capped cells that
+    overflow and are redone counted (SYZSIG_DEBUG_CAP_SPILL), and a batch whose
+    calls repeat one hot element hundreds of times, so that one cell of every
+    chunk overflows its capacity: each batch is redone with counted cells and
+    the slack doubles until capped cells are given up -- every batch exact."""
+    from syzkaller_amd import synth
+    from syzkaller_amd._lib import SYZSIG_DEBUG_CAP_SPILL, SYZSIG_DEBUG_EXACT_CELLS
+
+    if mode == "hot":
+        rng = np.random.default_rng(21)
+        pool = rng.integers(0, 1 << 32, 200_000, dtype=np.uint64).astype(np.uint32)
+        ncalls, per = 2048, 600
+        calls = [np.concatenate([rng.choice(pool, per - 300), np.full(300, 0x12345, np.uint32)]) for _ in range(ncalls)]
+        calls = [rng.permutation(c) for c in calls]
+        hs = np.concatenate(calls).astype(np.uint32)
+        hcnt = np.full(ncalls, per, np.uint32)
+        hcs = (np.arange(ncalls, dtype=np.uint64) * per).astype(np.uint64)
+        hprio = rng.integers(0, 4, ncalls).astype(np.uint8)
+        m0e = np.unique(rng.choice(pool, 20_000))
+        m0 = (m0e, rng.integers(0, 4, m0e.size).astype(np.int8))
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(gpu.dev)  # noqa: E731
+        db = (t(hs, np.int32), t(hcs, np.int64), t(hcnt, np.int32), t(hprio, np.uint8))
+        retries = []
+        gpu.eng.set_agg(2, 128)  # resets the capped-cell slack too
+        for _ in range(4):  # sd 6 -> 12 -> 24 -> counted cells only
+            st = compare(gpu, m0, (hs, hcs, hcnt, hprio), db, agg=2, reset=False)
+            retries.append(st["retries"])
+        gpu.eng.set_agg(1, 0)
+        assert retries[0] == 1 and retries[-1] == 0, retries
+        return
+    cfg = synth.synth_default(skew=1)
+    nprog, cpp = 128, 32
+    cl = synth.call_lengths(nprog, cpp, 2048)
+    m0 = synth.m0(cfg, 2048, 1_000_000)
+    dbg = {"capped": 0, "counted": SYZSIG_DEBUG_EXACT_CELLS, "spill": SYZSIG_DEBUG_CAP_SPILL}[mode]
+    gpu.eng.set_debug(dbg)
+    try:
+        st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl), agg=2)
+    finally:
+        gpu.eng.set_debug(0)
+    assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
+    assert st["retries"] == (1 if mode == "spill" else 0), st
 
 
 def fmix32_inv_np(h):
