@@ -48,7 +48,7 @@ __global__ __launch_bounds__(1024) void k_copy(const uint4* __restrict__ s, uint
 int main(int argc, char** argv)
 {
 	const uint32_t nblk = 256 * (argc > 1 ? atoi(argv[1]) : 2);
-	const uint32_t ncell = 2048, per_blk = ncell * 612;  // ~2.5 MB per block, 612 records per cell
+	const uint64_t per_blk = 2048 * 640;  // ~5.2 MB per block
 	const uint64_t n = (uint64_t)nblk * per_blk;
 	uint32_t *src, *dst;
 	CK(hipMalloc(&src, n * 4));
@@ -67,17 +67,20 @@ int main(int argc, char** argv)
 		CK(hipEventElapsedTime(&ms, a, b));
 	}
 	printf("copy  %.3f ms  %.0f GB/s (r+w)\n", ms, 2.0 * n * 4 / ms / 1e6);
-	const uint32_t pieces[] = {1, 4, 9, 18, 36, 72, 153};
-	for (uint32_t nt = 0; nt < 2; nt++)
+	// open cells per block x piece size (records): the L2 working set is
+	// 32 blocks per XCD x ncell lines
+	const uint32_t ncells[] = {2048, 1024, 512, 256};
+	const uint32_t pieces[] = {9, 18, 36, 16, 32};
+	for (uint32_t ncell : ncells)
 		for (uint32_t piece : pieces) {
 			for (int it = 0; it < 2; it++) {
 				CK(hipEventRecord(a));
-				k_scat<<<nblk, 1024>>>(src, dst, per_blk, ncell, piece, nt);
+				k_scat<<<nblk, 1024>>>(src, dst, (uint32_t)per_blk, ncell, piece, 1);
 				CK(hipEventRecord(b));
 				CK(hipEventSynchronize(b));
 				CK(hipEventElapsedTime(&ms, a, b));
 			}
-			printf("scatter piece %3u nt %u  %.3f ms  %.0f GB/s (r+w)\n", piece, nt, ms, 2.0 * n * 4 / ms / 1e6);
+			printf("scatter ncell %4u piece %3u  %.3f ms  %.0f GB/s (r+w)\n", ncell, piece, ms, 2.0 * n * 4 / ms / 1e6);
 		}
 	return 0;
 }

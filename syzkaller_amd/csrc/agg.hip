@@ -339,24 +339,21 @@ struct CapCells {
 	uint64_t nchunks;
 };
 
-template <bool kEntry, bool kCap>
+template <bool kEntry>
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __restrict__ sigs,
                                                              const uint64_t* __restrict__ call_start,
                                                              const uint32_t* __restrict__ call_len,
                                                              const uint8_t* __restrict__ call_prio, LevelMap lm,
                                                              uint64_t c0, uint64_t c1, AggGeom g, AggSrc x,
                                                              const uint32_t* __restrict__ offs,
-                                                             const uint64_t* __restrict__ rec_base, CapCells cc,
-                                                             uint32_t* recs)
+                                                             const uint64_t* __restrict__ rec_base, uint32_t* recs)
 {
 	constexpr uint32_t kWaves = kAggThreads / 64, kQuota = kAggTile / kWaves, kPer = kQuota / 64;
 	static_assert(kQuota % 64 == 0, "tile quota per wave");
-	static_assert(!(kEntry && kCap), "capped cells are for whole-chunk work items");
 	__shared__ uint32_t t_rec[kAggTile];   // sorted by partition: packed records
 	__shared__ uint16_t t_part[kAggTile];  // ... and their partitions
 	__shared__ uint64_t cur[kAggMaxParts];
 	__shared__ uint32_t hist[kAggMaxParts], pos[kAggMaxParts];
-	__shared__ uint32_t room[kCap ? kAggMaxParts : 1];  // capped: free records left in the cell
 	__shared__ uint64_t c_start[kScatChunkMax];  // the chunk's calls
 	__shared__ uint32_t c_len[kScatChunkMax];
 	__shared__ uint16_t c_meta[kScatChunkMax];
@@ -369,18 +366,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
 	const uint64_t ncalls = c1 - c0, nitems = (ncalls + (1ull << ib) - 1) >> ib;
 	const uint32_t per_t = (P + blockDim.x - 1) / blockDim.x;
-	bool spilled = false;
 	for (uint64_t ch = blockIdx.x; ch < nitems; ch += gridDim.x) {  // ch: work item (of 2^ibits calls)
 		const uint64_t cbeg = ch << ib;
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-			if (kCap) {
-				const uint32_t cap = cc.cap[ch];
-				cur[i] = cc.base[ch] + (uint64_t)i * cap;
-				room[kCap ? i : 0] = cap;
-			} else {
-				cur[i] = rec_base[i] + offs[ch * P + i];
-			}
+			cur[i] = rec_base[i] + offs[ch * P + i];
 			hist[i] = 0;
 		}
 		for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
@@ -480,31 +470,206 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 			n = fetch();
 			__syncthreads();
 			// consecutive threads write consecutive records of one partition's run
-			for (uint32_t d = threadIdx.x; d < nt; d += blockDim.x) {
-				const uint32_t p = t_part[d];
-				if (!kCap || d - pos[p] < room[kCap ? p : 0])
-					recs[cur[p] + d] = t_rec[d];
-				else
-					spilled = true;
-			}
+			for (uint32_t d = threadIdx.x; d < nt; d += blockDim.x)
+				recs[cur[t_part[d]] + d] = t_rec[d];
 			__syncthreads();
 			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
 				cur[i] += pos[i] + hist[i];  // advance by the run
-				if (kCap)
-					room[kCap ? i : 0] -= min(room[kCap ? i : 0], hist[i]);
 				hist[i] = 0;
 			}
 			if (!__syncthreads_or(n != 0))
 				break;
 		}
-		if (kCap) {
-			const uint32_t cap = cc.cap[ch];
-			for (uint32_t i = threadIdx.x; i < P; i += blockDim.x)
-				cc.cnt[(uint64_t)i * cc.nchunks + ch] = cap - room[kCap ? i : 0];
-			__syncthreads();  // room is reset by the next item
-		}
 	}
-	if (kCap && spilled)
+}
+
+// Capped cells written in whole 64-B blocks (the triage runs' scatter).
+// A store costs one memory request per 64-B segment it touches, whatever the
+// bytes: a ~9-record piece of a cell at an arbitrary offset touches ~1.6
+// segments, a whole aligned block one (scripts/mb_scatter.hip: 2.0-2.3 vs
+// 3.4-3.8 TB/s read+write).  So every partition has a write-combining buffer
+// of one block in LDS (2048 x 64 B): records go from registers straight into
+// their partition's buffer (one ds_add_rtn for a slot, one ds_write), and a
+// buffer that fills is written out whole, 16 lanes per block; a record that
+// finds its buffer full waits for the flush (next sub-round).  No tile sort,
+// no scan.  A cell's last partial block is written when its chunk ends.
+constexpr uint32_t kBlk = 16;  // records per written block (64 B)
+
+__global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t* __restrict__ sigs,
+                                                                 const uint64_t* __restrict__ call_start,
+                                                                 const uint32_t* __restrict__ call_len,
+                                                                 const uint8_t* __restrict__ call_prio, LevelMap lm,
+                                                                 uint64_t c0, uint64_t c1, AggGeom g, CapCells cc,
+                                                                 uint32_t* recs, uint32_t dbg)
+{
+	constexpr uint32_t kWaves = kAggThreads / 64, kPer = 12, kQuota = kPer * 64;
+	__shared__ uint32_t buf[kAggMaxParts][kBlk];  // per partition: the block being filled
+	__shared__ uint32_t fillc[kAggMaxParts];       // slots handed out in it (may overshoot kBlk)
+	__shared__ uint32_t written[kAggMaxParts];     // records of the cell written so far
+	__shared__ uint16_t flist[kAggMaxParts];       // partitions whose block filled this sub-round
+	__shared__ uint32_t nfl[2];                    // their count, by sub-round parity
+	__shared__ uint64_t c_start[kScatChunkMax];    // the chunk's calls
+	__shared__ uint32_t c_len[kScatChunkMax];
+	__shared__ uint16_t c_meta[kScatChunkMax];
+	const uint32_t P = 1u << g.pbits, cb = g.cbits();
+	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), grp = lane >> 4, slot = lane & (kBlk - 1);
+	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << cb) - 1) >> cb;
+	bool spilled = false;
+	uint32_t rnd = 0;  // sub-round parity
+	if (threadIdx.x < 2)
+		nfl[threadIdx.x] = 0;
+	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+		const uint64_t cbeg = ch << cb;
+		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << cb);
+		const uint32_t cap = cc.cap[ch];
+		const uint64_t cbase = cc.base[ch];
+		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+			fillc[i] = 0;
+			written[i] = 0;
+		}
+		for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) {
+			const uint64_t c = c0 + cbeg + i;
+			c_start[i] = call_start[c];
+			c_len[i] = call_len[c];
+			c_meta[i] = (uint16_t)g.meta(lm.lvl[call_prio[c]], cbeg + i);
+		}
+		__syncthreads();
+		uint32_t wc = w, wo = 0;  // this wave's walk: local call wc (then +kWaves), offset wo inside it
+		uint32_t ev[kPer], loc[kPer];
+		// issue the loads of this wave's next quota; returns how many records it has
+		auto fetch = [&]() -> uint32_t {
+			uint32_t q = 0;
+			while (q < kQuota && wc < nc) {
+				const uint32_t len = c_len[wc], m = min(kQuota - q, len - wo);
+				const uint32_t tag = ((wc - w) / kWaves) << 24;
+				if (q == 0) {
+#pragma unroll
+					for (uint32_t u = 0; u < kPer; u++)
+						loc[u] = tag | wo;  // clamped default: a valid address
+				}
+#pragma unroll
+				for (uint32_t u = 0; u < kPer; u++) {
+					const uint32_t i = u * 64 + lane;
+					loc[u] = i >= q && i < q + m ? tag | (wo + i - q) : loc[u];
+				}
+				q += m;
+				wo += m;
+				if (wo == len) {
+					wc += kWaves;
+					wo = 0;
+				}
+			}
+			if (q) {
+#pragma unroll
+				for (uint32_t u = 0; u < kPer; u++)
+					ev[u] = __builtin_nontemporal_load(&sigs[c_start[w + (loc[u] >> 24) * kWaves] + (loc[u] & 0xFFFFFFu)]);
+			}
+			return q;
+		};
+		// write out the blocks that filled in this sub-round: 16 lanes per block,
+		// four blocks per lane group in flight
+		auto flush = [&]() {
+			const uint32_t nf = nfl[rnd & 1];
+			if (threadIdx.x == 0)
+				nfl[(rnd + 1) & 1] = 0;  // the next sub-round's list (last read a sub-round ago)
+			for (uint32_t j0 = w * 4 + grp; j0 < nf; j0 += 4 * kWaves * 4) {
+				uint32_t pp[4], wr[4], v[4];
+#pragma unroll
+				for (uint32_t t = 0; t < 4; t++)
+					pp[t] = flist[min(j0 + t * kWaves * 4, nf - 1)];
+#pragma unroll
+				for (uint32_t t = 0; t < 4; t++) {
+					wr[t] = written[pp[t]];
+					v[t] = buf[pp[t]][slot];
+				}
+#pragma unroll
+				for (uint32_t t = 0; t < 4; t++) {
+					if (j0 + t * kWaves * 4 < nf) {
+						if (wr[t] + kBlk > cap)
+							spilled = true;  // the cell is full: the run is redone with counted cells
+						else if (!(dbg & 1))  // dbg & 1: timing only, no block stores
+							recs[cbase + (uint64_t)pp[t] * cap + wr[t] + slot] = v[t];
+					}
+				}
+				__builtin_amdgcn_wave_barrier();
+#pragma unroll
+				for (uint32_t t = 0; t < 4; t++) {
+					if (slot == 0 && j0 + t * kWaves * 4 < nf) {
+						written[pp[t]] = wr[t] + kBlk;
+						fillc[pp[t]] = 0;
+					}
+				}
+			}
+			rnd++;
+		};
+		uint32_t n = fetch();
+		for (;;) {
+			// the tile's records: packed record and partition
+			uint32_t rec[kPer], pt[kPer], pend = 0;
+#pragma unroll
+			for (uint32_t u = 0; u < kPer; u++) {
+				const uint32_t h = fmix32(ev[u]);
+				pt[u] = g.part(h);
+				rec[u] = g.rec(h, c_meta[w + (loc[u] >> 24) * kWaves]);
+				pend |= (uint32_t)(u * 64 + lane < n) << u;
+			}
+			if (dbg & 2)  // timing only: records are loaded and dropped
+				pend = 0;
+			n = fetch();  // the next tile's loads fly while this one is placed
+			for (;;) {
+				// place: a slot in the partition's block (all slot requests in
+				// flight together), or wait for its flush in the next sub-round
+				uint32_t sl[kPer], full = 0;
+#pragma unroll
+				for (uint32_t u = 0; u < kPer; u++)
+					sl[u] = (pend >> u) & 1 ? atomicAdd(&fillc[pt[u]], 1u) : kBlk;
+#pragma unroll
+				for (uint32_t u = 0; u < kPer; u++) {
+					if (sl[u] < kBlk) {
+						buf[pt[u]][sl[u]] = rec[u];
+						pend &= ~(1u << u);
+						full |= (uint32_t)(sl[u] == kBlk - 1) << u;
+					}
+				}
+				// the blocks this lane filled go to the flush list
+				while (__ballot(full != 0)) {
+					const bool has = full != 0;
+					const uint32_t cu = __builtin_ctz(full | (1u << kPer));
+					uint32_t pf = 0;
+#pragma unroll
+					for (uint32_t u = 0; u < kPer; u++)
+						pf = cu == u ? pt[u] : pf;
+					const uint64_t m = __ballot(has);
+					uint32_t base = 0;
+					if (lane == 0)
+						base = atomicAdd(&nfl[rnd & 1], (uint32_t)__popcll(m));
+					base = __shfl(base, 0, 64);
+					if (has)
+						flist[base + lane_rank(m)] = (uint16_t)pf;
+					full &= full - 1;
+				}
+				const bool more = __syncthreads_or(pend != 0);
+				flush();
+				__syncthreads();
+				if (!more)
+					break;
+			}
+			if (!__syncthreads_or(n != 0))
+				break;
+		}
+		// the chunk's last partial block of every cell, and the cell counts
+		for (uint32_t p = w * 4 + grp; p < P; p += kWaves * 4) {
+			const uint32_t c = fillc[p], wr = written[p];
+			if (wr + c > cap)
+				spilled = true;
+			else if (slot < c)
+				recs[cbase + (uint64_t)p * cap + wr + slot] = buf[p][slot];
+			if (slot == 0)
+				cc.cnt[(uint64_t)p * cc.nchunks + ch] = min(wr + c, cap);
+		}
+		__syncthreads();  // fillc/written/buf are reset by the next chunk
+	}
+	if (spilled)
 		*cc.ovf = 1u;
 }
 
@@ -568,16 +733,19 @@ __global__ __launch_bounds__(1024) void k_cell_plan(const uint64_t* __restrict__
 }
 
 // ---------------------------------------------------------------- aggregation
-// One workgroup per partition.  Waves take groups of kAggGroup cells (chunks)
-// from an LDS counter and stream them as 64-record slices: a slice lies in one
-// cell, so its chunk -- and the serial's high bits -- is uniform (scalar).
-// Cell (c, p): counted layout, the partition's records from rec_base[p] with
-// cell offsets offsT[p][.]; capped layout (kCap), cap[c] records from
-// base[c] + p * cap[c] of which cnt[p][c] are written.  Output: the
-// partition's distinct elements and their level firsts at
-// dist_*[p * kAggRegion ...], cnt[p] = how many, or kAggOverflow when they do
-// not fit the LDS table.
-// U slices per lane per batch, D batches in flight ahead of the one absorbed.
+// One workgroup per aggregation partition.  Waves take groups of kAggGroup
+// cells (chunks) from an LDS counter and walk each group as one virtual run.
+// Cell (c, p) of scatter partition p: counted layout, the partition's records
+// from rec_base[p] with cell offsets offsT[p][.]; capped layout (kCap), cap[c]
+// records from base[c] + p * cap[c] of which cnt[p][c] are written.  With
+// sub = 1 scatter partition p is aggregated as two partitions 2p + b, b = the
+// top bit of the records' residual (g.pbits = log2 of the scatter partitions):
+// the two workgroups of p run on one XCD at the same time (blocks 16k + x and
+// 16k + x + 8), so the second read of p's cells is an L2/Infinity-Cache hit.
+// Output: partition p2's distinct elements and their level firsts at
+// dist_*[p2 * kAggRegion ...], cnt[p2] = how many, or kAggOverflow when they
+// do not fit the LDS table.
+// U records per lane per batch, D batches in flight ahead of the one absorbed.
 template <uint32_t U, uint32_t D, bool kCap>
 __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict__ recs,
                                                      const uint64_t* __restrict__ rec_base,
@@ -585,7 +753,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
                                                      const uint64_t* __restrict__ cap_base,
                                                      const uint32_t* __restrict__ cap_len,
                                                      const uint32_t* __restrict__ cap_cnt, uint64_t nchunks, AggGeom g,
-                                                     uint32_t* dist_e, uint4* dist_f, uint32_t* cnt)
+                                                     uint32_t sub, uint32_t* dist_e, uint4* dist_f, uint32_t* cnt)
 {
 	__shared__ uint4 kb[kAggBuckets];  // keys (residuals), 4-slot buckets
 	__shared__ uint32_t fl[4][kAggSlots];
@@ -595,7 +763,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 	__shared__ uint2 q[kAggThreads / 64][64];
 	__shared__ uint32_t s_n, s_ovf, s_out, s_next;
 	const uint32_t* keys = reinterpret_cast<const uint32_t*>(kb);
-	const uint32_t P = 1u << g.pbits, lane = lane_id();
+	const uint32_t pb2 = g.pbits + sub, P2 = 1u << pb2, lane = lane_id();
 	uint2* wq = q[threadIdx.x >> 6];
 	uint32_t qn = 0;  // entries in this wave's queue (uniform)
 	// resolve the queue: find-or-insert each element, then its level first
@@ -603,7 +771,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 		uint32_t ins = 0;
 		if (lane < qn) {
 			const uint2 e = wq[lane];
-			const uint32_t hb = __umulhi(e.x << g.pbits, kAggBuckets);
+			const uint32_t hb = __umulhi(e.x << pb2, kAggBuckets);
 			const uint32_t slot = agg_find_insert(kb, e.x, hb, kb[hb], &s_ovf, ins);
 			if (slot != kAggNoSlot)
 				atomicMin(&fl[e.y >> 24][slot], e.y & 0xFFFFFFu);
@@ -616,7 +784,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 		__builtin_amdgcn_wave_barrier();
 	};
 	const uint64_t ngroups = (nchunks + kAggGroup - 1) / kAggGroup;
-	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
+	for (uint32_t b = blockIdx.x; b < P2; b += gridDim.x) {
+		// p2 = 2 p + half, the halves of p on one XCD (blocks b, b + 8); P2 % 16 == 0 when sub = 1
+		const uint32_t p2 = sub ? ((b & 7) + 8 * (b >> 4)) << 1 | ((b >> 3) & 1) : b, p = p2 >> sub;
 		for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
 			if (i < kAggBuckets)
 				kb[i] = make_uint4(kAggEmpty, kAggEmpty, kAggEmpty, kAggEmpty);
@@ -726,9 +896,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				for (uint32_t u = 0; u < U; u++) {
 					const uint32_t r = buf[u];
 					k[u] = (c[u] << g.cbits()) | g.local(r);
-					key[u] = g.resid(r);
+					key[u] = (r << sub) >> pb2;
 					lv[u] = g.level(r);
-					hb[u] = __umulhi(r & ~((1u << g.pbits) - 1), kAggBuckets);
+					hb[u] = __umulhi((r << sub) & ~((1u << pb2) - 1), kAggBuckets);
 				}
 				// home buckets of all U records in flight together (ds_read_b128 each)
 				uint4 B[U];
@@ -738,16 +908,18 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				bool any_need = false;
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++) {
-					const uint32_t f = bucket_find(B[u], key[u]);
+					// the other half's records (sub = 1) are skipped like found ones without a min
+					const bool mine = !sub || (buf[u] >> 31) == (p2 & 1);
+					const uint32_t f = mine ? bucket_find(B[u], key[u]) : 5;
 					slot[u] = f < 4 ? hb[u] * 4 + f : kAggNoSlot;
-					any_need |= f >= 4;
+					any_need |= f == 4;
 				}
 				// first sight of an element, or a chain past its home bucket: to the
 				// wave's queue (the record's own level first is taken there)
 				if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(any_need) != 0))) {
 #pragma unroll
 					for (uint32_t u = 0; u < U; u++) {
-						const bool nd = slot[u] == kAggNoSlot;
+						const bool nd = slot[u] == kAggNoSlot && (!sub || (buf[u] >> 31) == (p2 & 1));
 						const uint64_t m = __ballot(nd);
 						if (!m)
 							continue;
@@ -788,12 +960,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 		__syncthreads();
 		if (s_ovf) {
 			if (threadIdx.x == 0)
-				cnt[p] = kAggOverflow;
+				cnt[p2] = kAggOverflow;
 			__syncthreads();
 			continue;
 		}
-		// compact the occupied slots, elements restored from (p, residual)
-		const uint32_t hp = p << g.rbits();
+		// compact the occupied slots, elements restored from (p2, residual)
+		const uint32_t hp = p2 << (32 - pb2);
 		for (uint32_t i0 = 0; i0 < kAggSlots; i0 += kAggThreads) {
 			const uint32_t i = i0 + threadIdx.x;
 			const uint32_t key = i < kAggSlots ? keys[i] : kAggEmpty;
@@ -804,14 +976,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				wb = atomicAdd(&s_out, (uint32_t)__popcll(m));
 			wb = __shfl(wb, 0, 64);
 			if (occ) {
-				const uint64_t o = (uint64_t)p * kAggRegion + wb + lane_rank(m);
+				const uint64_t o = (uint64_t)p2 * kAggRegion + wb + lane_rank(m);
 				dist_e[o] = fmix32_inv(hp | key);
 				dist_f[o] = make_uint4(fl[0][i], fl[1][i], fl[2][i], fl[3][i]);
 			}
 		}
 		__syncthreads();
 		if (threadIdx.x == 0)
-			cnt[p] = s_out;
+			cnt[p2] = s_out;
 		__syncthreads();
 	}
 }
@@ -1487,20 +1659,22 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
                       uint64_t run_recs, const AggGeom& g, syzsig_batch_stats* st, AggOut* out, bool* done)
 {
 	*done = false;
-	const uint32_t P = 1u << g.pbits;
-	const uint64_t nchunks = (c1 - c0 + (1ull << g.cbits()) - 1) >> g.cbits();
+	AggGeom gs = g;
+	gs.ibits = gs.cbits();
+	const uint32_t sub = 0, S = 1u << gs.pbits, P = S;
+	const uint64_t nchunks = (c1 - c0 + (1ull << gs.cbits()) - 1) >> gs.cbits();
 	const bool tight = ctx->agg_dbg & SYZSIG_DEBUG_CAP_SPILL;
 	const float sd = tight ? 0.0f : ctx->cap_sd;
-	// upper bound of sum_c P * cap[c] (k_cell_plan): 1.25 records + per cell sd^2 + 128
-	const uint64_t bound = run_recs + run_recs / 4 + nchunks * P * (uint64_t)(sd * sd + 128.0f) + 64;
+	// upper bound of sum_c S * cap[c] (k_cell_plan): 1.25 records + per cell sd^2 + 128
+	const uint64_t bound = run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
 	void *recs, *cm, *de, *df, *dc;
 	SYZ_TRY(ws_get(ctx, 16, bound * 4, &recs));
-	SYZ_TRY(ws_get(ctx, 17, nchunks * 20 + (uint64_t)P * nchunks * 4 + 256, &cm));
+	SYZ_TRY(ws_get(ctx, 17, nchunks * 20 + (uint64_t)S * nchunks * 4 + 256, &cm));
 	uint64_t* sizes = (uint64_t*)cm;
 	uint64_t* cbase = sizes + nchunks;
 	uint32_t* ccap = (uint32_t*)(cbase + nchunks);
 	uint32_t* ccnt = ccap + nchunks;
-	uint32_t* ovf = ccnt + (uint64_t)P * nchunks;
+	uint32_t* ovf = ccnt + (uint64_t)S * nchunks;
 	SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
@@ -1508,18 +1682,17 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
 	SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
-	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.cbits(), sizes);
-	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, P, tight ? -1.0f : sd, cbase, ccap);
+	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, gs.cbits(), sizes);
+	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, tight ? -1.0f : sd, cbase, ccap);
 	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks};
-	const AggSrc x{nullptr, 1, 0, 0};
 	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
-	k_agg_scatter<false, true><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
-	                                                      c1, g, x, nullptr, nullptr, cc, (uint32_t*)recs);
+	k_agg_scatter_blk<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, gs, cc,
+	                                             (uint32_t*)recs, ctx->agg_dbg >> 10);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
 	k_agg<8, 1, true><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks,
-	                                            g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	                                            gs, sub, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -1610,13 +1783,12 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 		k_agg_count<false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, c0, c1, g, x, counts);
 	k_agg_scan_chunks<<<P, 1024, 0, s>>>(counts, nitems, ilog, P, offs, offsT, totals);
 	k_agg_scan_totals<<<1, 1024, 0, s>>>(totals, P, rec_base);
-	const CapCells nocap{nullptr, nullptr, nullptr, nullptr, 0};
 	if (entry)
-		k_agg_scatter<true, false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
-		                                                      c1, g, x, offs, rec_base, nocap, (uint32_t*)recs);
+		k_agg_scatter<true><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1,
+		                                               g, x, offs, rec_base, (uint32_t*)recs);
 	else
-		k_agg_scatter<false, false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
-		                                                       c1, g, x, offs, rec_base, nocap, (uint32_t*)recs);
+		k_agg_scatter<false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1,
+		                                                g, x, offs, rec_base, (uint32_t*)recs);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
@@ -1625,7 +1797,7 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
 	k_agg<8, 1, false><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr,
-	                                             nchunks, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	                                             nchunks, g, 0, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));

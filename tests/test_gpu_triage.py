@@ -137,10 +137,10 @@ def test_triage_finalize_deferred_path(gpu, case):
         assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
 
 
-@pytest.mark.parametrize("mode", ["capped", "counted", "spill", "hot"])
+@pytest.mark.parametrize("mode", ["capped", "capped_split", "counted", "spill", "hot"])
 def test_triage_cell_layouts(gpu, mode):
     """Both record layouts of the aggregation path against the oracle: capped
-    cells (default), counted cells (SYZSIG_DEBUG_EXACT_CELLS), capped cells that
+    cells (default; capped_split: at 2048 partitions), counted cells (SYZSIG_DEBUG_EXACT_CELLS), capped cells that
     overflow and are redone counted (SYZSIG_DEBUG_CAP_SPILL), and a batch whose
     calls repeat one hot element hundreds of times, so that one cell of every
     chunk overflows its capacity: each batch is redone with counted cells and
@@ -174,10 +174,13 @@ def test_triage_cell_layouts(gpu, mode):
     nprog, cpp = 128, 32
     cl = synth.call_lengths(nprog, cpp, 2048)
     m0 = synth.m0(cfg, 2048, 1_000_000)
-    dbg = {"capped": 0, "counted": SYZSIG_DEBUG_EXACT_CELLS, "spill": SYZSIG_DEBUG_CAP_SPILL}[mode]
+    dbg = {"counted": SYZSIG_DEBUG_EXACT_CELLS, "spill": SYZSIG_DEBUG_CAP_SPILL}.get(mode, 0)
+    # capped_split: 2048 partitions (the LDS write-combining buffers at their largest)
+    parts = 2048 if mode == "capped_split" else 0
     gpu.eng.set_debug(dbg)
     try:
-        st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl), agg=2)
+        st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl), agg=2,
+                     parts=parts)
     finally:
         gpu.eng.set_debug(0)
     assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
