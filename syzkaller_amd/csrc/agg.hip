@@ -494,6 +494,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 // finds its buffer full waits for the flush (next sub-round).  No tile sort,
 // no scan.  A cell's last partial block is written when its chunk ends.
 constexpr uint32_t kBlk = 16;  // records per written block (64 B)
+// records per lane per tile, tiles of loads in flight (VGPRs: ~4 kPer * kDepth)
+#ifndef SYZ_SCAT_PER
+#define SYZ_SCAT_PER 12
+#endif
+#ifndef SYZ_SCAT_DEPTH
+#define SYZ_SCAT_DEPTH 1
+#endif
 
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t* __restrict__ sigs,
                                                                  const uint64_t* __restrict__ call_start,
@@ -502,7 +509,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
                                                                  uint64_t c0, uint64_t c1, AggGeom g, CapCells cc,
                                                                  uint32_t* recs, uint32_t dbg)
 {
-	constexpr uint32_t kWaves = kAggThreads / 64, kPer = 12, kQuota = kPer * 64;
+	constexpr uint32_t kWaves = kAggThreads / 64, kPer = SYZ_SCAT_PER, kQuota = kPer * 64, kDepth = SYZ_SCAT_DEPTH;
+	static_assert(kDepth == 1 || kDepth == 2, "tiles in flight");
 	__shared__ uint32_t buf[kAggMaxParts][kBlk];  // per partition: the block being filled
 	__shared__ uint32_t fillc[kAggMaxParts];       // slots handed out in it (may overshoot kBlk)
 	__shared__ uint32_t written[kAggMaxParts];     // records of the cell written so far
@@ -535,9 +543,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 		}
 		__syncthreads();
 		uint32_t wc = w, wo = 0;  // this wave's walk: local call wc (then +kWaves), offset wo inside it
-		uint32_t ev[kPer], loc[kPer];
 		// issue the loads of this wave's next quota; returns how many records it has
-		auto fetch = [&]() -> uint32_t {
+		auto fetch = [&](uint32_t (&ev)[kPer], uint32_t (&loc)[kPer]) -> uint32_t {
 			uint32_t q = 0;
 			while (q < kQuota && wc < nc) {
 				const uint32_t len = c_len[wc], m = min(kQuota - q, len - wo);
@@ -602,8 +609,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			}
 			rnd++;
 		};
-		uint32_t n = fetch();
-		for (;;) {
+		// one tile: pack its records, refill its registers with the tile kDepth
+		// ahead, place the records; returns the refilled tile's record count
+		auto tile = [&](uint32_t (&ev)[kPer], uint32_t (&loc)[kPer], uint32_t n) -> uint32_t {
 			// the tile's records: packed record and partition
 			uint32_t rec[kPer], pt[kPer], pend = 0;
 #pragma unroll
@@ -615,7 +623,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			}
 			if (dbg & 2)  // timing only: records are loaded and dropped
 				pend = 0;
-			n = fetch();  // the next tile's loads fly while this one is placed
+			n = fetch(ev, loc);  // the loads fly while this tile (and the next) are placed
 			for (;;) {
 				// place: a slot in the partition's block (all slot requests in
 				// flight together), or wait for its flush in the next sub-round
@@ -654,8 +662,27 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 				if (!more)
 					break;
 			}
-			if (!__syncthreads_or(n != 0))
-				break;
+			return n;
+		};
+		uint32_t evA[kPer], locA[kPer];
+		uint32_t nA = fetch(evA, locA);
+		if constexpr (kDepth == 1) {
+			for (;;) {
+				nA = tile(evA, locA, nA);
+				if (!__syncthreads_or(nA != 0))
+					break;
+			}
+		} else {  // two register tiles, alternating: A = t, B = t + 1, A refilled with t + 2
+			uint32_t evB[kPer], locB[kPer];
+			uint32_t nB = fetch(evB, locB);
+			for (;;) {
+				nA = tile(evA, locA, nA);
+				if (!__syncthreads_or(nA != 0 || nB != 0))
+					break;
+				nB = tile(evB, locB, nB);
+				if (!__syncthreads_or(nA != 0 || nB != 0))
+					break;
+			}
 		}
 		// the chunk's last partial block of every cell, and the cell counts
 		for (uint32_t p = w * 4 + grp; p < P; p += kWaves * 4) {
@@ -735,16 +762,12 @@ __global__ __launch_bounds__(1024) void k_cell_plan(const uint64_t* __restrict__
 // ---------------------------------------------------------------- aggregation
 // One workgroup per aggregation partition.  Waves take groups of kAggGroup
 // cells (chunks) from an LDS counter and walk each group as one virtual run.
-// Cell (c, p) of scatter partition p: counted layout, the partition's records
-// from rec_base[p] with cell offsets offsT[p][.]; capped layout (kCap), cap[c]
-// records from base[c] + p * cap[c] of which cnt[p][c] are written.  With
-// sub = 1 scatter partition p is aggregated as two partitions 2p + b, b = the
-// top bit of the records' residual (g.pbits = log2 of the scatter partitions):
-// the two workgroups of p run on one XCD at the same time (blocks 16k + x and
-// 16k + x + 8), so the second read of p's cells is an L2/Infinity-Cache hit.
-// Output: partition p2's distinct elements and their level firsts at
-// dist_*[p2 * kAggRegion ...], cnt[p2] = how many, or kAggOverflow when they
-// do not fit the LDS table.
+// Cell (c, p): counted layout, the partition's records from rec_base[p] with
+// cell offsets offsT[p][.]; capped layout (kCap), cap[c] records from
+// base[c] + p * cap[c] of which cnt[p][c] are written.  Output: the
+// partition's distinct elements and their level firsts at
+// dist_*[p * kAggRegion ...], cnt[p] = how many, or kAggOverflow when they do
+// not fit the LDS table.
 // U records per lane per batch, D batches in flight ahead of the one absorbed.
 template <uint32_t U, uint32_t D, bool kCap>
 __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict__ recs,
@@ -753,7 +776,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
                                                      const uint64_t* __restrict__ cap_base,
                                                      const uint32_t* __restrict__ cap_len,
                                                      const uint32_t* __restrict__ cap_cnt, uint64_t nchunks, AggGeom g,
-                                                     uint32_t sub, uint32_t* dist_e, uint4* dist_f, uint32_t* cnt)
+                                                     uint32_t* dist_e, uint4* dist_f, uint32_t* cnt)
 {
 	__shared__ uint4 kb[kAggBuckets];  // keys (residuals), 4-slot buckets
 	__shared__ uint32_t fl[4][kAggSlots];
@@ -763,7 +786,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 	__shared__ uint2 q[kAggThreads / 64][64];
 	__shared__ uint32_t s_n, s_ovf, s_out, s_next;
 	const uint32_t* keys = reinterpret_cast<const uint32_t*>(kb);
-	const uint32_t pb2 = g.pbits + sub, P2 = 1u << pb2, lane = lane_id();
+	const uint32_t P = 1u << g.pbits, lane = lane_id();
 	uint2* wq = q[threadIdx.x >> 6];
 	uint32_t qn = 0;  // entries in this wave's queue (uniform)
 	// resolve the queue: find-or-insert each element, then its level first
@@ -771,7 +794,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 		uint32_t ins = 0;
 		if (lane < qn) {
 			const uint2 e = wq[lane];
-			const uint32_t hb = __umulhi(e.x << pb2, kAggBuckets);
+			const uint32_t hb = __umulhi(e.x << g.pbits, kAggBuckets);
 			const uint32_t slot = agg_find_insert(kb, e.x, hb, kb[hb], &s_ovf, ins);
 			if (slot != kAggNoSlot)
 				atomicMin(&fl[e.y >> 24][slot], e.y & 0xFFFFFFu);
@@ -784,9 +807,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 		__builtin_amdgcn_wave_barrier();
 	};
 	const uint64_t ngroups = (nchunks + kAggGroup - 1) / kAggGroup;
-	for (uint32_t b = blockIdx.x; b < P2; b += gridDim.x) {
-		// p2 = 2 p + half, the halves of p on one XCD (blocks b, b + 8); P2 % 16 == 0 when sub = 1
-		const uint32_t p2 = sub ? ((b & 7) + 8 * (b >> 4)) << 1 | ((b >> 3) & 1) : b, p = p2 >> sub;
+	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
 		for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
 			if (i < kAggBuckets)
 				kb[i] = make_uint4(kAggEmpty, kAggEmpty, kAggEmpty, kAggEmpty);
@@ -896,9 +917,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				for (uint32_t u = 0; u < U; u++) {
 					const uint32_t r = buf[u];
 					k[u] = (c[u] << g.cbits()) | g.local(r);
-					key[u] = (r << sub) >> pb2;
+					key[u] = g.resid(r);
 					lv[u] = g.level(r);
-					hb[u] = __umulhi((r << sub) & ~((1u << pb2) - 1), kAggBuckets);
+					hb[u] = __umulhi(r & ~((1u << g.pbits) - 1), kAggBuckets);
 				}
 				// home buckets of all U records in flight together (ds_read_b128 each)
 				uint4 B[U];
@@ -908,18 +929,16 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				bool any_need = false;
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++) {
-					// the other half's records (sub = 1) are skipped like found ones without a min
-					const bool mine = !sub || (buf[u] >> 31) == (p2 & 1);
-					const uint32_t f = mine ? bucket_find(B[u], key[u]) : 5;
+					const uint32_t f = bucket_find(B[u], key[u]);
 					slot[u] = f < 4 ? hb[u] * 4 + f : kAggNoSlot;
-					any_need |= f == 4;
+					any_need |= f >= 4;
 				}
 				// first sight of an element, or a chain past its home bucket: to the
 				// wave's queue (the record's own level first is taken there)
 				if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(any_need) != 0))) {
 #pragma unroll
 					for (uint32_t u = 0; u < U; u++) {
-						const bool nd = slot[u] == kAggNoSlot && (!sub || (buf[u] >> 31) == (p2 & 1));
+						const bool nd = slot[u] == kAggNoSlot;
 						const uint64_t m = __ballot(nd);
 						if (!m)
 							continue;
@@ -960,12 +979,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 		__syncthreads();
 		if (s_ovf) {
 			if (threadIdx.x == 0)
-				cnt[p2] = kAggOverflow;
+				cnt[p] = kAggOverflow;
 			__syncthreads();
 			continue;
 		}
-		// compact the occupied slots, elements restored from (p2, residual)
-		const uint32_t hp = p2 << (32 - pb2);
+		// compact the occupied slots, elements restored from (p, residual)
+		const uint32_t hp = p << g.rbits();
 		for (uint32_t i0 = 0; i0 < kAggSlots; i0 += kAggThreads) {
 			const uint32_t i = i0 + threadIdx.x;
 			const uint32_t key = i < kAggSlots ? keys[i] : kAggEmpty;
@@ -976,14 +995,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 				wb = atomicAdd(&s_out, (uint32_t)__popcll(m));
 			wb = __shfl(wb, 0, 64);
 			if (occ) {
-				const uint64_t o = (uint64_t)p2 * kAggRegion + wb + lane_rank(m);
+				const uint64_t o = (uint64_t)p * kAggRegion + wb + lane_rank(m);
 				dist_e[o] = fmix32_inv(hp | key);
 				dist_f[o] = make_uint4(fl[0][i], fl[1][i], fl[2][i], fl[3][i]);
 			}
 		}
 		__syncthreads();
 		if (threadIdx.x == 0)
-			cnt[p2] = s_out;
+			cnt[p] = s_out;
 		__syncthreads();
 	}
 }
@@ -1661,7 +1680,7 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	*done = false;
 	AggGeom gs = g;
 	gs.ibits = gs.cbits();
-	const uint32_t sub = 0, S = 1u << gs.pbits, P = S;
+	const uint32_t S = 1u << gs.pbits, P = S;
 	const uint64_t nchunks = (c1 - c0 + (1ull << gs.cbits()) - 1) >> gs.cbits();
 	const bool tight = ctx->agg_dbg & SYZSIG_DEBUG_CAP_SPILL;
 	const float sd = tight ? 0.0f : ctx->cap_sd;
@@ -1692,7 +1711,7 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
 	k_agg<8, 1, true><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks,
-	                                            gs, sub, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	                                            gs, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -1797,7 +1816,7 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
 	k_agg<8, 1, false><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr,
-	                                             nchunks, g, 0, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	                                             nchunks, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
