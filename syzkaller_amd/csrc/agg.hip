@@ -568,11 +568,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			}
 			if (q) {
 #pragma unroll
-				for (uint32_t u = 0; u < kPer; u++) {
-					const uint64_t at = c_start[w + (loc[u] >> 24) * kWaves] + (loc[u] & 0xFFFFFFu);
-					// dbg & 4: timing only, synthetic records instead of loads
-					ev[u] = dbg & 4 ? (uint32_t)at * 0x9E3779B1u : __builtin_nontemporal_load(&sigs[at]);
-				}
+				for (uint32_t u = 0; u < kPer; u++)
+					ev[u] = __builtin_nontemporal_load(&sigs[c_start[w + (loc[u] >> 24) * kWaves] + (loc[u] & 0xFFFFFFu)]);
 			}
 			return q;
 		};

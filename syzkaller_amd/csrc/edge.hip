@@ -90,10 +90,16 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 			r[w] = payload << 1 | any;
 		lds_barrier();
 		uint32_t o = 0;
+		if constexpr (W >= 4) {
 #pragma unroll
-		for (uint32_t i = 0; i < W / 4; i++) {
-			const uint4 a = reinterpret_cast<const uint4*>(r)[i];
-			o |= a.x | a.y | a.z | a.w;
+			for (uint32_t i = 0; i < W / 4; i++) {
+				const uint4 a = reinterpret_cast<const uint4*>(r)[i];
+				o |= a.x | a.y | a.z | a.w;
+			}
+		} else {
+#pragma unroll
+			for (uint32_t i = 0; i < W; i++)
+				o |= r[i];
 		}
 		seq++;
 		row = r;
@@ -294,6 +300,12 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 	if (ctx->edge_waves == 8)
 		k_edge_dedup<8><<<grid, 512, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
+	else if (ctx->edge_waves == 2)
+		k_edge_dedup<2><<<grid, 128, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
+		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
+	else if (ctx->edge_waves == 1)
+		k_edge_dedup<1><<<grid, 64, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
+		                                              nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	else
 		k_edge_dedup<4><<<grid, 256, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);

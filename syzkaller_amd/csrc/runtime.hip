@@ -123,7 +123,7 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 	if (const char* v = getenv("SYZSIG_AGG_DBG"))
 		c->agg_dbg = (uint32_t)atoi(v);
 	if (const char* v = getenv("SYZSIG_EDGE_WAVES"))
-		c->edge_waves = atoi(v) == 8 ? 8 : 4;
+		c->edge_waves = atoi(v) == 8 ? 8 : atoi(v) == 2 ? 2 : atoi(v) == 1 ? 1 : 4;
 	if (const char* v = getenv("SYZSIG_AGG_PARTS")) {
 		const uint32_t n = (uint32_t)atoi(v);
 		if (n >= 8 && n <= 2048 && !(n & (n - 1)))
