@@ -502,15 +502,21 @@ constexpr uint32_t kBlk = 16;  // records per written block (64 B)
 #define SYZ_SCAT_DEPTH 1
 #endif
 
+// Work items of 2^ibits calls own their cells (items = chunks for a triage
+// batch).  kEntry (Minimize): the level comes from each record's own prio
+// (x.elem_prio), and only the records whose element shard x.shard owns are kept.
+template <bool kEntry>
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t* __restrict__ sigs,
                                                                  const uint64_t* __restrict__ call_start,
                                                                  const uint32_t* __restrict__ call_len,
                                                                  const uint8_t* __restrict__ call_prio, LevelMap lm,
-                                                                 uint64_t c0, uint64_t c1, AggGeom g, CapCells cc,
-                                                                 uint32_t* recs, uint32_t dbg)
+                                                                 uint64_t c0, uint64_t c1, AggGeom g, AggSrc x,
+                                                                 CapCells cc, uint32_t* recs, uint32_t dbg)
 {
-	constexpr uint32_t kWaves = kAggThreads / 64, kPer = SYZ_SCAT_PER, kQuota = kPer * 64, kDepth = SYZ_SCAT_DEPTH;
+	constexpr uint32_t kWaves = kAggThreads / 64, kPer = kEntry ? 8 : SYZ_SCAT_PER, kQuota = kPer * 64;
+	constexpr uint32_t kDepth = SYZ_SCAT_DEPTH;
 	static_assert(kDepth == 1 || kDepth == 2, "tiles in flight");
+	static_assert(!kEntry || kDepth == 1, "pv holds one tile's prios");
 	__shared__ uint32_t buf[kAggMaxParts][kBlk];  // per partition: the block being filled
 	__shared__ uint32_t fillc[kAggMaxParts];       // slots handed out in it (may overshoot kBlk)
 	__shared__ uint32_t written[kAggMaxParts];     // records of the cell written so far
@@ -519,16 +525,21 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 	__shared__ uint64_t c_start[kScatChunkMax];    // the chunk's calls
 	__shared__ uint32_t c_len[kScatChunkMax];
 	__shared__ uint16_t c_meta[kScatChunkMax];
-	const uint32_t P = 1u << g.pbits, cb = g.cbits();
+	__shared__ uint8_t s_lvl[kEntry ? 256 : 1];
+	const uint32_t P = 1u << g.pbits, cb = g.cbits(), ib = g.ibits;
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), grp = lane >> 4, slot = lane & (kBlk - 1);
-	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << cb) - 1) >> cb;
+	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << ib) - 1) >> ib;  // work items
 	bool spilled = false;
+	if (kEntry) {
+		for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
+			s_lvl[kEntry ? i : 0] = lm.lvl[i];
+	}
 	uint32_t rnd = 0;  // sub-round parity
 	if (threadIdx.x < 2)
 		nfl[threadIdx.x] = 0;
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-		const uint64_t cbeg = ch << cb;
-		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << cb);
+		const uint64_t cbeg = ch << ib;
+		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
 		const uint32_t cap = cc.cap[ch];
 		const uint64_t cbase = cc.base[ch];
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
@@ -539,10 +550,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			const uint64_t c = c0 + cbeg + i;
 			c_start[i] = call_start[c];
 			c_len[i] = call_len[c];
-			c_meta[i] = (uint16_t)g.meta(lm.lvl[call_prio[c]], cbeg + i);
+			c_meta[i] = (uint16_t)g.meta(kEntry ? 0 : lm.lvl[call_prio[c]], cbeg + i);
 		}
 		__syncthreads();
 		uint32_t wc = w, wo = 0;  // this wave's walk: local call wc (then +kWaves), offset wo inside it
+		uint32_t pv[kEntry ? kPer : 1];  // kEntry: the records' prios (of the last fetch)
 		// issue the loads of this wave's next quota; returns how many records it has
 		auto fetch = [&](uint32_t (&ev)[kPer], uint32_t (&loc)[kPer]) -> uint32_t {
 			uint32_t q = 0;
@@ -568,8 +580,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			}
 			if (q) {
 #pragma unroll
-				for (uint32_t u = 0; u < kPer; u++)
-					ev[u] = __builtin_nontemporal_load(&sigs[c_start[w + (loc[u] >> 24) * kWaves] + (loc[u] & 0xFFFFFFu)]);
+				for (uint32_t u = 0; u < kPer; u++) {
+					const uint64_t at = c_start[w + (loc[u] >> 24) * kWaves] + (loc[u] & 0xFFFFFFu);
+					ev[u] = __builtin_nontemporal_load(&sigs[at]);
+					if (kEntry)
+						pv[kEntry ? u : 0] = (uint8_t)__builtin_nontemporal_load(&x.elem_prio[at]);
+				}
 			}
 			return q;
 		};
@@ -618,8 +634,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			for (uint32_t u = 0; u < kPer; u++) {
 				const uint32_t h = fmix32(ev[u]);
 				pt[u] = g.part(h);
-				rec[u] = g.rec(h, c_meta[w + (loc[u] >> 24) * kWaves]);
-				pend |= (uint32_t)(u * 64 + lane < n) << u;
+				uint32_t meta = c_meta[w + (loc[u] >> 24) * kWaves];
+				if (kEntry)
+					meta |= (uint32_t)s_lvl[pv[kEntry ? u : 0]] << cb;
+				rec[u] = g.rec(h, meta);
+				const bool keep = !kEntry || x.nshards == 1 || owner_of(ev[u], x.nshards) == x.shard;
+				pend |= (uint32_t)(u * 64 + lane < n && keep) << u;
 			}
 			if (dbg & 2)  // timing only: records are loaded and dropped
 				pend = 0;
@@ -760,7 +780,7 @@ __global__ __launch_bounds__(1024) void k_cell_plan(const uint64_t* __restrict__
 }
 
 // ---------------------------------------------------------------- aggregation
-// One workgroup per aggregation partition.  Waves take groups of kAggGroup
+// One workgroup per aggregation partition.  Waves take groups of gsz
 // cells (chunks) from an LDS counter and walk each group as one virtual run.
 // Cell (c, p): counted layout, the partition's records from rec_base[p] with
 // cell offsets offsT[p][.]; capped layout (kCap), cap[c] records from
@@ -776,7 +796,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
                                                      const uint64_t* __restrict__ cap_base,
                                                      const uint32_t* __restrict__ cap_len,
                                                      const uint32_t* __restrict__ cap_cnt, uint64_t nchunks, AggGeom g,
-                                                     uint32_t* dist_e, uint4* dist_f, uint32_t* cnt)
+                                                     uint32_t ilog, uint32_t gsz, uint32_t* dist_e, uint4* dist_f,
+                                                     uint32_t* cnt)
 {
 	__shared__ uint4 kb[kAggBuckets];  // keys (residuals), 4-slot buckets
 	__shared__ uint32_t fl[4][kAggSlots];
@@ -806,7 +827,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 		qn = 0;
 		__builtin_amdgcn_wave_barrier();
 	};
-	const uint64_t ngroups = (nchunks + kAggGroup - 1) / kAggGroup;
+	const uint64_t ngroups = (nchunks + gsz - 1) / gsz;
 	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
 		for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
 			if (i < kAggBuckets)
@@ -829,15 +850,15 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 			gi = __builtin_amdgcn_readfirstlane(__shfl(gi, 0, 64));
 			if (gi >= ngroups || lds_flag(&s_ovf))
 				break;
-			// the group's cells, one per lane 0..kAggGroup-1: first record and
+			// the group's cells, one per lane 0..gsz-1: first record and
 			// records.  The group is walked as one virtual run, cell after cell:
 			// virtual offset v of cell i is record recs[v + delta_i].
-			const uint64_t ch0 = (uint64_t)gi * kAggGroup;
+			const uint64_t ch0 = (uint64_t)gi * gsz;
 			uint64_t lbase = 0;
 			uint32_t llen = 0;
 			{
 				const uint64_t c = ch0 + lane;
-				if (lane < kAggGroup && c < nchunks) {
+				if (lane < gsz && c < nchunks) {
 					if (kCap) {
 						lbase = cap_base[c] + (uint64_t)p * cap_len[c];
 						llen = cap_cnt[(uint64_t)p * nchunks + c];
@@ -847,14 +868,16 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 					}
 				}
 			}
-			uint32_t lvs = llen;  // inclusive scan over lanes 0..kAggGroup-1, then exclusive
+			uint32_t lvs = llen;  // inclusive scan over lanes 0..gsz-1, then exclusive
 #pragma unroll
-			for (uint32_t o = 1; o < kAggGroup; o <<= 1) {
-				const uint32_t y = __shfl_up(lvs, o, 64);
-				if (lane >= o)
-					lvs += y;
+			for (uint32_t o = 1; o < 64; o <<= 1) {
+				if (o < gsz) {
+					const uint32_t y = __shfl_up(lvs, o, 64);
+					if (lane >= o)
+						lvs += y;
+				}
 			}
-			const uint32_t n = __builtin_amdgcn_readlane(lvs, kAggGroup - 1);
+			const uint32_t n = __builtin_amdgcn_readlane(lvs, gsz - 1);
 			if (n == 0)
 				continue;
 			lvs -= llen;
@@ -863,9 +886,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 			// Per batch [o0, o0 + U * 64): the cell of o0 (the last cell starting
 			// at or before it: a non-empty one, as an empty cell shares its
 			// successor's start) and the cells starting inside the batch.
-			auto cells = [&](uint32_t o0, uint32_t& c0, uint32_t& inside) {
-				c0 = (uint32_t)__popcll(__ballot(lane < kAggGroup && lvs <= o0)) - 1;
-				inside = (uint32_t)__ballot(lane < kAggGroup && lvs > o0 && lvs < o0 + U * 64);
+			auto cells = [&](uint32_t o0, uint32_t& c0, uint64_t& inside) {
+				c0 = (uint32_t)__popcll(__ballot(lane < gsz && lvs <= o0)) - 1;
+				inside = __ballot(lane < gsz && lvs > o0 && lvs < o0 + U * 64);
 			};
 			auto delta_of = [&](uint32_t i) -> uint64_t {
 				const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)ldelta, i);
@@ -878,7 +901,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 			// record changes nothing (min is idempotent), so no lane needs a
 			// validity test.
 			auto fetch = [&](uint32_t (&buf)[U], uint32_t o0) {
-				uint32_t c0, inside;
+				uint32_t c0;
+				uint64_t inside;
 				cells(min(o0, nl), c0, inside);  // a prefetch past the group reads its last record
 				const uint64_t d0 = delta_of(c0);
 				uint32_t v[U];
@@ -888,8 +912,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 					v[u] = min(o0 + u * 64 + lane, nl);
 					d[u] = d0;
 				}
-				for (uint32_t m = __builtin_amdgcn_readfirstlane(inside); m; m &= m - 1) {
-					const uint32_t j = __builtin_ctz(m), vs = __builtin_amdgcn_readlane(lvs, j);
+				for (uint64_t m = inside; m; m &= m - 1) {
+					const uint32_t j = __builtin_ctzll(m), vs = __builtin_amdgcn_readlane(lvs, j);
 					const uint64_t dj = delta_of(j);
 #pragma unroll
 					for (uint32_t u = 0; u < U; u++)
@@ -900,15 +924,16 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 					buf[u] = __builtin_nontemporal_load(&recs[v[u] + d[u]]);
 			};
 			auto absorb = [&](const uint32_t (&buf)[U], uint32_t o0) {
-				uint32_t c0, inside;
+				uint32_t c0;
+				uint64_t inside;
 				cells(o0, c0, inside);
 				uint32_t key[U], lv[U], k[U], hb[U], slot[U], c[U];
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++)
 					c[u] = (uint32_t)ch0 + c0;
 				// a uniform loop over the (0-2 typically) cells starting inside the batch
-				for (uint32_t m = __builtin_amdgcn_readfirstlane(inside); m; m &= m - 1) {
-					const uint32_t vs = __builtin_amdgcn_readlane(lvs, __builtin_ctz(m));
+				for (uint64_t m = inside; m; m &= m - 1) {
+					const uint32_t vs = __builtin_amdgcn_readlane(lvs, __builtin_ctzll(m));
 #pragma unroll
 					for (uint32_t u = 0; u < U; u++)
 						c[u] += min(o0 + u * 64 + lane, nl) >= vs;
@@ -916,7 +941,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 #pragma unroll
 				for (uint32_t u = 0; u < U; u++) {
 					const uint32_t r = buf[u];
-					k[u] = (c[u] << g.cbits()) | g.local(r);
+					k[u] = ((c[u] >> ilog) << g.cbits()) | g.local(r);
 					key[u] = g.resid(r);
 					lv[u] = g.level(r);
 					hb[u] = __umulhi(r & ~((1u << g.pbits) - 1), kAggBuckets);
@@ -1668,22 +1693,35 @@ static AggGeom agg_geom_for(syzsig_ctx* ctx, uint64_t nrec, double distinct_hint
 	return g;
 }
 
-// The count-free attempt of a triage run: scatter into capped cells (no count
-// pass, no scan), then aggregate.  *done = false when the run must be redone
-// with counted cells: a cell overflowed (the slack is doubled for the next run,
-// and capped cells are given up past kCapSdMax), or a partition overflowed the
-// LDS table (its HBM fallback reads counted cells).
+// k_agg's cells per wave work item: ~64 items per partition (4 per wave),
+// at least kAggGroup and at most one cell per lane
+static uint32_t agg_group_size(uint64_t ncells)
+{
+	uint32_t gz = kAggGroup;
+	while (gz < 64 && ncells / gz > 64)
+		gz <<= 1;
+	return gz;
+}
+
+// The count-free attempt: scatter into capped cells (no count pass, no scan),
+// then aggregate.  Cells belong to work items of 2^g.ibits calls (chunks for a
+// triage run, smaller items for Minimize: xp != nullptr).  *done = false when
+// the run must be redone with counted cells: a cell overflowed (the slack is
+// doubled for the next run of the kind, and capped cells are given up past
+// kCapSdMax), or a partition overflowed the LDS table (its HBM fallback reads
+// counted cells).
 constexpr float kCapSdMax = 24.0f;
 static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const LevelMap& lm,
-                      uint64_t run_recs, const AggGeom& g, syzsig_batch_stats* st, AggOut* out, bool* done)
+                      uint64_t run_recs, const AggGeom& g, const AggSrc* xp, syzsig_batch_stats* st, AggOut* out,
+                      bool* done)
 {
 	*done = false;
-	AggGeom gs = g;
-	gs.ibits = gs.cbits();
+	const AggGeom gs = g;
 	const uint32_t S = 1u << gs.pbits, P = S;
-	const uint64_t nchunks = (c1 - c0 + (1ull << gs.cbits()) - 1) >> gs.cbits();
+	const uint64_t nchunks = (c1 - c0 + (1ull << gs.ibits) - 1) >> gs.ibits;  // work items
 	const bool tight = ctx->agg_dbg & SYZSIG_DEBUG_CAP_SPILL;
-	const float sd = tight ? 0.0f : ctx->cap_sd;
+	float& slack = xp ? ctx->cap_sd_entry : ctx->cap_sd;
+	const float sd = tight ? 0.0f : slack;
 	// upper bound of sum_c S * cap[c] (k_cell_plan): 1.25 records + per cell sd^2 + 128
 	const uint64_t bound = run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
 	void *recs, *cm, *de, *df, *dc;
@@ -1701,17 +1739,23 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
 	SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
-	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, gs.cbits(), sizes);
+	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, gs.ibits, sizes);
 	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, tight ? -1.0f : sd, cbase, ccap);
 	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks};
 	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
-	k_agg_scatter_blk<<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, gs, cc,
-	                                             (uint32_t*)recs, ctx->agg_dbg >> 10);
+	if (xp)
+		k_agg_scatter_blk<true><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
+		                                                   c1, gs, *xp, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
+	else
+		k_agg_scatter_blk<false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
+		                                                    c1, gs, AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs,
+		                                                    ctx->agg_dbg >> 10);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
 	k_agg<8, 1, true><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks,
-	                                            gs, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	                                            gs, gs.items_per_chunk_log2(), agg_group_size(nchunks),
+	                                            (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -1730,7 +1774,7 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	if (*hov) {
 		st->retries++;
 		if (!tight)
-			ctx->cap_sd = ctx->cap_sd * 2 > kCapSdMax ? 0.0f : ctx->cap_sd * 2;
+			slack = slack * 2 > kCapSdMax ? 0.0f : slack * 2;
 		return SYZSIG_OK;
 	}
 	uint64_t D = 0;
@@ -1744,7 +1788,8 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	st->distinct += D;
 	st->parts = P;
 	st->survivors += D;
-	ctx->agg_distinct_ratio = run_recs ? (double)D / (double)run_recs : 0;
+	if (!xp)
+		ctx->agg_distinct_ratio = run_recs ? (double)D / (double)run_recs : 0;
 	out->dist_e = (const uint32_t*)de;
 	out->dist_f = (const uint4*)df;
 	out->cnt = (const uint32_t*)dc;
@@ -1774,10 +1819,10 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	if (entry)
 		while (g.ibits > 0 && ((c1 - c0) >> g.ibits) < 2048)
 			g.ibits--;
-	if (!entry && (ctx->cap_sd > 0 || (ctx->agg_dbg & SYZSIG_DEBUG_CAP_SPILL)) &&
+	if (((entry ? ctx->cap_sd_entry : ctx->cap_sd) > 0 || (ctx->agg_dbg & SYZSIG_DEBUG_CAP_SPILL)) &&
 	    !(ctx->agg_dbg & SYZSIG_DEBUG_EXACT_CELLS)) {
 		bool done = false;
-		SYZ_TRY(agg_capped(ctx, b, c0, c1, lm, run_recs, g, st, out, &done));
+		SYZ_TRY(agg_capped(ctx, b, c0, c1, lm, run_recs, g, xp, st, out, &done));
 		if (done)
 			return SYZSIG_OK;
 	}
@@ -1816,7 +1861,8 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
 	k_agg<8, 1, false><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr,
-	                                             nchunks, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	                                             nchunks, g, 0, agg_group_size(nchunks), (uint32_t*)de, (uint4*)df,
+	                                             (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));

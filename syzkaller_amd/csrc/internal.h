@@ -97,6 +97,7 @@ struct syzsig_ctx {
 	uint32_t agg_parts = 0;               // fixed partition count of the aggregation path (0 = adaptive)
 	double agg_distinct_ratio = 0;        // distinct/records of the last aggregated run (sizes the next)
 	float cap_sd = syz::kCapSdDefault;    // capped-cell slack in standard deviations (agg.hip; 0 = counted cells)
+	float cap_sd_entry = syz::kCapSdDefault;  // the same for Minimize's runs
 	uint32_t edge_waves = 4;              // waves per program of k_edge_dedup (4 or 8; SYZSIG_EDGE_WAVES)
 	uint32_t agg_variant = 0;             // k_agg pipeline variant (SYZSIG_AGG_VARIANT; tuning)
 	uint32_t agg_dbg = 0;                 // timing-only experiments (SYZSIG_AGG_DBG; results invalid if set)

@@ -181,7 +181,7 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_agg: mode must be 0..2 and parts 0 or a power of two in 8..2048");
 	ctx->part_mode = mode;
 	ctx->agg_parts = parts;
-	ctx->cap_sd = syz::kCapSdDefault;  // capped cells again, with the default slack
+	ctx->cap_sd = ctx->cap_sd_entry = syz::kCapSdDefault;  // capped cells again, with the default slack
 	return SYZSIG_OK;
 }
 
