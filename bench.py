@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI, the product path); gloo only to rehearse N>1 ranks "
                          "sharing fewer GPUs (rank r uses GPU r mod device_count)")
+    ap.add_argument("--ns-hint", type=int, default=4_000_000, help="newSignal size hint (make(Signal, hint))")
     ap.add_argument("--table-hint", type=int, default=0,
                     help="size maxSignal's table for this many entries (default: the library's policy)")
     ap.add_argument("--cpu-threads", type=int, default=16,
@@ -320,7 +321,7 @@ def main():
         sized.Merge(ms)
         ms = sized
     pristine = ms.clone()
-    ns = S.Signal.make(4_000_000, dev.eng)
+    ns = S.Signal.make(a.ns_hint, dev.eng)
     # checkNewSignal's outputs: the calls with new signal, every call's DiffRaw
     # result (pairs), maxSignal and newSignal (per-record bits are not part of
     # the reference's result and are not computed)

@@ -1265,7 +1265,10 @@ __global__ __launch_bounds__(kFinThreads) void k_agg_finalize(const uint32_t* __
 // launch start sits before the first slot that was empty then; a slot seen
 // occupied, or claimed by another element, is occupied at launch end, so the
 // occupied-prefix invariant of every probe sequence still holds.
-constexpr uint32_t kFxThreads = 512, kFxSet = 8192, kFxBuf = 2048, kFxProbe = 64;
+#ifndef SYZ_FX_BUF
+#define SYZ_FX_BUF 2048
+#endif
+constexpr uint32_t kFxThreads = 512, kFxSet = 8192, kFxBuf = SYZ_FX_BUF, kFxProbe = 64;
 enum : int { kFxTaken = 0, kFxClaimed = 1, kFxFull = 2 };
 
 __device__ __forceinline__ int fx_claim(uint32_t* set, uint32_t tag, uint64_t rel)
