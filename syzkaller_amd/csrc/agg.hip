@@ -1979,8 +1979,10 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 	const bool fresh_ns = D && !*ns;
 	if (fresh_ns)
 		SYZ_TRY(syzsig_set_make(ctx, D, ns));
+	// newSignal takes up to D changes per batch: kept at most half full, so its
+	// probe chains stay short in the finalize (0.34 -> 0.28 ms at C2)
 	if (D)
-		SYZ_TRY(set_reserve(*ns, D));
+		SYZ_TRY(set_reserve_load(*ns, D, kTargetLoad));
 	const uint64_t need_pairs = *npairs_io + 4 * D;
 	SYZ_TRY(ws_grow_keep(ctx, 15, need_pairs * 8 + 64, *npairs_io * 8, &pr));
 	*pairs_out = (uint64_t*)pr;

@@ -146,6 +146,7 @@ int counters_fetch(syzsig_ctx* ctx);  // sync + copy to ctx->h_cnt
 uint64_t buckets_for(uint64_t n_entries);
 int set_alloc(syzsig_ctx* ctx, uint64_t nbuckets, syzsig_set** out);
 int set_reserve(syzsig_set* s, uint64_t extra);  // ensure room for len+extra
+int set_reserve_load(syzsig_set* s, uint64_t extra, double load);  // ... at most `load` full
 int set_rehash(syzsig_set* s, uint64_t nbuckets, bool drop_absent);
 int set_ensure_triage_state(syzsig_set* s);
 int merge_pairs_dev(syzsig_ctx* ctx, syzsig_set* dst, const uint64_t* d_pairs, uint64_t n);

@@ -318,8 +318,13 @@ int set_rehash(syzsig_set* s, uint64_t nbuckets, bool drop_absent)
 
 int set_reserve(syzsig_set* s, uint64_t extra)
 {
+	return set_reserve_load(s, extra, kMaxLoad);
+}
+
+int set_reserve_load(syzsig_set* s, uint64_t extra, double load)
+{
 	uint64_t need = s->len + extra;
-	if ((double)need <= kMaxLoad * (double)s->nslots())
+	if ((double)need <= load * (double)s->nslots())
 		return SYZSIG_OK;
 	return set_rehash(s, buckets_for(need), false);
 }
