@@ -66,6 +66,14 @@ constexpr uint32_t kAggTile = 18432;  // records per scatter tile (18 per lane; 
 #define SYZ_AGG_GROUP 8
 #endif
 constexpr uint32_t kAggGroup = SYZ_AGG_GROUP;  // cells per wave work item of k_agg (<= 64)
+// k_agg's record pipeline: U records per lane per batch, D batches in flight ahead
+#ifndef SYZ_AGG_U
+#define SYZ_AGG_U 4
+#endif
+#ifndef SYZ_AGG_D
+#define SYZ_AGG_D 2
+#endif
+constexpr uint32_t kAggU = SYZ_AGG_U, kAggD = SYZ_AGG_D;
 
 static_assert(0x85ebca6bu * 0xa5cb9243u == 1u, "fmix32_inv multiplier");
 static_assert(0xc2b2ae35u * 0x7ed1b41du == 1u, "fmix32_inv multiplier");
@@ -1756,7 +1764,7 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
-	k_agg<8, 1, true><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks,
+	k_agg<kAggU, kAggD, true><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks,
 	                                            gs, gs.items_per_chunk_log2(), agg_group_size(nchunks),
 	                                            (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
@@ -1863,7 +1871,7 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
-	k_agg<8, 1, false><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr,
+	k_agg<kAggU, kAggD, false><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr,
 	                                             nchunks, g, 0, agg_group_size(nchunks), (uint32_t*)de, (uint4*)df,
 	                                             (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
