@@ -502,12 +502,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 // finds its buffer full waits for the flush (next sub-round).  No tile sort,
 // no scan.  A cell's last partial block is written when its chunk ends.
 constexpr uint32_t kBlk = 16;  // records per written block (64 B)
-// records per lane per tile, tiles of loads in flight (VGPRs: ~4 kPer * kDepth)
+// records per lane per tile
 #ifndef SYZ_SCAT_PER
 #define SYZ_SCAT_PER 12
-#endif
-#ifndef SYZ_SCAT_DEPTH
-#define SYZ_SCAT_DEPTH 1
 #endif
 
 // Work items of 2^ibits calls own their cells (items = chunks for a triage
@@ -522,9 +519,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
                                                                  CapCells cc, uint32_t* recs, uint32_t dbg)
 {
 	constexpr uint32_t kWaves = kAggThreads / 64, kPer = kEntry ? 8 : SYZ_SCAT_PER, kQuota = kPer * 64;
-	constexpr uint32_t kDepth = SYZ_SCAT_DEPTH;
-	static_assert(kDepth == 1 || kDepth == 2, "tiles in flight");
-	static_assert(!kEntry || kDepth == 1, "pv holds one tile's prios");
 	__shared__ uint32_t buf[kAggMaxParts][kBlk];  // per partition: the block being filled
 	__shared__ uint32_t fillc[kAggMaxParts];       // slots handed out in it (may overshoot kBlk)
 	__shared__ uint32_t written[kAggMaxParts];     // records of the cell written so far
@@ -633,11 +627,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			}
 			rnd++;
 		};
-		// one tile: pack its records, refill its registers with the tile kDepth
-		// ahead, place the records; returns the refilled tile's record count
-		auto tile = [&](uint32_t (&ev)[kPer], uint32_t (&loc)[kPer], uint32_t n) -> uint32_t {
-			// the tile's records: packed record and partition
-			uint32_t rec[kPer], pt[kPer], pend = 0;
+		// a tile's records: packed record and partition, and the mask of those to place
+		auto pack = [&](const uint32_t (&ev)[kPer], const uint32_t (&loc)[kPer], uint32_t n, uint32_t (&rec)[kPer],
+		                uint32_t (&pt)[kPer]) -> uint32_t {
+			uint32_t pend = 0;
 #pragma unroll
 			for (uint32_t u = 0; u < kPer; u++) {
 				const uint32_t h = fmix32(ev[u]);
@@ -649,68 +642,58 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 				const bool keep = !kEntry || x.nshards == 1 || owner_of(ev[u], x.nshards) == x.shard;
 				pend |= (uint32_t)(u * 64 + lane < n && keep) << u;
 			}
-			if (dbg & 2)  // timing only: records are loaded and dropped
-				pend = 0;
-			n = fetch(ev, loc);  // the loads fly while this tile (and the next) are placed
-			for (;;) {
-				// place: a slot in the partition's block (all slot requests in
-				// flight together), or wait for its flush in the next sub-round
-				uint32_t sl[kPer], full = 0;
+			return dbg & 2 ? 0u : pend;  // dbg & 2: timing only, records loaded and dropped
+		};
+		// one placement pass: a slot in each record's partition block (all slot
+		// requests in flight together), or it waits for the block's flush; the
+		// blocks this lane filled go to the flush list.  Returns what is left.
+		auto place = [&](const uint32_t (&rec)[kPer], const uint32_t (&pt)[kPer], uint32_t pend) -> uint32_t {
+			uint32_t sl[kPer], full = 0;
+#pragma unroll
+			for (uint32_t u = 0; u < kPer; u++)
+				sl[u] = (pend >> u) & 1 ? atomicAdd(&fillc[pt[u]], 1u) : kBlk;
+#pragma unroll
+			for (uint32_t u = 0; u < kPer; u++) {
+				if (sl[u] < kBlk) {
+					buf[pt[u]][sl[u]] = rec[u];
+					pend &= ~(1u << u);
+					full |= (uint32_t)(sl[u] == kBlk - 1) << u;
+				}
+			}
+			while (__ballot(full != 0)) {
+				const bool has = full != 0;
+				const uint32_t cu = __builtin_ctz(full | (1u << kPer));
+				uint32_t pf = 0;
 #pragma unroll
 				for (uint32_t u = 0; u < kPer; u++)
-					sl[u] = (pend >> u) & 1 ? atomicAdd(&fillc[pt[u]], 1u) : kBlk;
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; u++) {
-					if (sl[u] < kBlk) {
-						buf[pt[u]][sl[u]] = rec[u];
-						pend &= ~(1u << u);
-						full |= (uint32_t)(sl[u] == kBlk - 1) << u;
-					}
-				}
-				// the blocks this lane filled go to the flush list
-				while (__ballot(full != 0)) {
-					const bool has = full != 0;
-					const uint32_t cu = __builtin_ctz(full | (1u << kPer));
-					uint32_t pf = 0;
-#pragma unroll
-					for (uint32_t u = 0; u < kPer; u++)
-						pf = cu == u ? pt[u] : pf;
-					const uint64_t m = __ballot(has);
-					uint32_t base = 0;
-					if (lane == 0)
-						base = atomicAdd(&nfl[rnd & 1], (uint32_t)__popcll(m));
-					base = __shfl(base, 0, 64);
-					if (has)
-						flist[base + lane_rank(m)] = (uint16_t)pf;
-					full &= full - 1;
-				}
+					pf = cu == u ? pt[u] : pf;
+				const uint64_t m = __ballot(has);
+				uint32_t base = 0;
+				if (lane == 0)
+					base = atomicAdd(&nfl[rnd & 1], (uint32_t)__popcll(m));
+				base = __shfl(base, 0, 64);
+				if (has)
+					flist[base + lane_rank(m)] = (uint16_t)pf;
+				full &= full - 1;
+			}
+			return pend;
+		};
+		uint32_t ev[kPer], loc[kPer];
+		uint32_t n = fetch(ev, loc);
+		for (;;) {
+			uint32_t rec[kPer], pt[kPer];
+			uint32_t pend = pack(ev, loc, n, rec, pt);
+			n = fetch(ev, loc);  // the next tile's loads fly while this one is placed
+			for (;;) {
+				pend = place(rec, pt, pend);
 				const bool more = __syncthreads_or(pend != 0);
 				flush();
 				__syncthreads();
 				if (!more)
 					break;
 			}
-			return n;
-		};
-		uint32_t evA[kPer], locA[kPer];
-		uint32_t nA = fetch(evA, locA);
-		if constexpr (kDepth == 1) {
-			for (;;) {
-				nA = tile(evA, locA, nA);
-				if (!__syncthreads_or(nA != 0))
-					break;
-			}
-		} else {  // two register tiles, alternating: A = t, B = t + 1, A refilled with t + 2
-			uint32_t evB[kPer], locB[kPer];
-			uint32_t nB = fetch(evB, locB);
-			for (;;) {
-				nA = tile(evA, locA, nA);
-				if (!__syncthreads_or(nA != 0 || nB != 0))
-					break;
-				nB = tile(evB, locB, nB);
-				if (!__syncthreads_or(nA != 0 || nB != 0))
-					break;
-			}
+			if (!__syncthreads_or(n != 0))
+				break;
 		}
 		// the chunk's last partial block of every cell, and the cell counts
 		for (uint32_t p = w * 4 + grp; p < P; p += kWaves * 4) {
