@@ -345,6 +345,7 @@ struct CapCells {
 	uint32_t* cnt;         // [P][nchunks] records in cell (c, p)
 	uint32_t* ovf;         // set to 1 by a cell overflow
 	uint64_t nchunks;
+	uint32_t* dummy;       // one 64-B line per block: the target of stores that are not made
 };
 
 template <bool kEntry>
@@ -501,7 +502,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 // buffer that fills is written out whole, 16 lanes per block; a record that
 // finds its buffer full waits for the flush (next sub-round).  No tile sort,
 // no scan.  A cell's last partial block is written when its chunk ends.
-constexpr uint32_t kBlk = 16;  // records per written block (64 B)
+constexpr uint32_t kBlk = 16;            // records per written block (64 B)
+constexpr uint32_t kDummyLines = 2048;  // CapCells::dummy lines
 // records per lane per tile
 #ifndef SYZ_SCAT_PER
 #define SYZ_SCAT_PER 12
@@ -520,8 +522,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 {
 	constexpr uint32_t kWaves = kAggThreads / 64, kPer = kEntry ? 8 : SYZ_SCAT_PER, kQuota = kPer * 64;
 	__shared__ uint32_t buf[kAggMaxParts][kBlk];  // per partition: the block being filled
-	__shared__ uint32_t fillc[kAggMaxParts];       // slots handed out in it (may overshoot kBlk)
-	__shared__ uint32_t written[kAggMaxParts];     // records of the cell written so far
+	__shared__ uint32_t fillc[kAggMaxParts + 1];   // slots handed out in it (may overshoot kBlk)
+	__shared__ uint32_t written[kAggMaxParts + 1]; // records of the cell written so far (+ a spare)
 	__shared__ uint16_t flist[kAggMaxParts];       // partitions whose block filled this sub-round
 	__shared__ uint32_t nfl[2];                    // their count, by sub-round parity
 	__shared__ uint64_t c_start[kScatChunkMax];    // the chunk's calls
@@ -597,11 +599,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			const uint32_t nf = nfl[rnd & 1];
 			if (threadIdx.x == 0)
 				nfl[(rnd + 1) & 1] = 0;  // the next sub-round's list (last read a sub-round ago)
-			for (uint32_t j0 = w * 4 + grp; j0 < nf; j0 += 4 * kWaves * 4) {
+			// a uniform loop; a lane group past the list stores its block to this
+			// block's dummy line instead (a store without a branch)
+			for (uint32_t jb = 0; jb < nf; jb += 4 * kWaves * 4) {
 				uint32_t pp[4], wr[4], v[4];
 #pragma unroll
 				for (uint32_t t = 0; t < 4; t++)
-					pp[t] = flist[min(j0 + t * kWaves * 4, nf - 1)];
+					pp[t] = flist[min(jb + t * kWaves * 4 + w * 4 + grp, nf - 1)];
 #pragma unroll
 				for (uint32_t t = 0; t < 4; t++) {
 					wr[t] = written[pp[t]];
@@ -609,19 +613,19 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 				}
 #pragma unroll
 				for (uint32_t t = 0; t < 4; t++) {
-					if (j0 + t * kWaves * 4 < nf) {
-						if (wr[t] + kBlk > cap)
-							spilled = true;  // the cell is full: the run is redone with counted cells
-						else if (!(dbg & 1))  // dbg & 1: timing only, no block stores
-							recs[cbase + (uint64_t)pp[t] * cap + wr[t] + slot] = v[t];
-					}
+					const bool ok = jb + t * kWaves * 4 + w * 4 + grp < nf, fits = wr[t] + kBlk <= cap;
+					spilled |= ok && !fits;  // the cell is full: the run is redone with counted cells
+					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp[t] * cap + wr[t]
+					                         : cc.dummy + (blockIdx.x % kDummyLines) * kBlk;
+					d[slot] = v[t];
 				}
 				__builtin_amdgcn_wave_barrier();
+				if (slot == 0) {  // (a group past the list updates the spare entry kAggMaxParts)
 #pragma unroll
-				for (uint32_t t = 0; t < 4; t++) {
-					if (slot == 0 && j0 + t * kWaves * 4 < nf) {
-						written[pp[t]] = wr[t] + kBlk;
-						fillc[pp[t]] = 0;
+					for (uint32_t t = 0; t < 4; t++) {
+						const uint32_t q = jb + t * kWaves * 4 + w * 4 + grp < nf ? pp[t] : kAggMaxParts;
+						written[q] = wr[t] + kBlk;
+						fillc[q] = 0;
 					}
 				}
 			}
@@ -1719,7 +1723,7 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	// upper bound of sum_c S * cap[c] (k_cell_plan): 1.25 records + per cell sd^2 + 128
 	const uint64_t bound = run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
 	void *recs, *cm, *de, *df, *dc;
-	SYZ_TRY(ws_get(ctx, 16, bound * 4, &recs));
+	SYZ_TRY(ws_get(ctx, 16, (bound + kDummyLines * kBlk) * 4, &recs));
 	SYZ_TRY(ws_get(ctx, 17, nchunks * 20 + (uint64_t)S * nchunks * 4 + 256, &cm));
 	uint64_t* sizes = (uint64_t*)cm;
 	uint64_t* cbase = sizes + nchunks;
@@ -1735,7 +1739,7 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
 	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, gs.ibits, sizes);
 	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, tight ? -1.0f : sd, cbase, ccap);
-	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks};
+	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
 	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
 	if (xp)
 		k_agg_scatter_blk<true><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
