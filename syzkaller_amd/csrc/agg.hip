@@ -530,8 +530,21 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 	__shared__ uint32_t c_len[kScatChunkMax];
 	__shared__ uint16_t c_meta[kScatChunkMax];
 	__shared__ uint8_t s_lvl[kEntry ? 256 : 1];
+	__shared__ uint32_t s_or[2][kWaves];
 	const uint32_t P = 1u << g.pbits, cb = g.cbits(), ib = g.ibits;
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), grp = lane >> 4, slot = lane & (kBlk - 1);
+	// Workgroup OR in one barrier (__syncthreads_or takes three): every wave
+	// writes its flag to a row, all read the row; two rows alternate, so a row
+	// is rewritten only after every wave passed the barrier of the call between.
+	uint32_t seq = 0;
+	auto wg_or = [&](bool pred) -> bool {
+		uint32_t* r = s_or[seq++ & 1];
+		const bool any = __ballot(pred) != 0;
+		if (lane == 0)
+			r[w] = any;
+		__syncthreads();
+		return __ballot(r[lane & (kWaves - 1)] != 0) != 0;  // lane i reads wave i's flag
+	};
 	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << ib) - 1) >> ib;  // work items
 	bool spilled = false;
 	if (kEntry) {
@@ -690,13 +703,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			n = fetch(ev, loc);  // the next tile's loads fly while this one is placed
 			for (;;) {
 				pend = place(rec, pt, pend);
-				const bool more = __syncthreads_or(pend != 0);
+				const bool more = wg_or(pend != 0);
 				flush();
-				__syncthreads();
 				if (!more)
 					break;
+				__syncthreads();
 			}
-			if (!__syncthreads_or(n != 0))
+			if (!wg_or(n != 0))  // (its barrier also ends the last flush)
 				break;
 		}
 		// the chunk's last partial block of every cell, and the cell counts
