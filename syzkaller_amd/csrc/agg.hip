@@ -508,6 +508,9 @@ constexpr uint32_t kDummyLines = 2048;  // CapCells::dummy lines
 #ifndef SYZ_SCAT_PER
 #define SYZ_SCAT_PER 12
 #endif
+#ifndef SYZ_SCAT_PER_ENTRY  // (Minimize: the prios take registers too)
+#define SYZ_SCAT_PER_ENTRY 10
+#endif
 
 // Work items of 2^ibits calls own their cells (items = chunks for a triage
 // batch).  kEntry (Minimize): the level comes from each record's own prio
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
                                                                  uint64_t c0, uint64_t c1, AggGeom g, AggSrc x,
                                                                  CapCells cc, uint32_t* recs, uint32_t dbg)
 {
-	constexpr uint32_t kWaves = kAggThreads / 64, kPer = kEntry ? 8 : SYZ_SCAT_PER, kQuota = kPer * 64;
+	constexpr uint32_t kWaves = kAggThreads / 64, kPer = kEntry ? SYZ_SCAT_PER_ENTRY : SYZ_SCAT_PER, kQuota = kPer * 64;
 	__shared__ uint32_t buf[kAggMaxParts][kBlk];  // per partition: the block being filled
 	__shared__ uint32_t fillc[kAggMaxParts + 1];   // slots handed out in it (may overshoot kBlk)
 	__shared__ uint32_t written[kAggMaxParts + 1]; // records of the cell written so far (+ a spare)
