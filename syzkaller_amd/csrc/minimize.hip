@@ -113,17 +113,28 @@ __global__ __launch_bounds__(256) void k_min_prio_mask(const uint8_t* __restrict
 	};
 	const uint64_t n16 = ((uintptr_t)prios & 15) ? 0 : n / 16;
 	const uint4* p16 = reinterpret_cast<const uint4*>(prios);
-	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
-		const uint4 v = p16[i];
-		const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-		if (((v.x | v.y | v.z | v.w) & 0xE0E0E0E0u) == 0) {  // every byte < 32
+	// four 16-B loads in flight per thread (one at a time leaves the stream
+	// latency-bound); a load past the end re-reads element 0, which is harmless
+	// for a set of values
+	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n16; i += 4 * stride) {
+		uint4 vv[4];
 #pragma unroll
-			for (uint32_t k = 0; k < 16; k++)
-				lo |= 1u << ((w[k >> 2] >> ((k & 3) * 8)) & 31);
-		} else {
+		for (uint32_t j = 0; j < 4; j++)
+			vv[j] = p16[i + j * stride < n16 ? i + j * stride : 0];
 #pragma unroll
-			for (uint32_t k = 0; k < 16; k++)
-				add_slow((w[k >> 2] >> ((k & 3) * 8)) & 0xFF);
+		for (uint32_t j = 0; j < 4; j++) {
+			const uint4 v = vv[j];
+			const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+			if (((v.x | v.y | v.z | v.w) & 0xE0E0E0E0u) == 0) {  // every byte < 32
+#pragma unroll
+				for (uint32_t k = 0; k < 16; k++)
+					lo |= 1u << ((w[k >> 2] >> ((k & 3) * 8)) & 31);
+			} else {
+#pragma unroll
+				for (uint32_t k = 0; k < 16; k++)
+					add_slow((w[k >> 2] >> ((k & 3) * 8)) & 0xFF);
+			}
 		}
 	}
 	for (uint64_t i = n16 * 16 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
