@@ -164,6 +164,27 @@ int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, const 
                               const int8_t* d_prios, uint64_t nctx, uint32_t nshards, uint32_t shard,
                               uint64_t hint_distinct, uint8_t* d_keep, uint64_t* n_out);
 
+/* Minimize split by data (one process per GPU): part `part` of
+ * `nparts` takes a contiguous range of the contexts in sort order (Len desc,
+ * index asc), cut at about total/nparts entries per part, and reads only those
+ * contexts' entries.  It aggregates them per element and writes one winner
+ * record per distinct element of its range,
+ *     e << 32 | (prio ^ 0x80) << 24 | (0xFFFFFF - rank)
+ * (rank = the context's position in the global sort order; the max of the low
+ * 32 bits over the parts is argmax (prio, -rank), the reference's winner),
+ * grouped by owner_of(e, nshards) into d_send (send_cap >= the part's entries
+ * suffices); send_counts[g] = records for owner g, packed at their exclusive
+ * prefix sum.  nshards <= 64; at most 4 distinct prios per part. */
+int syzsig_minimize_split_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, const uint32_t* d_elems,
+                              const int8_t* d_prios, uint64_t nctx, uint32_t nparts, uint32_t part, uint32_t nshards,
+                              uint64_t hint_distinct, uint64_t* d_send, uint64_t send_cap, uint64_t* send_counts);
+/* Owner side of the split: the winner records every part sent to this owner
+ * (d_recs, any order) -> the max per element -> d_keep[i] = 1 iff context i
+ * wins one of them.  The OR (max) of d_keep over the owners is
+ * syzsig_minimize_dev's d_keep; *n_out = this owner's count. */
+int syzsig_minimize_resolve_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, uint64_t nctx, const uint64_t* d_recs,
+                                uint64_t nrec, uint8_t* d_keep, uint64_t* n_out);
+
 /* ---- pkg/cover/cover.go:7-30: type Cover map[uint32]struct{} ----
  * A Cover is a syzsig_set whose entries all carry prio 0.  Merge(raw)
  * (cover.go:9-18) allocates a NULL *cov even when n == 0, then inserts every
@@ -359,6 +380,11 @@ typedef struct {
 	uint64_t seed;
 	uint32_t nblocks_log2, region_log2, nsys, skew, restart_log2;
 	uint32_t errno_permille, any_permille, bad_pc_ppm;
+	/* 1: SURVEY 8(d)'s global walk -- each call starts at a uniform block and
+	 * walks b <- (4b + 1 + r%4) mod 2^nblocks_log2 with no restarts (region_log2,
+	 * nsys, skew and restart_log2 then only pick the call's prio draw); M0's
+	 * known elements are that walk's whole edge universe. */
+	uint32_t global_walk;
 } syzsig_synth_cfg;
 
 void syzsig_synth_default(syzsig_synth_cfg* cfg);

@@ -35,7 +35,8 @@ class CorruptedSerial(SyzsigError):
 class SynthCfg(ctypes.Structure):
     _fields_ = [("seed", c_uint64), ("nblocks_log2", c_uint32), ("region_log2", c_uint32),
                 ("nsys", c_uint32), ("skew", c_uint32), ("restart_log2", c_uint32),
-                ("errno_permille", c_uint32), ("any_permille", c_uint32), ("bad_pc_ppm", c_uint32)]
+                ("errno_permille", c_uint32), ("any_permille", c_uint32), ("bad_pc_ppm", c_uint32),
+                ("global_walk", c_uint32)]
 
 
 class Batch(ctypes.Structure):
@@ -94,6 +95,9 @@ SIGNATURES = {
     "syzsig_minimize": (c_int, [_P, _P, _P, _P, c_uint64, c_uint64, _P, POINTER(c_uint64)]),
     "syzsig_minimize_dev": (c_int, [_P, _P, _P, _P, c_uint64, c_uint64, _P, POINTER(c_uint64)]),
     "syzsig_minimize_shard_dev": (c_int, [_P, _P, _P, _P, c_uint64, c_uint32, c_uint32, c_uint64, _P, POINTER(c_uint64)]),
+    "syzsig_minimize_split_dev": (c_int, [_P, _P, _P, _P, c_uint64, c_uint32, c_uint32, c_uint32, c_uint64, _P,
+                                          c_uint64, _P]),
+    "syzsig_minimize_resolve_dev": (c_int, [_P, _P, c_uint64, _P, c_uint64, _P, POINTER(c_uint64)]),
     "syzsig_check_new_signal": (c_int, [_P, _PP, _PP, _P, c_uint64, _P, _P, _P, c_uint32, _P,
                                         POINTER(c_uint32), _P]),
     "syzsig_triage_batch": (c_int, [_P, _P, _PP, POINTER(Batch), POINTER(BatchStats)]),

@@ -800,26 +800,47 @@ __global__ __launch_bounds__(1024) void k_cell_plan(const uint64_t* __restrict__
 // dist_*[p * kAggRegion ...], cnt[p] = how many, or kAggOverflow when they do
 // not fit the LDS table.
 // U records per lane per batch, D batches in flight ahead of the one absorbed.
+// The LDS of one aggregation workgroup: keys (residuals) in 4-slot buckets,
+// the level firsts, and per wave the records whose element was not in its
+// home bucket (first sight, or a probe chain), gathered across batches and
+// resolved 64 at a time with every lane busy: (residual, level << 24 | serial).
+struct AggLds {
+	uint4 kb[kAggBuckets];
+	uint32_t fl[4][kAggSlots];
+	uint2 q[kAggThreads / 64][64];
+	uint32_t s_n, s_ovf, s_out, s_next;
+};
+
+// Where the records of one partition are (see k_agg).
+struct AggCells {
+	const uint32_t* recs;
+	const uint64_t* rec_base;  // counted layout
+	const uint32_t* offsT;
+	const uint64_t* cap_base;  // capped layout
+	const uint32_t* cap_len;
+	const uint32_t* cap_cnt;
+	uint64_t nchunks;
+	uint32_t ilog, gsz;
+};
+
+// Aggregate partition p into the LDS table (every thread of the workgroup;
+// ends with a barrier).  Returns false when its distinct elements overflow
+// the table (s_ovf).
 template <uint32_t U, uint32_t D, bool kCap>
-__global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict__ recs,
-                                                     const uint64_t* __restrict__ rec_base,
-                                                     const uint32_t* __restrict__ offsT,
-                                                     const uint64_t* __restrict__ cap_base,
-                                                     const uint32_t* __restrict__ cap_len,
-                                                     const uint32_t* __restrict__ cap_cnt, uint64_t nchunks, AggGeom g,
-                                                     uint32_t ilog, uint32_t gsz, uint32_t* dist_e, uint4* dist_f,
-                                                     uint32_t* cnt)
+__device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCells& x, const AggGeom& g)
 {
-	__shared__ uint4 kb[kAggBuckets];  // keys (residuals), 4-slot buckets
-	__shared__ uint32_t fl[4][kAggSlots];
-	// per wave: records whose element was not in its home bucket (first sight,
-	// or a probe chain), gathered across batches and resolved 64 at a time
-	// with every lane busy: (residual, level << 24 | serial)
-	__shared__ uint2 q[kAggThreads / 64][64];
-	__shared__ uint32_t s_n, s_ovf, s_out, s_next;
-	const uint32_t* keys = reinterpret_cast<const uint32_t*>(kb);
-	const uint32_t P = 1u << g.pbits, lane = lane_id();
-	uint2* wq = q[threadIdx.x >> 6];
+	uint4* kb = L.kb;
+	auto& fl = L.fl;
+	const uint32_t* __restrict__ recs = x.recs;
+	const uint64_t* __restrict__ rec_base = x.rec_base;
+	const uint32_t* __restrict__ offsT = x.offsT;
+	const uint64_t* __restrict__ cap_base = x.cap_base;
+	const uint32_t* __restrict__ cap_len = x.cap_len;
+	const uint32_t* __restrict__ cap_cnt = x.cap_cnt;
+	const uint64_t nchunks = x.nchunks;
+	const uint32_t ilog = x.ilog, gsz = x.gsz;
+	const uint32_t lane = lane_id();
+	uint2* wq = L.q[threadIdx.x >> 6];
 	uint32_t qn = 0;  // entries in this wave's queue (uniform)
 	// resolve the queue: find-or-insert each element, then its level first
 	auto flush_queue = [&]() {
@@ -827,193 +848,213 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 		if (lane < qn) {
 			const uint2 e = wq[lane];
 			const uint32_t hb = __umulhi(e.x << g.pbits, kAggBuckets);
-			const uint32_t slot = agg_find_insert(kb, e.x, hb, kb[hb], &s_ovf, ins);
+			const uint32_t slot = agg_find_insert(kb, e.x, hb, kb[hb], &L.s_ovf, ins);
 			if (slot != kAggNoSlot)
 				atomicMin(&fl[e.y >> 24][slot], e.y & 0xFFFFFFu);
 		}
 		// inserts counted per flush (overflow = more than kAggLimit distinct)
 		const uint32_t n_ins = (uint32_t)wave_sum_u64(ins);
-		if (n_ins && lane == 0 && atomicAdd(&s_n, n_ins) + n_ins > kAggLimit)
-			lds_flag_set(&s_ovf);
+		if (n_ins && lane == 0 && atomicAdd(&L.s_n, n_ins) + n_ins > kAggLimit)
+			lds_flag_set(&L.s_ovf);
 		qn = 0;
 		__builtin_amdgcn_wave_barrier();
 	};
 	const uint64_t ngroups = (nchunks + gsz - 1) / gsz;
+	for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
+		if (i < kAggBuckets)
+			kb[i] = make_uint4(kAggEmpty, kAggEmpty, kAggEmpty, kAggEmpty);
+		fl[0][i] = fl[1][i] = fl[2][i] = fl[3][i] = kAggNone;
+	}
+	if (threadIdx.x == 0) {
+		L.s_n = 0;
+		L.s_ovf = 0;
+		L.s_out = 0;
+		L.s_next = 0;
+	}
+	__syncthreads();
+	const uint32_t* ot = offsT + (uint64_t)p * (nchunks + 1);
+	// no barrier inside: a wave leaves early once overflow is flagged
+	for (;;) {
+		uint32_t gi = 0;
+		if (lane == 0)
+			gi = atomicAdd(&L.s_next, 1u);
+		gi = __builtin_amdgcn_readfirstlane(__shfl(gi, 0, 64));
+		if (gi >= ngroups || lds_flag(&L.s_ovf))
+			break;
+		// the group's cells, one per lane 0..gsz-1: first record and
+		// records.  The group is walked as one virtual run, cell after cell:
+		// virtual offset v of cell i is record recs[v + delta_i].
+		const uint64_t ch0 = (uint64_t)gi * gsz;
+		uint64_t lbase = 0;
+		uint32_t llen = 0;
+		{
+			const uint64_t c = ch0 + lane;
+			if (lane < gsz && c < nchunks) {
+				if (kCap) {
+					lbase = cap_base[c] + (uint64_t)p * cap_len[c];
+					llen = cap_cnt[(uint64_t)p * nchunks + c];
+				} else {
+					lbase = rec_base[p] + ot[c];
+					llen = ot[c + 1] - ot[c];
+				}
+			}
+		}
+		uint32_t lvs = llen;  // inclusive scan over lanes 0..gsz-1, then exclusive
+#pragma unroll
+		for (uint32_t o = 1; o < 64; o <<= 1) {
+			if (o < gsz) {
+				const uint32_t y = __shfl_up(lvs, o, 64);
+				if (lane >= o)
+					lvs += y;
+			}
+		}
+		const uint32_t n = __builtin_amdgcn_readlane(lvs, gsz - 1);
+		if (n == 0)
+			continue;
+		lvs -= llen;
+		const uint64_t ldelta = lbase - lvs;
+		const uint32_t nl = n - 1;
+		// Per batch [o0, o0 + U * 64): the cell of o0 (the last cell starting
+		// at or before it: a non-empty one, as an empty cell shares its
+		// successor's start) and the cells starting inside the batch.
+		auto cells = [&](uint32_t o0, uint32_t& c0, uint64_t& inside) {
+			c0 = (uint32_t)__popcll(__ballot(lane < gsz && lvs <= o0)) - 1;
+			inside = __ballot(lane < gsz && lvs > o0 && lvs < o0 + U * 64);
+		};
+		auto delta_of = [&](uint32_t i) -> uint64_t {
+			const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)ldelta, i);
+			const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(ldelta >> 32), i);
+			return (uint64_t)hi << 32 | lo;
+		};
+		// Records stream through registers one batch ahead of the LDS work,
+		// ping-ponging between register buffers.  Loads are unconditional:
+		// lanes past the group re-read its last record -- a second copy of a
+		// record changes nothing (min is idempotent), so no lane needs a
+		// validity test.
+		auto fetch = [&](uint32_t (&buf)[U], uint32_t o0) {
+			uint32_t c0;
+			uint64_t inside;
+			cells(min(o0, nl), c0, inside);  // a prefetch past the group reads its last record
+			const uint64_t d0 = delta_of(c0);
+			uint32_t v[U];
+			uint64_t d[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++) {
+				v[u] = min(o0 + u * 64 + lane, nl);
+				d[u] = d0;
+			}
+			for (uint64_t m = inside; m; m &= m - 1) {
+				const uint32_t j = __builtin_ctzll(m), vs = __builtin_amdgcn_readlane(lvs, j);
+				const uint64_t dj = delta_of(j);
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					d[u] = v[u] >= vs ? dj : d[u];
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++)
+				buf[u] = __builtin_nontemporal_load(&recs[v[u] + d[u]]);
+		};
+		auto absorb = [&](const uint32_t (&buf)[U], uint32_t o0) {
+			uint32_t c0;
+			uint64_t inside;
+			cells(o0, c0, inside);
+			uint32_t key[U], lv[U], k[U], hb[U], slot[U], c[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++)
+				c[u] = (uint32_t)ch0 + c0;
+			// a uniform loop over the (0-2 typically) cells starting inside the batch
+			for (uint64_t m = inside; m; m &= m - 1) {
+				const uint32_t vs = __builtin_amdgcn_readlane(lvs, __builtin_ctzll(m));
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					c[u] += min(o0 + u * 64 + lane, nl) >= vs;
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++) {
+				const uint32_t r = buf[u];
+				k[u] = ((c[u] >> ilog) << g.cbits()) | g.local(r);
+				key[u] = g.resid(r);
+				lv[u] = g.level(r);
+				hb[u] = __umulhi(r & ~((1u << g.pbits) - 1), kAggBuckets);
+			}
+			// home buckets of all U records in flight together (ds_read_b128 each)
+			uint4 B[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++)
+				B[u] = kb[hb[u]];
+			bool any_need = false;
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++) {
+				const uint32_t f = bucket_find(B[u], key[u]);
+				slot[u] = f < 4 ? hb[u] * 4 + f : kAggNoSlot;
+				any_need |= f >= 4;
+			}
+			// first sight of an element, or a chain past its home bucket: to the
+			// wave's queue (the record's own level first is taken there)
+			if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(any_need) != 0))) {
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++) {
+					const bool nd = slot[u] == kAggNoSlot;
+					const uint64_t m = __ballot(nd);
+					if (!m)
+						continue;
+					const uint32_t c = (uint32_t)__popcll(m);
+					if (qn + c > 64)
+						flush_queue();
+					if (nd)
+						wq[qn + lane_rank(m)] = make_uint2(key[u], (lv[u] << 24) | k[u]);
+					qn += c;
+				}
+				__builtin_amdgcn_wave_barrier();
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < U; u++)
+				if (slot[u] != kAggNoSlot)
+					atomicMin(&fl[lv[u]][slot[u]], k[u]);
+		};
+		// a ring of D + 1 register buffers, rotated by full unrolling (static
+		// indices: no register moves that would wait for the prefetch)
+		uint32_t buf[D + 1][U];
+#pragma unroll
+		for (uint32_t d = 0; d < D; d++)
+			fetch(buf[d], d * U * 64);
+		bool more = true;
+		for (uint32_t o0 = 0; more;) {
+#pragma unroll
+			for (uint32_t t = 0; t <= D; t++) {
+				if (more) {
+					fetch(buf[(t + D) % (D + 1)], o0 + D * U * 64);
+					absorb(buf[t], o0);
+					o0 += U * 64;
+					more = o0 < n && !lds_flag(&L.s_ovf);
+				}
+			}
+		}
+	}
+	flush_queue();  // every record is absorbed before the barrier
+	__syncthreads();
+	return !L.s_ovf;
+}
+
+// ---------------------------------------------------------------- aggregation
+// One workgroup per aggregation partition.  Waves take groups of gsz
+// cells (chunks) from an LDS counter and walk each group as one virtual run.
+// Cell (c, p): counted layout, the partition's records from rec_base[p] with
+// cell offsets offsT[p][.]; capped layout (kCap), cap[c] records from
+// base[c] + p * cap[c] of which cnt[p][c] are written.  Output: the
+// partition's distinct elements and their level firsts at
+// dist_*[p * kAggRegion ...], cnt[p] = how many, or kAggOverflow when they do
+// not fit the LDS table.
+// U records per lane per batch, D batches in flight ahead of the one absorbed.
+template <uint32_t U, uint32_t D, bool kCap>
+__global__ __launch_bounds__(kAggThreads) void k_agg(AggCells x, AggGeom g, uint32_t* dist_e, uint4* dist_f,
+                                                     uint32_t* cnt)
+{
+	__shared__ AggLds L;
+	const uint32_t* keys = reinterpret_cast<const uint32_t*>(L.kb);
+	const uint32_t P = 1u << g.pbits, lane = lane_id();
 	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
-		for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
-			if (i < kAggBuckets)
-				kb[i] = make_uint4(kAggEmpty, kAggEmpty, kAggEmpty, kAggEmpty);
-			fl[0][i] = fl[1][i] = fl[2][i] = fl[3][i] = kAggNone;
-		}
-		if (threadIdx.x == 0) {
-			s_n = 0;
-			s_ovf = 0;
-			s_out = 0;
-			s_next = 0;
-		}
-		__syncthreads();
-		const uint32_t* ot = offsT + (uint64_t)p * (nchunks + 1);
-		// no barrier inside: a wave leaves early once overflow is flagged
-		for (;;) {
-			uint32_t gi = 0;
-			if (lane == 0)
-				gi = atomicAdd(&s_next, 1u);
-			gi = __builtin_amdgcn_readfirstlane(__shfl(gi, 0, 64));
-			if (gi >= ngroups || lds_flag(&s_ovf))
-				break;
-			// the group's cells, one per lane 0..gsz-1: first record and
-			// records.  The group is walked as one virtual run, cell after cell:
-			// virtual offset v of cell i is record recs[v + delta_i].
-			const uint64_t ch0 = (uint64_t)gi * gsz;
-			uint64_t lbase = 0;
-			uint32_t llen = 0;
-			{
-				const uint64_t c = ch0 + lane;
-				if (lane < gsz && c < nchunks) {
-					if (kCap) {
-						lbase = cap_base[c] + (uint64_t)p * cap_len[c];
-						llen = cap_cnt[(uint64_t)p * nchunks + c];
-					} else {
-						lbase = rec_base[p] + ot[c];
-						llen = ot[c + 1] - ot[c];
-					}
-				}
-			}
-			uint32_t lvs = llen;  // inclusive scan over lanes 0..gsz-1, then exclusive
-#pragma unroll
-			for (uint32_t o = 1; o < 64; o <<= 1) {
-				if (o < gsz) {
-					const uint32_t y = __shfl_up(lvs, o, 64);
-					if (lane >= o)
-						lvs += y;
-				}
-			}
-			const uint32_t n = __builtin_amdgcn_readlane(lvs, gsz - 1);
-			if (n == 0)
-				continue;
-			lvs -= llen;
-			const uint64_t ldelta = lbase - lvs;
-			const uint32_t nl = n - 1;
-			// Per batch [o0, o0 + U * 64): the cell of o0 (the last cell starting
-			// at or before it: a non-empty one, as an empty cell shares its
-			// successor's start) and the cells starting inside the batch.
-			auto cells = [&](uint32_t o0, uint32_t& c0, uint64_t& inside) {
-				c0 = (uint32_t)__popcll(__ballot(lane < gsz && lvs <= o0)) - 1;
-				inside = __ballot(lane < gsz && lvs > o0 && lvs < o0 + U * 64);
-			};
-			auto delta_of = [&](uint32_t i) -> uint64_t {
-				const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)ldelta, i);
-				const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(ldelta >> 32), i);
-				return (uint64_t)hi << 32 | lo;
-			};
-			// Records stream through registers one batch ahead of the LDS work,
-			// ping-ponging between register buffers.  Loads are unconditional:
-			// lanes past the group re-read its last record -- a second copy of a
-			// record changes nothing (min is idempotent), so no lane needs a
-			// validity test.
-			auto fetch = [&](uint32_t (&buf)[U], uint32_t o0) {
-				uint32_t c0;
-				uint64_t inside;
-				cells(min(o0, nl), c0, inside);  // a prefetch past the group reads its last record
-				const uint64_t d0 = delta_of(c0);
-				uint32_t v[U];
-				uint64_t d[U];
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++) {
-					v[u] = min(o0 + u * 64 + lane, nl);
-					d[u] = d0;
-				}
-				for (uint64_t m = inside; m; m &= m - 1) {
-					const uint32_t j = __builtin_ctzll(m), vs = __builtin_amdgcn_readlane(lvs, j);
-					const uint64_t dj = delta_of(j);
-#pragma unroll
-					for (uint32_t u = 0; u < U; u++)
-						d[u] = v[u] >= vs ? dj : d[u];
-				}
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++)
-					buf[u] = __builtin_nontemporal_load(&recs[v[u] + d[u]]);
-			};
-			auto absorb = [&](const uint32_t (&buf)[U], uint32_t o0) {
-				uint32_t c0;
-				uint64_t inside;
-				cells(o0, c0, inside);
-				uint32_t key[U], lv[U], k[U], hb[U], slot[U], c[U];
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++)
-					c[u] = (uint32_t)ch0 + c0;
-				// a uniform loop over the (0-2 typically) cells starting inside the batch
-				for (uint64_t m = inside; m; m &= m - 1) {
-					const uint32_t vs = __builtin_amdgcn_readlane(lvs, __builtin_ctzll(m));
-#pragma unroll
-					for (uint32_t u = 0; u < U; u++)
-						c[u] += min(o0 + u * 64 + lane, nl) >= vs;
-				}
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++) {
-					const uint32_t r = buf[u];
-					k[u] = ((c[u] >> ilog) << g.cbits()) | g.local(r);
-					key[u] = g.resid(r);
-					lv[u] = g.level(r);
-					hb[u] = __umulhi(r & ~((1u << g.pbits) - 1), kAggBuckets);
-				}
-				// home buckets of all U records in flight together (ds_read_b128 each)
-				uint4 B[U];
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++)
-					B[u] = kb[hb[u]];
-				bool any_need = false;
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++) {
-					const uint32_t f = bucket_find(B[u], key[u]);
-					slot[u] = f < 4 ? hb[u] * 4 + f : kAggNoSlot;
-					any_need |= f >= 4;
-				}
-				// first sight of an element, or a chain past its home bucket: to the
-				// wave's queue (the record's own level first is taken there)
-				if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(any_need) != 0))) {
-#pragma unroll
-					for (uint32_t u = 0; u < U; u++) {
-						const bool nd = slot[u] == kAggNoSlot;
-						const uint64_t m = __ballot(nd);
-						if (!m)
-							continue;
-						const uint32_t c = (uint32_t)__popcll(m);
-						if (qn + c > 64)
-							flush_queue();
-						if (nd)
-							wq[qn + lane_rank(m)] = make_uint2(key[u], (lv[u] << 24) | k[u]);
-						qn += c;
-					}
-					__builtin_amdgcn_wave_barrier();
-				}
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++)
-					if (slot[u] != kAggNoSlot)
-						atomicMin(&fl[lv[u]][slot[u]], k[u]);
-			};
-			// a ring of D + 1 register buffers, rotated by full unrolling (static
-			// indices: no register moves that would wait for the prefetch)
-			uint32_t buf[D + 1][U];
-#pragma unroll
-			for (uint32_t d = 0; d < D; d++)
-				fetch(buf[d], d * U * 64);
-			bool more = true;
-			for (uint32_t o0 = 0; more;) {
-#pragma unroll
-				for (uint32_t t = 0; t <= D; t++) {
-					if (more) {
-						fetch(buf[(t + D) % (D + 1)], o0 + D * U * 64);
-						absorb(buf[t], o0);
-						o0 += U * 64;
-						more = o0 < n && !lds_flag(&s_ovf);
-					}
-				}
-			}
-		}
-		flush_queue();  // every record is absorbed before the barrier
-		__syncthreads();
-		if (s_ovf) {
+		if (!agg_partition<U, D, kCap>(L, p, x, g)) {
 			if (threadIdx.x == 0)
 				cnt[p] = kAggOverflow;
 			__syncthreads();
@@ -1028,17 +1069,17 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(const uint32_t* __restrict_
 			const uint64_t m = __ballot(occ);
 			uint32_t wb = 0;
 			if (lane == 0 && m)
-				wb = atomicAdd(&s_out, (uint32_t)__popcll(m));
+				wb = atomicAdd(&L.s_out, (uint32_t)__popcll(m));
 			wb = __shfl(wb, 0, 64);
 			if (occ) {
 				const uint64_t o = (uint64_t)p * kAggRegion + wb + lane_rank(m);
 				dist_e[o] = fmix32_inv(hp | key);
-				dist_f[o] = make_uint4(fl[0][i], fl[1][i], fl[2][i], fl[3][i]);
+				dist_f[o] = make_uint4(L.fl[0][i], L.fl[1][i], L.fl[2][i], L.fl[3][i]);
 			}
 		}
 		__syncthreads();
 		if (threadIdx.x == 0)
-			cnt[p] = s_out;
+			cnt[p] = L.s_out;
 		__syncthreads();
 	}
 }
@@ -1560,6 +1601,250 @@ __global__ __launch_bounds__(256) void k_fin_deferred(const uint32_t* __restrict
 		ns_deferred(def_ns, def_ns_cnt, ns_slots, ns_bmask, ctr, gridDim.x - kDeferBlocks, blockIdx.x - kDeferBlocks);
 }
 
+// ---------------------------------------------------------------- fused
+// The fast path of a triage run: aggregation and finalize in one launch.  A
+// workgroup aggregates partition p in its LDS table (agg_partition), takes
+// the distinct elements into registers (slot t + k * 1024 of the table for
+// thread t), and then resolves them exactly as k_agg_finalize_x does --
+// maxSignal and newSignal slice p without device-scope atomics, claims in an
+// LDS set, pairs through an LDS buffer -- with the freed table as its LDS.  The
+// distinct lists never go to HBM, and the random slice probes of one
+// workgroup overlap the LDS-bound aggregation of the others.  Tables are
+// reserved for the run's largest possible distinct count before the launch,
+// so nothing here waits for the host.  A partition whose distinct elements
+// overflow the LDS table commits nothing (cnt[p] = kAggOverflow; the host
+// aggregates it in HBM afterwards: partitions hold disjoint elements, so
+// the order of commits does not matter); a spilled cell (*spill, set by the
+// scatter) makes every workgroup commit nothing and the run is redone.
+struct FinArgs {
+	LevelMap lm;
+	uint64_t c0;
+	uint64_t* slots;
+	uint64_t bmask;
+	uint32_t ms_shift;
+	uint64_t* ns_slots;
+	uint64_t ns_bmask;
+	uint32_t ns_shift;
+	uint8_t* call_new;
+	uint64_t* pairs;
+	unsigned long long* npairs;
+	unsigned long long* ctr;
+	uint32_t* def_e;
+	uint4* def_f;
+	unsigned long long* def_cnt;
+	uint64_t* def_ns;
+	unsigned long long* def_ns_cnt;
+	const uint32_t* spill;
+	uint32_t dbg;
+};
+
+#ifndef SYZ_AF_ILP
+#define SYZ_AF_ILP 2
+#endif
+constexpr uint32_t kAfBuf = 8192;                                          // pair buffer (64 KB of the freed LDS)
+constexpr uint32_t kAfPer = (kAggSlots + kAggThreads - 1) / kAggThreads;  // table slots per thread
+constexpr uint32_t kAfIlp = SYZ_AF_ILP;                                    // elements resolved together
+static_assert(sizeof(AggLds) >= kFxSet * 4 + kAfBuf * 8, "the finalize reuses the aggregation LDS");
+static_assert(kAfPer % kAfIlp == 0, "finalize rounds");
+
+template <uint32_t U, uint32_t D>
+__global__ __launch_bounds__(kAggThreads) void k_agg_fin(AggCells x, AggGeom g, FinArgs fa, uint32_t* cnt)
+{
+	__shared__ AggLds L;
+	__shared__ uint32_t s_n;
+	__shared__ unsigned long long s_base;
+	uint32_t* claim = reinterpret_cast<uint32_t*>(&L);
+	uint64_t* buf = reinterpret_cast<uint64_t*>(claim + kFxSet);
+	const uint32_t* keys = reinterpret_cast<const uint32_t*>(L.kb);
+	const uint32_t P = 1u << g.pbits;
+	if (*fa.spill)
+		return;  // a cell overflowed: the run is redone with counted cells, nothing committed
+	uint32_t inserted = 0, changed = 0, ns_ins = 0, distinct = 0, novf = 0;  // (per thread: < 2^32)
+	auto flush = [&](uint32_t nb) {  // every thread; nb = s_n read after a barrier
+		nb = min(nb, kAfBuf);
+		if (threadIdx.x == 0)
+			s_base = atomicAdd(fa.npairs, (unsigned long long)nb);
+		__syncthreads();
+		for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x)
+			fa.pairs[s_base + t] = buf[t];
+		__syncthreads();
+		if (threadIdx.x == 0)
+			s_n = 0;
+		__syncthreads();
+	};
+	auto emit = [&](uint64_t v) {
+		const uint32_t k = atomicAdd(&s_n, 1u);
+		if (k < kAfBuf)
+			buf[k] = v;
+		else
+			fa.pairs[atomicAdd(fa.npairs, 1ull)] = v;
+	};
+	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
+		if (!agg_partition<U, D, true>(L, p, x, g)) {
+			if (threadIdx.x == 0) {
+				cnt[p] = kAggOverflow;
+				novf++;
+			}
+			__syncthreads();
+			continue;
+		}
+		// this thread's distinct elements into registers, elements restored from (p, residual)
+		const uint32_t hp = p << g.rbits();
+		uint32_t ge[kAfPer];
+		uint4 gf[kAfPer];
+		uint32_t valid = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < kAfPer; k++) {
+			const uint32_t i = threadIdx.x + k * kAggThreads;
+			const uint32_t key = i < kAggSlots ? keys[i] : kAggEmpty;
+			valid |= (uint32_t)(key != kAggEmpty) << k;
+			ge[k] = fmix32_inv(hp | key);
+			gf[k] = i < kAggSlots ? make_uint4(L.fl[0][i], L.fl[1][i], L.fl[2][i], L.fl[3][i])
+			                      : make_uint4(kAggNone, kAggNone, kAggNone, kAggNone);
+		}
+		distinct += __popc(valid);
+		if (threadIdx.x == 0)
+			cnt[p] = (uint32_t)L.s_n;  // (the table's insert count: the partition's distinct elements)
+		__syncthreads();  // the table is read: its LDS is the claim set and the pair buffer now
+		for (uint32_t i = threadIdx.x; i < kFxSet; i += blockDim.x)
+			claim[i] = 0;
+		if (threadIdx.x == 0)
+			s_n = 0;
+		__syncthreads();
+		const uint64_t ms0 = (uint64_t)p << fa.ms_shift, ms1 = (uint64_t)(p + 1) << fa.ms_shift;
+		const uint64_t ns0 = (uint64_t)p << fa.ns_shift, ns1 = (uint64_t)(p + 1) << fa.ns_shift;
+#pragma unroll
+		for (uint32_t k0 = 0; k0 < kAfPer; k0 += kAfIlp) {
+			int top[kAfIlp];
+			Bucket bm[kAfIlp], bn[kAfIlp];
+#pragma unroll
+			for (uint32_t j = 0; j < kAfIlp; j++) {
+				const uint32_t k = k0 + j;
+				const uint32_t f[4] = {gf[k].x, gf[k].y, gf[k].z, gf[k].w};
+				top[j] = -1;
+#pragma unroll
+				for (int l = 0; l < 4; l++)
+					if (((valid >> k) & 1) && l < (int)fa.lm.n && f[l] != kAggNone)
+						top[j] = l;
+				if (top[j] >= 0) {
+					bm[j] = load_bucket(fa.slots + (home_bucket(ge[k], fa.bmask) << kBucketShift));
+					bn[j] = load_bucket(fa.ns_slots + (home_bucket(ge[k], fa.ns_bmask) << kBucketShift));
+				}
+			}
+#pragma unroll
+			for (uint32_t j = 0; j < kAfIlp; j++) {
+				if (top[j] < 0)
+					continue;
+				const uint32_t k = k0 + j, e = ge[k];
+				const uint32_t f[4] = {gf[k].x, gf[k].y, gf[k].z, gf[k].w};
+				const int8_t Pv = fa.lm.val[top[j]];
+				const uint64_t word = make_slot(e, Pv);
+				uint64_t old = 0;
+				// (dbg & 32, tests: defer every walk that leaves the home bucket)
+				const uint64_t hm = home_bucket(e, fa.bmask), hn = home_bucket(e, fa.ns_bmask);
+				const int64_t idx = fx_walk(fa.slots, hm, fa.dbg & 32 ? hm + 1 : ms1, ms0 << kBucketShift, e, bm[j],
+				                            claim, 0, old);
+				if (idx < 0) {  // the atomic path takes the whole element
+					const uint64_t d = atomicAdd(fa.def_cnt, 1ull);
+					fa.def_e[d] = e;
+					fa.def_f[d] = gf[k];
+					continue;
+				}
+				const bool present = slot_live(old);
+				const int p0 = present ? (int)slot_prio(old) : -1000;
+				if ((int)Pv <= p0)
+					continue;  // (a claimed slot always has Pv > p0)
+				fa.slots[idx] = word;  // the block's own slice: no other writer
+				inserted += !present;
+				changed++;
+				uint64_t nold = 0;
+				const int64_t nidx = fx_walk(fa.ns_slots, hn, fa.dbg & 32 ? hn + 1 : ns1, ns0 << kBucketShift, e,
+				                             bn[j], claim, 1, nold);
+				if (nidx < 0) {
+					fa.def_ns[atomicAdd(fa.def_ns_cnt, 1ull)] = ((uint64_t)e << 32) | prio_biased(Pv);
+				} else if (nold == 0 || nold < word) {
+					fa.ns_slots[nidx] = word;
+					ns_ins += nold == 0;
+				}
+				// the staircase: first records of strictly rising level above M0[e]
+				uint32_t mk = kAggNone;
+#pragma unroll
+				for (int l = 3; l >= 0; l--) {
+					if (l > top[j] || f[l] == kAggNone)
+						continue;
+					if ((int)fa.lm.val[l] <= p0)
+						break;
+					if (f[l] < mk) {
+						mk = f[l];
+						const uint64_t c = fa.c0 + f[l];
+						fa.call_new[c] = 1;
+						emit((c << 32) | e);
+					}
+				}
+			}
+			__syncthreads();
+			const uint32_t nb = s_n;
+			if (nb > (k0 + kAfIlp < kAfPer ? kAfBuf / 2 : 0))
+				flush(nb);
+		}
+	}
+	block_count(&fa.ctr[kCntInserted], inserted);
+	block_count(&fa.ctr[kCntChanged], changed);
+	block_count(&fa.ctr[kCntAux], ns_ins);
+	block_count(&fa.ctr[kCntDistinct], distinct);
+	block_count(&fa.ctr[kCntAggOvf], novf);
+}
+
+// Fallback of the fused path: the records of the partitions that overflowed
+// the LDS table, aggregated in one HBM table keyed by h (as k_agg_global) from
+// their capped cells.  One wave per (partition, chunk).
+__global__ __launch_bounds__(256) void k_agg_global_cap(const uint32_t* __restrict__ recs,
+                                                        const uint64_t* __restrict__ cap_base,
+                                                        const uint32_t* __restrict__ cap_len,
+                                                        const uint32_t* __restrict__ cap_cnt, uint64_t nchunks,
+                                                        AggGeom g, const uint32_t* __restrict__ ovl, uint32_t novl,
+                                                        uint32_t* gkeys, uint32_t* gfl, uint64_t C,
+                                                        unsigned long long* err)
+{
+	const uint32_t lane = lane_id();
+	const uint64_t items = (uint64_t)novl * nchunks, nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	uint64_t bad = 0;
+	for (uint64_t it = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); it < items; it += nwaves) {
+		const uint32_t p = ovl[it / nchunks];
+		const uint64_t c = it % nchunks;
+		const uint32_t* pr = recs + cap_base[c] + (uint64_t)p * cap_len[c];
+		const uint32_t n = cap_cnt[(uint64_t)p * nchunks + c];
+		for (uint32_t j = lane; j < n; j += 64) {
+			const uint32_t r = pr[j];
+			const uint32_t k = ((uint32_t)c << g.cbits()) | g.local(r), l = g.level(r);
+			const uint32_t h = (p << g.rbits()) | g.resid(r);
+			uint64_t i = C;
+			if (h != kAggEmpty) {
+				i = fmix32(h ^ 0x632BE5ABu) & (C - 1);
+				for (uint64_t step = 0;; step++) {
+					uint32_t key = gkeys[i];
+					if (key == kAggEmpty) {
+						key = atomicCAS(&gkeys[i], kAggEmpty, h);
+						if (key == kAggEmpty)
+							break;
+					}
+					if (key == h)
+						break;
+					i = (i + 1) & (C - 1);
+					if (step >= C) {
+						bad++;
+						i = ~0ull;
+						break;
+					}
+				}
+			}
+			if (i != ~0ull)
+				atomicMin(&gfl[(uint64_t)l * (C + 1) + i], k);
+		}
+	}
+	block_count(err, bad);
+}
+
 // ---------------------------------------------------------------- new bits
 __device__ __forceinline__ uint64_t pair_hash(uint64_t k)
 {
@@ -1767,9 +2052,9 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
-	k_agg<kAggU, kAggD, true><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks,
-	                                            gs, gs.items_per_chunk_log2(), agg_group_size(nchunks),
-	                                            (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, gs.items_per_chunk_log2(),
+	                  agg_group_size(nchunks)};
+	k_agg<kAggU, kAggD, true><<<P, kAggThreads, 0, s>>>(xc, gs, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -1874,9 +2159,9 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
-	k_agg<kAggU, kAggD, false><<<P, kAggThreads, 0, s>>>((const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr,
-	                                             nchunks, g, 0, agg_group_size(nchunks), (uint32_t*)de, (uint4*)df,
-	                                             (uint32_t*)dc);
+	const AggCells xc{(const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr, nchunks, 0,
+	                  agg_group_size(nchunks)};
+	k_agg<kAggU, kAggD, false><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -1972,12 +2257,240 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	return SYZSIG_OK;
 }
 
+// The fused fast path of one triage run (k_agg_fin): scatter into capped
+// cells, then aggregation + finalize in one launch, with one host
+// synchronisation at the end.  maxSignal and newSignal are reserved for the
+// run's largest possible distinct count D_max = min(records, P * kAggLimit)
+// (a growth only when len + D_max would pass 90 % of the table; the usual
+// policy loads apply to the expected count), so the kernels never wait for
+// the host.  *done = false: nothing was committed and the caller takes the
+// counted-cell path (a cell spilled; the slack is doubled for the next run).
+static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0,
+                            uint64_t c1, const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st,
+                            uint64_t** pairs_out, uint64_t* npairs_io, bool* done)
+{
+	*done = false;
+	AggGeom g = agg_geom_for(ctx, run_recs, 0);
+	g.ibits = g.cbits();  // work items are whole chunks
+	const uint32_t S = 1u << g.pbits, P = S;
+	const uint64_t nchunks = (c1 - c0 + (1ull << g.ibits) - 1) >> g.ibits;
+	// distinct elements the fused kernel can commit: an LDS partition holds at
+	// most kAggLimit (one that overflows is committed after the sync)
+	const uint64_t d_max = std::min<uint64_t>(run_recs, (uint64_t)P * kAggLimit);
+	const double ratio = ctx->agg_distinct_ratio > 0 ? ctx->agg_distinct_ratio : 1.0 / 32;
+	const uint64_t d_est = std::min<uint64_t>(d_max, (uint64_t)(ratio * (double)run_recs) + 1);
+	// capacity for every possible change, before anything is committed
+	SYZ_TRY(set_reserve(ms, d_est));
+	SYZ_TRY(set_reserve_load(ms, d_max, kHardLoad));
+	// newSignal.Merge allocates a nil receiver (signal.go:121-125) -- but only
+	// when some DiffRaw is non-empty: a fresh set is dropped again if nothing changed
+	const bool fresh_ns = !*ns;
+	if (fresh_ns)
+		SYZ_TRY(syzsig_set_make(ctx, d_est, ns));
+	syzsig_set* nsp = *ns;
+	// at most half full for the expected changes (short probe chains: 0.34 ->
+	// 0.28 ms at C2), never past kHardLoad for the largest possible count
+	SYZ_TRY(set_reserve_load(nsp, d_est, kTargetLoad));
+	SYZ_TRY(set_reserve_load(nsp, d_max, kHardLoad));
+	if (ms->nbuckets < P || nsp->nbuckets < P) {  // slices need a bucket per partition
+		if (fresh_ns) {
+			syzsig_set_free(nsp);
+			*ns = nullptr;
+		}
+		return SYZSIG_OK;
+	}
+	const float sd = ctx->cap_sd;
+	const uint64_t bound = run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
+	void *recs, *cm, *dc, *pr, *dd, *dn;
+	SYZ_TRY(ws_get(ctx, 16, (bound + kDummyLines * kBlk) * 4, &recs));
+	SYZ_TRY(ws_get(ctx, 17, nchunks * 20 + (uint64_t)S * nchunks * 4 + 256, &cm));
+	uint64_t* sizes = (uint64_t*)cm;
+	uint64_t* cbase = sizes + nchunks;
+	uint32_t* ccap = (uint32_t*)(cbase + nchunks);
+	uint32_t* ccnt = ccap + nchunks;
+	uint32_t* ovf = ccnt + (uint64_t)S * nchunks;
+	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
+	SYZ_TRY(ws_grow_keep(ctx, 15, (*npairs_io + 4 * d_max) * 8 + 64, *npairs_io * 8, &pr));
+	*pairs_out = (uint64_t*)pr;
+	SYZ_TRY(ws_get(ctx, 32, d_max * 20 + 64, &dd));
+	SYZ_TRY(ws_get(ctx, 33, d_max * 8 + 64, &dn));
+	const hipStream_t s = ctx->stream;
+	SYZ_TRY(counters_reset(ctx));
+	memcpy(ctx->h_pin + kPinPairs, npairs_io, 8);  // consumed before the counters_fetch below
+	SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], ctx->h_pin + kPinPairs, 8, hipMemcpyHostToDevice, s));
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
+	SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
+	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.ibits, sizes);
+	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap);
+	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
+	k_agg_scatter_blk<false><<<(int)std::min<uint64_t>(nchunks, 2048), kAggThreads, 0, s>>>(
+	    b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, g, AggSrc{nullptr, 1, 0, 0}, cc,
+	    (uint32_t*)recs, ctx->agg_dbg >> 10);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
+	const uint32_t pb = g.pbits;
+	FinArgs fa;
+	fa.lm = lm;
+	fa.c0 = c0;
+	fa.slots = ms->slots;
+	fa.bmask = ms->nbuckets - 1;
+	fa.ms_shift = (63 - __builtin_clzll(ms->nbuckets)) - pb;
+	fa.ns_slots = nsp->slots;
+	fa.ns_bmask = nsp->nbuckets - 1;
+	fa.ns_shift = (63 - __builtin_clzll(nsp->nbuckets)) - pb;
+	fa.call_new = b->call_new;
+	fa.pairs = (uint64_t*)pr;
+	fa.npairs = &ctx->d_cnt[kCntAux2];
+	fa.ctr = ctx->d_cnt;
+	fa.def_e = (uint32_t*)dd;
+	fa.def_f = (uint4*)((char*)dd + ((d_max * 4 + 15) & ~15ull));
+	fa.def_cnt = &ctx->d_cnt[kCntDefer];
+	fa.def_ns = (uint64_t*)dn;
+	fa.def_ns_cnt = &ctx->d_cnt[kCntDeferNs];
+	fa.spill = ovf;
+	fa.dbg = ctx->agg_dbg;
+	const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks)};
+	k_agg_fin<kAggU, kAggD><<<P, kAggThreads, 0, s>>>(xc, g, fa, (uint32_t*)dc);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
+	k_fin_deferred<<<2 * kDeferBlocks, 256, 0, s>>>(fa.def_e, fa.def_f, fa.def_cnt, lm, c0, ms->slots, ms->nbuckets - 1,
+	                                                nsp->slots, nsp->nbuckets - 1, b->call_new, (uint64_t*)pr,
+	                                                fa.npairs, ctx->d_cnt, fa.def_ns, fa.def_ns_cnt);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[3], s));
+	uint32_t* hov = (uint32_t*)(ctx->h_pin + kPinCounts);
+	SYZ_HIP(hipMemcpyAsync(hov, ovf, 4, hipMemcpyDeviceToHost, s));
+	SYZ_TRY(counters_fetch(ctx));  // the run's one synchronisation
+	if (ctx->timing) {
+		float t0 = 0, t1 = 0, t2 = 0;
+		SYZ_HIP(hipEventElapsedTime(&t0, ctx->ev[0], ctx->ev[1]));
+		SYZ_HIP(hipEventElapsedTime(&t1, ctx->ev[1], ctx->ev[2]));
+		SYZ_HIP(hipEventElapsedTime(&t2, ctx->ev[2], ctx->ev[3]));
+		st->part_ms += t0;
+		st->probe_ms += t1;
+		st->decide_ms += t2;
+	}
+	if (*hov) {  // a cell spilled: nothing committed, redo with counted cells
+		st->retries++;
+		ctx->cap_sd = ctx->cap_sd * 2 > kCapSdMax ? 0.0f : ctx->cap_sd * 2;
+		if (fresh_ns) {
+			syzsig_set_free(nsp);
+			*ns = nullptr;
+		}
+		return SYZSIG_OK;
+	}
+	if (ctx->h_cnt[kCntOverflow])
+		return fail(SYZSIG_EIO, "triage: table overflow after reserve (internal error)");
+	uint64_t D = ctx->h_cnt[kCntDistinct];
+	uint64_t inserted = ctx->h_cnt[kCntInserted], changed = ctx->h_cnt[kCntChanged], ns_ins = ctx->h_cnt[kCntAux];
+	uint64_t npairs = ctx->h_cnt[kCntAux2];
+	const uint64_t novf = ctx->h_cnt[kCntAggOvf];
+	if (novf) {
+		// partitions past the LDS table: aggregated in HBM from their cells,
+		// then finalized with the atomic code (their elements are disjoint from
+		// every committed partition's)
+		std::vector<uint32_t> hc(P);
+		SYZ_HIP(hipMemcpy(hc.data(), dc, P * 4, hipMemcpyDeviceToHost));
+		std::vector<uint32_t> ovl;
+		uint64_t ovrec = 0;
+		std::vector<uint32_t> hcnt((uint64_t)P * nchunks);
+		SYZ_HIP(hipMemcpy(hcnt.data(), ccnt, hcnt.size() * 4, hipMemcpyDeviceToHost));
+		for (uint32_t q = 0; q < P; q++) {
+			if (hc[q] != kAggOverflow)
+				continue;
+			ovl.push_back(q);
+			for (uint64_t c = 0; c < nchunks; c++)
+				ovrec += hcnt[(uint64_t)q * nchunks + c];
+		}
+		const uint64_t C = pow2_at_least(std::max<uint64_t>(2 * ovrec, 1024));
+		void *gk, *ol, *de2, *df2, *dc2;
+		SYZ_TRY(ws_get(ctx, 23, C * 4 + (C + 1) * 16 + 64, &gk));
+		void* gf = (char*)gk + C * 4;
+		SYZ_TRY(ws_get(ctx, 22, ovl.size() * 4 + 64, &ol));
+		SYZ_TRY(ws_get(ctx, 30, ovrec * 4 + 64, &de2));
+		SYZ_TRY(ws_get(ctx, 31, ovrec * 16 + 64, &df2));
+		SYZ_HIP(hipMemsetAsync(gk, 0xff, C * 4 + (C + 1) * 16, s));
+		SYZ_HIP(hipMemcpyAsync(ol, ovl.data(), ovl.size() * 4, hipMemcpyHostToDevice, s));
+		SYZ_TRY(counters_reset(ctx));
+		k_agg_global_cap<<<grid_for(ovl.size() * nchunks * 64, 256, 8192), 256, 0, s>>>(
+		    (const uint32_t*)recs, cbase, ccap, ccnt, nchunks, g, (const uint32_t*)ol, (uint32_t)ovl.size(),
+		    (uint32_t*)gk, (uint32_t*)gf, C, &ctx->d_cnt[kCntError]);
+		k_agg_global_compact<<<grid_for(C + 1, 256, 8192), 256, 0, s>>>((const uint32_t*)gk, (const uint32_t*)gf, C,
+		                                                                 (uint32_t*)de2, (uint4*)df2,
+		                                                                 &ctx->d_cnt[kCntAux2]);
+		SYZ_HIP(hipGetLastError());
+		SYZ_TRY(counters_fetch(ctx));
+		if (ctx->h_cnt[kCntError])
+			return fail(SYZSIG_EIO, "triage: aggregation table overflow (internal error)");
+		const uint64_t gcnt = ctx->h_cnt[kCntAux2];
+		D += gcnt;
+		std::vector<uint32_t> rc;
+		for (uint64_t left = gcnt; left; left -= std::min<uint64_t>(left, kAggRegion))
+			rc.push_back((uint32_t)std::min<uint64_t>(left, kAggRegion));
+		if (!rc.empty()) {
+			// the reservations above covered the committed partitions (<= kAggLimit
+			// distinct each); these elements come on top
+			SYZ_TRY(set_reserve(ms, gcnt));
+			SYZ_TRY(set_reserve_load(nsp, gcnt, kHardLoad));
+			SYZ_TRY(ws_grow_keep(ctx, 15, (npairs + 4 * gcnt) * 8 + 64, npairs * 8, &pr));
+			*pairs_out = (uint64_t*)pr;
+			SYZ_TRY(ws_get(ctx, 35, rc.size() * 4 + 64, &dc2));
+			SYZ_HIP(hipMemcpyAsync(dc2, rc.data(), rc.size() * 4, hipMemcpyHostToDevice, s));
+			SYZ_TRY(counters_reset(ctx));
+			memcpy(ctx->h_pin + kPinPairs, &npairs, 8);
+			SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], ctx->h_pin + kPinPairs, 8, hipMemcpyHostToDevice, s));
+			k_agg_finalize<<<(uint32_t)rc.size(), kFinThreads, 0, s>>>(
+			    (const uint32_t*)de2, (const uint4*)df2, (const uint32_t*)dc2, (uint32_t)rc.size(), lm, c0, ms->slots,
+			    ms->nbuckets - 1, nsp->slots, nsp->nbuckets - 1, b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2],
+			    ctx->d_cnt, ctx->agg_dbg);
+			SYZ_HIP(hipGetLastError());
+			SYZ_TRY(counters_fetch(ctx));  // (synchronizes: rc is consumed)
+			if (ctx->h_cnt[kCntOverflow])
+				return fail(SYZSIG_EIO, "triage: table overflow after reserve (internal error)");
+			inserted += ctx->h_cnt[kCntInserted];
+			changed += ctx->h_cnt[kCntChanged];
+			ns_ins += ctx->h_cnt[kCntAux];
+			npairs = ctx->h_cnt[kCntAux2];
+		}
+		st->overflow_parts += novf;
+	}
+	if (fresh_ns && changed == 0) {
+		syzsig_set_free(nsp);
+		*ns = nullptr;
+		nsp = nullptr;
+	}
+	ms->len += inserted;
+	if (nsp)
+		nsp->len += ns_ins;
+	st->distinct += D;
+	st->parts = P;
+	st->survivors += D;
+	st->inserted += inserted;
+	st->changed += changed;
+	st->candidates += changed;
+	st->runs++;
+	ctx->agg_distinct_ratio = run_recs ? (double)D / (double)run_recs : 0;
+	*npairs_io = npairs;
+	*done = true;
+	return SYZSIG_OK;
+}
+
 // One run of calls [c0, c1) with level map lm.  Pairs are appended at
 // pairs[*npairs_io ...] (internal buffer, grown as needed).
 int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,
                    const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs_out,
                    uint64_t* npairs_io)
 {
+	if (ctx->cap_sd > 0 && !(ctx->agg_dbg & (SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL | 16))) {
+		bool done = false;
+		SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, c0, c1, lm, run_recs, st, pairs_out, npairs_io, &done));
+		if (done)
+			return SYZSIG_OK;
+	}
 	AggOut a;
 	SYZ_TRY(agg_aggregate(ctx, b, c0, c1, lm, run_recs, st, &a));
 	const uint64_t D = a.D;

@@ -120,6 +120,7 @@ struct SynthCfg {
 	uint32_t errno_permille;// call fails (errno != 0) w.p. /1000 (300)
 	uint32_t any_permille;  // call contains an ANY pointer w.p. /1000 (100)
 	uint32_t bad_pc_ppm;    // out-of-range PC rate per PC, parts per million (0)
+	uint32_t global_walk;   // 1: SURVEY 8(d)'s walk over all B blocks from a uniform start (0)
 };
 
 SYZ_HD uint64_t synth_pc(uint32_t block) { return kPcBase + 5ull * block; }
@@ -175,6 +176,18 @@ SYZ_HD void synth_trace(const SynthCfg& c, uint64_t prog, uint32_t call, uint64_
 	uint32_t bmask = (1u << c.nblocks_log2) - 1, wmask = (1u << c.region_log2) - 1;
 	uint32_t rmask = (1u << c.restart_log2) - 1;
 	uint64_t s = seed_mix(c.seed, prog, call);
+	if (c.global_walk) {  // b <- (4b + 1 + r%4) mod B from a uniform block, no restarts
+		uint32_t b = (uint32_t)(splitmix64(&s) >> 20) & bmask;
+		for (uint32_t i = 0; i < n; i++) {
+			uint64_t r = splitmix64(&s);
+			uint64_t pc = synth_pc(b);
+			if (c.bad_pc_ppm && ((r >> 40) % 1000000) < c.bad_pc_ppm)
+				pc = 0x1000ull + i;
+			out[i] = pc;
+			b = (4 * b + 1 + (uint32_t)((r >> 8) & 3)) & bmask;
+		}
+		return;
+	}
 	uint32_t x = 0;
 	for (uint32_t i = 0; i < n; i++) {
 		uint64_t r = splitmix64(&s);
@@ -194,6 +207,14 @@ SYZ_HD void synth_trace(const SynthCfg& c, uint64_t prog, uint32_t call, uint64_
 // restart edge and entry signal, exactly as write_coverage_signal would derive
 // them), the rest are uniform u32; prio uniform in 0..3.
 SYZ_HD uint32_t synth_known_per_sys(const SynthCfg& c) { return (1u << c.region_log2) * 5 + 1; }
+// known elements of M0 for `known_sys` syscalls (global walk: the whole edge
+// universe -- every block's first-PC signal and its 4 out-edges -- once known_sys > 0)
+SYZ_HD uint64_t synth_n_known(const SynthCfg& c, uint64_t known_sys)
+{
+	if (c.global_walk)
+		return known_sys ? 5ull << c.nblocks_log2 : 0;
+	return known_sys * synth_known_per_sys(c);
+}
 
 SYZ_HD void synth_m0_elem(const SynthCfg& c, uint64_t i, uint64_t n_known, uint32_t* elem, int8_t* prio)
 {
@@ -204,9 +225,19 @@ SYZ_HD void synth_m0_elem(const SynthCfg& c, uint64_t i, uint64_t n_known, uint3
 		*elem = (uint32_t)(r >> 32);
 		return;
 	}
+	uint32_t W = 1u << c.region_log2, bmask = (1u << c.nblocks_log2) - 1;
+	if (c.global_walk) {
+		const uint64_t B = 1ull << c.nblocks_log2;
+		if (i < B) {  // a call starting at block i: sig = pc ^ 0
+			*elem = (uint32_t)synth_pc((uint32_t)i);
+			return;
+		}
+		const uint32_t x = (uint32_t)((i - B) >> 2), j = (uint32_t)((i - B) & 3);
+		*elem = (uint32_t)synth_pc((4 * x + 1 + j) & bmask) ^ exec_hash((uint32_t)synth_pc(x));
+		return;
+	}
 	uint32_t per = synth_known_per_sys(c);
 	uint32_t sys = (uint32_t)(i / per), k = (uint32_t)(i % per);
-	uint32_t W = 1u << c.region_log2, bmask = (1u << c.nblocks_log2) - 1;
 	uint32_t entry = synth_entry(c, sys);
 	if (k == 0) {  // first PC of a call: sig = pc ^ 0
 		*elem = (uint32_t)synth_pc(entry);

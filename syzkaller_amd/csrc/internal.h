@@ -55,6 +55,8 @@ enum Counter : int {
 	kCntAux2,
 	kCntDefer,          // triage finalize: elements deferred to the atomic path
 	kCntDeferNs,        // triage finalize: newSignal merges deferred to the atomic path
+	kCntDistinct,       // fused triage: distinct elements aggregated
+	kCntAggOvf,         // fused triage: partitions that overflowed the LDS table
 	kNumCounters = 16,
 };
 
@@ -62,6 +64,10 @@ struct Workspace {
 	void* ptr = nullptr;
 	size_t size = 0;
 };
+
+// the debug flags that change only the path taken, never a result
+constexpr uint32_t kDebugResultPreserving =
+    SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL;
 
 // capped cells of the aggregation path (agg.hip): default slack, in standard deviations
 constexpr float kCapSdDefault = 6.0f;
@@ -86,7 +92,7 @@ struct syzsig_ctx {
 	// pinned staging for the small per-batch copies (a pageable copy is staged
 	// and synchronous): syz::kPin* offsets
 	char* h_pin = nullptr;
-	// grow-only scratch buffers by role: 0-2 set ops, 3-6 triage candidates and
+	// grow-only scratch buffers by role (35: the fused triage fallback): 0-2 set ops, 3-6 triage candidates and
 	// small state, 7-10 host uploads of minimize, 11-14 triage partitions and
 	// minimize internals and triage pairs (13-15), 16-23 + 30-31 triage aggregation,
 	// 24-29 check_new_signal uploads, 32-33 the finalize's deferred lists, 40-47 manager poll
@@ -100,7 +106,7 @@ struct syzsig_ctx {
 	float cap_sd_entry = syz::kCapSdDefault;  // the same for Minimize's runs
 	uint32_t edge_waves = 4;              // waves per program of k_edge_dedup (4 or 8; SYZSIG_EDGE_WAVES)
 	uint32_t agg_variant = 0;             // k_agg pipeline variant (SYZSIG_AGG_VARIANT; tuning)
-	uint32_t agg_dbg = 0;                 // timing-only experiments (SYZSIG_AGG_DBG; results invalid if set)
+	uint32_t agg_dbg = 0;                 // SYZSIG_DEBUG_* path flags; timing-only bits need -DSYZ_EXPERIMENTS
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	double last_ms = 0;                   // device time of the last timed entry point's kernels
 };
@@ -193,6 +199,7 @@ int pairs_from_bits(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* bits
 // the default load-factor policy: a table is grown when live/slots exceeds this
 constexpr double kMaxLoad = 0.75;
 constexpr double kTargetLoad = 0.5;
+constexpr double kHardLoad = 0.9;  // a reservation for a worst case grows the table only past this
 constexpr uint32_t kMaxProbeBuckets = 4096;
 
 inline int grid_for(uint64_t n, int block, int max_blocks = 2048)

@@ -167,6 +167,118 @@ __global__ __launch_bounds__(256) void k_min_from_dist(const uint4* __restrict__
 	}
 }
 
+// prios present among the entries of the virtual batch's calls (one wave per
+// call): the data-split parts read only their own contexts' entries
+__global__ __launch_bounds__(256) void k_min_prio_mask_calls(const uint64_t* __restrict__ cstart,
+                                                             const uint32_t* __restrict__ clen, uint64_t n,
+                                                             const uint8_t* __restrict__ prios, uint32_t* mask)
+{
+	uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	for (uint64_t c = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); c < n; c += nwaves) {
+		const uint64_t s0 = cstart[c];
+		for (uint32_t j = lane_id(); j < clen[c]; j += 64) {
+			const uint32_t u = prios[s0 + j];
+#pragma unroll
+			for (uint32_t k = 0; k < 8; k++)
+				m[k] |= (u >> 5) == k ? 1u << (u & 31) : 0u;
+		}
+	}
+#pragma unroll
+	for (uint32_t k = 0; k < 8; k++) {
+		uint32_t r = m[k];
+		for (int d = 32; d >= 1; d >>= 1)
+			r |= __shfl_xor(r, d, 64);
+		if (lane_id() == 0 && r)
+			atomicOr(&mask[k], r);
+	}
+}
+
+// A part's winner record of a distinct element (see syzsig_minimize_split_dev):
+// e << 32 | (prio ^ 0x80) << 24 | (0xFFFFFF - global rank); the max of the low
+// 32 bits over the parts is argmax (prio, -rank), the reference's winner.
+__device__ __forceinline__ uint64_t min_winner(uint32_t e, uint4 f4, const LevelMap& lm, uint32_t rank_lo)
+{
+	const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
+	int top = 0;
+#pragma unroll
+	for (int l = 0; l < 4; l++)
+		if (l < (int)lm.n && f[l] != 0xFFFFFFFFu)
+			top = l;
+	return ((uint64_t)e << 32) | ((uint64_t)prio_biased(lm.val[top]) << 24) | (0xFFFFFFu - (rank_lo + f[top]));
+}
+
+constexpr uint32_t kMinMaxShards = 64;
+
+// winner records per owner (block histogram, one atomic per owner per block)
+__global__ __launch_bounds__(256) void k_min_split_count(const uint32_t* __restrict__ dist_e,
+                                                         const uint32_t* __restrict__ cnt, uint32_t nregions,
+                                                         uint32_t nshards, unsigned long long* counts)
+{
+	__shared__ uint32_t h[kMinMaxShards];
+	if (threadIdx.x < kMinMaxShards)
+		h[threadIdx.x] = 0;
+	__syncthreads();
+	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
+		const uint32_t n = cnt[r];
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+			atomicAdd(&h[owner_of(dist_e[(uint64_t)r * kAggRegion + i], nshards)], 1u);
+	}
+	__syncthreads();
+	if (threadIdx.x < nshards && h[threadIdx.x])
+		atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+// winner records -> send[], grouped by owner (cursor[g] = next free slot of g)
+__global__ __launch_bounds__(256) void k_min_split_scatter(const uint32_t* __restrict__ dist_e,
+                                                           const uint4* __restrict__ dist_f,
+                                                           const uint32_t* __restrict__ cnt, uint32_t nregions,
+                                                           LevelMap lm, uint32_t rank_lo, uint32_t nshards,
+                                                           unsigned long long* cursor, uint64_t* send)
+{
+	__shared__ uint32_t h[kMinMaxShards];
+	__shared__ unsigned long long base[kMinMaxShards];
+	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
+		if (threadIdx.x < kMinMaxShards)
+			h[threadIdx.x] = 0;
+		__syncthreads();
+		const uint32_t n = cnt[r];
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+			atomicAdd(&h[owner_of(dist_e[(uint64_t)r * kAggRegion + i], nshards)], 1u);
+		__syncthreads();
+		if (threadIdx.x < nshards) {
+			base[threadIdx.x] = h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)h[threadIdx.x]) : 0;
+			h[threadIdx.x] = 0;
+		}
+		__syncthreads();
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+			const uint64_t o = (uint64_t)r * kAggRegion + i;
+			const uint32_t e = dist_e[o], g = owner_of(e, nshards);
+			send[base[g] + atomicAdd(&h[g], 1u)] = min_winner(e, dist_f[o], lm, rank_lo);
+		}
+		__syncthreads();
+	}
+}
+
+// owner side: the max winner record per element (the slot word IS the record:
+// key e in the top 32 bits, never 0 because rank < 2^24 - 1)
+__global__ void k_min_resolve(uint64_t* slots, uint64_t bmask, const uint64_t* __restrict__ recs, uint64_t n,
+                              unsigned long long* cnt)
+{
+	const uint64_t maxp = max_probe_for(bmask);
+	uint64_t ovf = 0;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t v = recs[i];
+		uint64_t old;
+		const int64_t s = tbl_find_or_insert(slots, bmask, (uint32_t)(v >> 32), v, old, maxp);
+		if (s < 0)
+			ovf++;
+		else if (old != 0 && old < v)
+			atomicMax(reinterpret_cast<unsigned long long*>(slots + s), (unsigned long long)v);
+	}
+	block_count(&cnt[kCntOverflow], ovf);
+}
+
 __global__ void k_count_u8(const uint8_t* __restrict__ a, uint64_t n, unsigned long long* cnt)
 {
 	uint64_t c = 0;
@@ -231,7 +343,178 @@ static int minimize_agg(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* 
 	return SYZSIG_OK;
 }
 
+// The stable order by (Len desc, index asc) of nctx contexts: order[r] = the
+// context at rank r (scratch slots 13-15).
+static int minimize_order(syzsig_ctx* ctx, const uint64_t* d_off, uint64_t nctx, const uint32_t** order)
+{
+	hipStream_t st = ctx->stream;
+	void *dk, *dtmp = nullptr;
+	SYZ_TRY(ws_get(ctx, 13, nctx * 16 + 64, &dk));
+	uint32_t* dv = (uint32_t*)dk + nctx;
+	uint32_t* dk2 = dv + nctx;
+	uint32_t* dv2 = dk2 + nctx;
+	k_min_keys<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, nctx, (uint32_t*)dk, dv);
+	size_t tmp_bytes = 0;
+	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)dk, dk2, dv, dv2, (int)nctx, 0, 32, st));
+	SYZ_TRY(ws_get(ctx, 15, tmp_bytes + 64, &dtmp));
+	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, (uint32_t*)dk, dk2, dv, dv2, (int)nctx, 0, 32, st));
+	*order = dv2;
+	return SYZSIG_OK;
+}
+
 extern "C" {
+
+int syzsig_minimize_split_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
+                              uint64_t nctx, uint32_t nparts, uint32_t part, uint32_t nshards, uint64_t hint_distinct,
+                              uint64_t* d_send, uint64_t send_cap, uint64_t* send_counts)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !send_counts || (nctx && !d_off) || (send_cap && !d_send))
+		return fail(SYZSIG_EINVAL, "minimize_split: NULL argument");
+	if (nparts == 0 || part >= nparts || nshards == 0 || nshards > kMinMaxShards)
+		return fail(SYZSIG_EINVAL, "minimize_split: need part < nparts and 1 <= nshards <= 64");
+	for (uint32_t g = 0; g < nshards; g++)
+		send_counts[g] = 0;
+	if (nctx == 0)
+		return SYZSIG_OK;
+	if (nctx >= 0xFFFFFFull)
+		return fail(SYZSIG_ERANGE, "minimize: more than 2^24-2 contexts");
+	hipStream_t st = ctx->stream;
+	const uint32_t* order = nullptr;
+	SYZ_TRY(minimize_order(ctx, d_off, nctx, &order));
+	// this part's range of ranks: cut at about part * total / nparts entries
+	std::vector<uint64_t> off(nctx + 1);
+	std::vector<uint32_t> ord(nctx);
+	SYZ_HIP(hipMemcpyAsync(off.data(), d_off, (nctx + 1) * 8, hipMemcpyDeviceToHost, st));
+	SYZ_HIP(hipMemcpyAsync(ord.data(), order, nctx * 4, hipMemcpyDeviceToHost, st));
+	SYZ_HIP(hipStreamSynchronize(st));
+	uint64_t total = 0;
+	for (uint64_t i = 0; i < nctx; i++) {
+		if (off[i + 1] < off[i])
+			return fail(SYZSIG_EINVAL, "minimize_split: ctx_off not monotone");
+		total += off[i + 1] - off[i];
+	}
+	if (total && (!d_elems || !d_prios))
+		return fail(SYZSIG_EINVAL, "minimize: NULL entry arrays");
+	const uint64_t want_lo = total * part / nparts, want_hi = total * (part + 1) / nparts;
+	uint64_t cum = 0, r_lo = nctx, r_hi = nctx;
+	for (uint64_t r = 0; r < nctx; r++) {
+		if (r_lo == nctx && cum >= want_lo && (part > 0 || r == 0))
+			r_lo = r;
+		if (cum >= want_hi && part + 1 < nparts) {
+			r_hi = r;
+			break;
+		}
+		cum += off[ord[r] + 1] - off[ord[r]];
+	}
+	if (r_lo > r_hi)
+		r_lo = r_hi;
+	uint64_t local = 0;
+	for (uint64_t r = r_lo; r < r_hi; r++)
+		local += off[ord[r] + 1] - off[ord[r]];
+	if (local == 0)
+		return SYZSIG_OK;
+	if (local > send_cap)
+		return fail(SYZSIG_ERANGE, "minimize_split: send buffer smaller than the part's entries");
+	// the part's contexts as a virtual batch in rank order
+	const uint64_t n = r_hi - r_lo;
+	void* vb;
+	SYZ_TRY(ws_get(ctx, 34, n * 12 + 128, &vb));
+	uint32_t* dmask = (uint32_t*)vb;
+	uint64_t* cstart = (uint64_t*)((char*)vb + 64);
+	uint32_t* clen = (uint32_t*)(cstart + n);
+	SYZ_TRY(counters_reset(ctx));
+	SYZ_HIP(hipMemsetAsync(dmask, 0, 32, st));
+	k_min_calls<<<grid_for(n, 256), 256, 0, st>>>(d_off, order + r_lo, n, cstart, clen, &ctx->d_cnt[kCntAux]);
+	k_min_prio_mask_calls<<<grid_for(n * 64, 256, 4096), 256, 0, st>>>(cstart, clen, n, (const uint8_t*)d_prios, dmask);
+	SYZ_HIP(hipGetLastError());
+	uint32_t* hmask = (uint32_t*)(ctx->h_pin + kPinMask);
+	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 32, hipMemcpyDeviceToHost, st));
+	SYZ_TRY(counters_fetch(ctx));
+	if (ctx->h_cnt[kCntAux])
+		return fail(SYZSIG_ERANGE, "minimize_split: a context of >= 2^24 entries");
+	int8_t levels[4];
+	uint32_t nl = 0;
+	for (int v = -128; v <= 127; v++) {
+		const uint8_t u = (uint8_t)(int8_t)v;
+		if ((hmask[u >> 5] >> (u & 31)) & 1) {
+			if (nl == 4)
+				return fail(SYZSIG_ERANGE, "minimize_split: more than 4 distinct prios in a part");
+			levels[nl++] = (int8_t)v;
+		}
+	}
+	LevelMap lm;
+	SYZ_TRY(level_map_from_levels(levels, nl, &lm));
+	syzsig_batch b = {};
+	b.sigs = d_elems;
+	b.call_start = cstart;
+	b.call_len = clen;
+	b.ncalls = n;
+	b.nrec = total;
+	const AggSrc x{d_prios, 1, 0, (double)(hint_distinct ? std::min(hint_distinct, local) : local)};
+	syzsig_batch_stats bst = {};
+	AggOut a;
+	SYZ_TRY(agg_aggregate(ctx, &b, 0, n, lm, local, &bst, &a, &x));
+	void* dcur;
+	SYZ_TRY(ws_get(ctx, 36, 2 * kMinMaxShards * 8, &dcur));
+	unsigned long long* counts = (unsigned long long*)dcur;
+	unsigned long long* cursor = counts + kMinMaxShards;
+	SYZ_HIP(hipMemsetAsync(counts, 0, kMinMaxShards * 8, st));
+	const int grid = (int)std::min<uint32_t>(a.nregions, 2048);
+	k_min_split_count<<<grid, 256, 0, st>>>(a.dist_e, a.cnt, a.nregions, nshards, counts);
+	SYZ_HIP(hipGetLastError());
+	unsigned long long h[kMinMaxShards];
+	SYZ_HIP(hipMemcpyAsync(h, counts, nshards * 8, hipMemcpyDeviceToHost, st));
+	SYZ_HIP(hipStreamSynchronize(st));
+	unsigned long long offs[kMinMaxShards], run = 0;
+	for (uint32_t g = 0; g < nshards; g++) {
+		offs[g] = run;
+		run += h[g];
+		send_counts[g] = h[g];
+	}
+	SYZ_HIP(hipMemcpyAsync(cursor, offs, nshards * 8, hipMemcpyHostToDevice, st));
+	k_min_split_scatter<<<grid, 256, 0, st>>>(a.dist_e, a.dist_f, a.cnt, a.nregions, lm, (uint32_t)r_lo, nshards, cursor,
+	                                          d_send);
+	SYZ_HIP(hipGetLastError());
+	SYZ_HIP(hipStreamSynchronize(st));
+	return SYZSIG_OK;
+}
+
+int syzsig_minimize_resolve_dev(syzsig_ctx* ctx, const uint64_t* d_off, uint64_t nctx, const uint64_t* d_recs,
+                                uint64_t nrec, uint8_t* d_keep, uint64_t* n_out)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !n_out || (nctx && (!d_off || !d_keep)) || (nrec && !d_recs))
+		return fail(SYZSIG_EINVAL, "minimize_resolve: NULL argument");
+	*n_out = 0;
+	if (nctx == 0)
+		return SYZSIG_OK;
+	if (nctx >= 0xFFFFFFull)
+		return fail(SYZSIG_ERANGE, "minimize: more than 2^24-2 contexts");
+	hipStream_t st = ctx->stream;
+	SYZ_HIP(hipMemsetAsync(d_keep, 0, nctx, st));
+	if (nrec) {
+		const uint32_t* order = nullptr;
+		SYZ_TRY(minimize_order(ctx, d_off, nctx, &order));
+		syzsig_set* t = nullptr;
+		SYZ_TRY(set_alloc(ctx, buckets_for(nrec), &t));
+		SYZ_TRY(counters_reset(ctx));
+		k_min_resolve<<<grid_for(nrec, 256, 8192), 256, 0, st>>>(t->slots, t->nbuckets - 1, d_recs, nrec, ctx->d_cnt);
+		k_min_winners<<<grid_for(t->nslots(), 256), 256, 0, st>>>(t->slots, t->nslots(), order, d_keep);
+		hipError_t e = hipGetLastError();
+		int rc = e == hipSuccess ? counters_fetch(ctx) : hip_fail(e, "k_min_resolve", __FILE__, __LINE__);
+		syzsig_set_free(t);
+		SYZ_TRY(rc);
+		if (ctx->h_cnt[kCntOverflow])
+			return fail(SYZSIG_EIO, "minimize_resolve: table overflow (internal error)");
+	}
+	SYZ_TRY(counters_reset(ctx));
+	k_count_u8<<<grid_for(nctx, 256), 256, 0, st>>>(d_keep, nctx, ctx->d_cnt);
+	SYZ_HIP(hipGetLastError());
+	SYZ_TRY(counters_fetch(ctx));
+	*n_out = ctx->h_cnt[kCntAux];
+	return SYZSIG_OK;
+}
 
 int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
                               uint64_t nctx, uint32_t nshards, uint32_t shard, uint64_t hint_distinct, uint8_t* d_keep,

@@ -17,8 +17,8 @@
 // target (a reply, or a fuzzer's final newMaxSignal) is the max-merge of the
 // (e, p) routed to it:
 //   k_poll_keys / radix sort   records by (e, poll), input order kept
-//   k_poll_walk                one thread per element: the events, and
-//                              maxSignal.Merge of the element's final max
+//   k_poll_walk                one thread per element: the events (read-only)
+//   k_poll_commit              maxSignal.Merge of the events, once every target exists
 //   k_poll_fanout              (target, e, p) of every event for every other
 //                              fuzzer into one max-table keyed by (target, e)
 //   k_poll_pre                 pre-batch newMaxSignal of polling fuzzers
@@ -34,6 +34,8 @@ namespace syz {
 
 constexpr uint64_t kPollEmpty = ~0ull;
 constexpr uint32_t kPollMaxTargets = (1u << 24) - 2;  // targets < 2^24 - 1 keep a word != kPollEmpty
+constexpr uint64_t kPollMaxNext = 1ull << 28;     // polls x fuzzers per batch (the dense next-target table)
+constexpr uint64_t kPollMaxFanout = 1ull << 31;   // polled entries x fuzzers per batch (bounds the fan-out table)
 
 // target-table word: target << 40 | elem << 8 | prio ^ 0x80 (key = the top 56 bits)
 __device__ __forceinline__ uint64_t poll_word(uint32_t t, uint32_t e, uint32_t pb)
@@ -83,11 +85,12 @@ __global__ void k_poll_keys(const uint32_t* __restrict__ elems, const uint32_t* 
 
 // One thread per element run of the sorted records: M0[e], then the polls in
 // order, each poll's last entry of e (Deserialize: a later duplicate wins).
+// Read-only on maxSignal: the events are committed by k_poll_commit once every
+// target set exists, so a failed allocation leaves the manager untouched.
 __global__ void k_poll_walk(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint64_t n,
-                            const int8_t* __restrict__ prios, uint64_t* ms, uint64_t ms_bmask, uint64_t* ev,
-                            unsigned long long* nev, unsigned long long* ctr)
+                            const int8_t* __restrict__ prios, const uint64_t* ms, uint64_t ms_bmask, uint64_t* ev,
+                            unsigned long long* nev)
 {
-	uint64_t ins = 0, ovf = 0, changed = 0;
 	for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
 		const uint32_t e = (uint32_t)(sk[r] >> 32);
 		if (r > 0 && (uint32_t)(sk[r - 1] >> 32) == e)
@@ -96,7 +99,6 @@ __global__ void k_poll_walk(const uint64_t* __restrict__ sk, const uint32_t* __r
 		int m = -1000;  // absent: below every prio (signal.go:79-81)
 		if (tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v))
 			m = slot_prio(v);
-		const int m0 = m;
 		for (uint64_t q = r; q < n && (uint32_t)(sk[q] >> 32) == e; q++) {
 			if (q + 1 < n && sk[q + 1] == sk[q])
 				continue;  // an earlier duplicate inside one Serial
@@ -106,16 +108,24 @@ __global__ void k_poll_walk(const uint64_t* __restrict__ sk, const uint32_t* __r
 				m = p;
 			}
 		}
-		if (m > m0) {
-			const int rr = tbl_merge(ms, ms_bmask, e, (int8_t)m);
-			ins += rr == 1;
-			ovf += rr < 0;
-			changed++;
-		}
+	}
+}
+
+// maxSignal.Merge(newMax_i) for every poll: the events, max-merged (an
+// element's last event carries its final max, the earlier ones are below it).
+__global__ void k_poll_commit(const uint64_t* __restrict__ ev, const unsigned long long* __restrict__ nev,
+                              uint64_t* ms, uint64_t ms_bmask, unsigned long long* ctr)
+{
+	const uint64_t n = *nev;
+	uint64_t ins = 0, ovf = 0;
+	for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < n; x += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t w = ev[x];
+		const int rr = tbl_merge(ms, ms_bmask, (uint32_t)(w >> 32), (int8_t)((uint8_t)w ^ 0x80u));
+		ins += rr == 1;
+		ovf += rr < 0;
 	}
 	block_count(&ctr[kCntInserted], ins);
 	block_count(&ctr[kCntOverflow], ovf);
-	block_count(&ctr[kCntChanged], changed);
 }
 
 // every event of poll i, for every fuzzer g != f_i: target next_target[i * F + g]
@@ -188,6 +198,16 @@ static uint64_t pow2_ge(uint64_t x)
 
 using namespace syz;
 
+// Sets this call made, freed again if it fails before the commit.
+struct PollFresh {
+	std::vector<syzsig_set*> sets;
+	~PollFresh()
+	{
+		for (syzsig_set* x : sets)
+			syzsig_set_free(x);
+	}
+};
+
 extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_max,
                                          uint32_t nfuzzers, const uint32_t* poll_fuzzer, const uint64_t* poll_off,
                                          const uint32_t* elems, const int8_t* prios, uint32_t npolls,
@@ -209,6 +229,10 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 	if (n && (!elems || !prios))
 		return fail(SYZSIG_EINVAL, "manager_poll_batch: NULL Serial arrays");
 	const uint32_t F = nfuzzers, K = npolls;
+	// the dense next-target table (K * F) and the fan-out table (<= n * (F - 1)
+	// events) are bounded before any state is touched
+	if ((uint64_t)K * F > kPollMaxNext || n * (uint64_t)F > kPollMaxFanout)
+		return fail(SYZSIG_ERANGE, "manager_poll_batch: polls x fuzzers or entries x fuzzers too large for one batch");
 	const hipStream_t s = ctx->stream;
 	// next target of (poll i, fuzzer g): g's next poll after i, else K + g (its final newMaxSignal)
 	std::vector<uint32_t> next((uint64_t)K * F), rec_poll(n), last(F);
@@ -221,11 +245,18 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 	for (uint32_t i = 0; i < K; i++)
 		for (uint64_t r = poll_off[i]; r < poll_off[i + 1]; r++)
 			rec_poll[r - poll_off[0]] = i;
-	const bool fresh_ms = !*max_signal;  // Merge allocates a nil maxSignal only for a non-empty newMax
-	if (fresh_ms)
-		SYZ_TRY(syzsig_set_make(ctx, n, max_signal));
+	// Nothing the caller can see changes until every set is made and sized:
+	// sets made here are freed again on an early return (PollFresh), and
+	// maxSignal, the fuzzers' sets and the replies are written only by the
+	// commit at the end, whose only failure is an internal overflow.
+	PollFresh fresh;
 	syzsig_set* ms = *max_signal;
-	SYZ_TRY(set_reserve(ms, n));
+	const bool fresh_ms = !ms;  // Merge allocates a nil maxSignal only for a non-empty newMax
+	if (fresh_ms) {
+		SYZ_TRY(syzsig_set_make(ctx, n, &ms));
+		fresh.sets.push_back(ms);
+	}
+	SYZ_TRY(set_reserve(ms, n));  // (a growth keeps the contents)
 	// uploads and scratch: records, sorted records, events, the target table
 	void *de, *dp, *drp, *dk, *dv, *dk2, *dv2, *dev, *dnext, *dtmp = nullptr;
 	SYZ_TRY(ws_get(ctx, 40, n * 4 + 64, &de));
@@ -259,18 +290,11 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 		                                           (uint32_t*)dv2, (int)n, 0, 64, s));
 		k_poll_walk<<<grid_for(n, 256), 256, 0, s>>>((const uint64_t*)dk2, (const uint32_t*)dv2, n,
 		                                             (const int8_t*)dp, ms->slots, ms->nbuckets - 1, (uint64_t*)dev,
-		                                             nev, ctx->d_cnt);
+		                                             nev);
 		SYZ_HIP(hipGetLastError());
 	}
 	SYZ_TRY(counters_fetch(ctx));
-	if (ctx->h_cnt[kCntOverflow])
-		return fail(SYZSIG_EIO, "manager_poll_batch: maxSignal overflow after reserve (internal error)");
-	ms->len += ctx->h_cnt[kCntInserted];
 	const uint64_t E = ctx->h_cnt[kCntAux];
-	if (fresh_ms && !E) {
-		syzsig_set_free(ms);
-		*max_signal = nullptr;
-	}
 	// the target table: every event for every other fuzzer + pre-batch sets of polling fuzzers
 	uint64_t entries = E * (F ? F - 1 : 0);
 	for (uint32_t g = 0; g < F; g++)
@@ -296,29 +320,32 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 	std::vector<unsigned int> hc((uint64_t)K + F);
 	SYZ_HIP(hipMemcpyAsync(hc.data(), tcount, ((uint64_t)K + F) * 4, hipMemcpyDeviceToHost, s));
 	SYZ_HIP(hipStreamSynchronize(s));
-	// the polling fuzzers' newMaxSignal is nil after their poll (manager.go:1049-1052)
-	for (uint32_t g = 0; g < F; g++) {
-		if (last[g] < K && new_max[g]) {
-			syzsig_set_free(new_max[g]);
-			new_max[g] = nullptr;
-		}
-	}
-	// target sets: the replies, then every fuzzer's newMaxSignal after the batch
+	// target sets: the replies, then every fuzzer's newMaxSignal after the batch.
+	// A polling fuzzer's own set goes into its first reply and is nil after its
+	// poll (manager.go:1049-1052), so its final set is a new one.
+	std::vector<syzsig_set*> tset((uint64_t)K + F, nullptr);
 	std::vector<PollTarget> tg((uint64_t)K + F, PollTarget{nullptr, 0});
 	for (uint64_t t = 0; t < (uint64_t)K + F; t++) {
 		if (!hc[t])
 			continue;
-		syzsig_set** sp = t < K ? &replies[t] : &new_max[t - K];
-		if (!*sp)
-			SYZ_TRY(syzsig_set_make(ctx, hc[t], sp));
-		else
-			SYZ_TRY(set_reserve(*sp, hc[t]));
-		tg[t] = PollTarget{(*sp)->slots, (*sp)->nbuckets - 1};
+		const bool keep = t >= K && last[t - K] >= K && new_max[t - K];  // a non-polling fuzzer's existing set
+		if (keep) {
+			tset[t] = new_max[t - K];
+			SYZ_TRY(set_reserve(tset[t], hc[t]));
+		} else {
+			SYZ_TRY(syzsig_set_make(ctx, hc[t], &tset[t]));
+			fresh.sets.push_back(tset[t]);
+		}
+		tg[t] = PollTarget{tset[t]->slots, tset[t]->nbuckets - 1};
 	}
 	void* dtg;
 	SYZ_TRY(ws_get(ctx, 39, ((uint64_t)K + F) * sizeof(PollTarget) + 64, &dtg));
 	SYZ_HIP(hipMemcpyAsync(dtg, tg.data(), ((uint64_t)K + F) * sizeof(PollTarget), hipMemcpyHostToDevice, s));
+	// ---- commit: maxSignal.Merge of the events, the targets filled ----
 	SYZ_TRY(counters_reset(ctx));
+	if (E)
+		k_poll_commit<<<grid_for(E, 256, 8192), 256, 0, s>>>((const uint64_t*)dev, nev, ms->slots, ms->nbuckets - 1,
+		                                                     ctx->d_cnt);
 	k_poll_scatter<<<grid_for(C, 256, 8192), 256, 0, s>>>((const uint64_t*)dT, C, (const PollTarget*)dtg, tins,
 	                                                      ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
@@ -326,12 +353,25 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 	SYZ_HIP(hipMemcpyAsync(hi.data(), tins, ((uint64_t)K + F) * 4, hipMemcpyDeviceToHost, s));
 	SYZ_TRY(counters_fetch(ctx));  // (synchronizes: hi and tg are consumed)
 	if (ctx->h_cnt[kCntOverflow])
-		return fail(SYZSIG_EIO, "manager_poll_batch: target overflow after reserve (internal error)");
-	for (uint64_t t = 0; t < (uint64_t)K + F; t++) {
-		if (!hc[t])
-			continue;
-		syzsig_set* st = t < K ? replies[t] : new_max[t - K];
-		st->len += hi[t];
+		return fail(SYZSIG_EIO, "manager_poll_batch: table overflow after reserve (internal error)");
+	fresh.sets.clear();  // everything made here is handed out now
+	ms->len += ctx->h_cnt[kCntInserted];
+	if (fresh_ms && !E)
+		syzsig_set_free(ms);  // nothing merged: maxSignal stays nil
+	else
+		*max_signal = ms;
+	for (uint32_t g = 0; g < F; g++) {
+		if (last[g] < K) {  // polled: the old set went into a reply; the final one is new (or nil)
+			syzsig_set_free(new_max[g]);
+			new_max[g] = tset[K + g];
+		} else if (!new_max[g]) {
+			new_max[g] = tset[K + g];
+		}
 	}
+	for (uint64_t t = 0; t < (uint64_t)K + F; t++)
+		if (tset[t])
+			tset[t]->len += hi[t];
+	for (uint32_t i = 0; i < K; i++)
+		replies[i] = tset[i];
 	return SYZSIG_OK;
 }

@@ -120,8 +120,15 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 		c->part_mode = atoi(v);
 	if (const char* v = getenv("SYZSIG_AGG_VARIANT"))
 		c->agg_variant = (uint32_t)atoi(v);
-	if (const char* v = getenv("SYZSIG_AGG_DBG"))
+	if (const char* v = getenv("SYZSIG_AGG_DBG")) {
 		c->agg_dbg = (uint32_t)atoi(v);
+#ifndef SYZ_EXPERIMENTS
+		// timing-only bits (skipped merges, dropped records) exist only in an
+		// experiment build (make exp EXPFLAGS=-DSYZ_EXPERIMENTS): a stray variable
+		// can select the result-preserving debug paths and nothing else
+		c->agg_dbg &= syz::kDebugResultPreserving;
+#endif
+	}
 	if (const char* v = getenv("SYZSIG_EDGE_WAVES"))
 		c->edge_waves = atoi(v) == 8 ? 8 : atoi(v) == 2 ? 2 : atoi(v) == 1 ? 1 : 4;
 	if (const char* v = getenv("SYZSIG_AGG_PARTS")) {
@@ -190,8 +197,7 @@ int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags)
 	SYZ_LOCK(ctx);
 	if (!ctx)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_debug: ctx is NULL");
-	ctx->agg_dbg = flags & (SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS |
-	                        SYZSIG_DEBUG_CAP_SPILL);  // only the result-preserving flags
+	ctx->agg_dbg = flags & syz::kDebugResultPreserving;
 	return SYZSIG_OK;
 }
 

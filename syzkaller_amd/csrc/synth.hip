@@ -16,6 +16,7 @@ static SynthCfg to_cfg(const syzsig_synth_cfg* c)
 	s.errno_permille = c->errno_permille;
 	s.any_permille = c->any_permille;
 	s.bad_pc_ppm = c->bad_pc_ppm;
+	s.global_walk = c->global_walk;
 	return s;
 }
 
@@ -62,6 +63,7 @@ void syzsig_synth_default(syzsig_synth_cfg* c)
 	c->errno_permille = 300;
 	c->any_permille = 100;
 	c->bad_pc_ppm = 0;
+	c->global_walk = 0;
 }
 
 int syzsig_synth_traces_host(const syzsig_synth_cfg* cfg, uint64_t prog_base, uint64_t nprog, uint32_t cpp,
@@ -102,7 +104,7 @@ int syzsig_synth_m0_host(const syzsig_synth_cfg* cfg, uint64_t known_sys, uint64
 	if (!cfg_ok(cfg) || (n && (!elems || !prios)))
 		return fail(SYZSIG_EINVAL, "synth_m0: bad argument");
 	SynthCfg s = to_cfg(cfg);
-	uint64_t n_known = known_sys * synth_known_per_sys(s);
+	uint64_t n_known = synth_n_known(s, known_sys);
 	for (uint64_t i = 0; i < n; i++)
 		synth_m0_elem(s, i, n_known, &elems[i], &prios[i]);
 	return SYZSIG_OK;
@@ -117,7 +119,7 @@ int syzsig_synth_m0_dev(syzsig_ctx* ctx, const syzsig_synth_cfg* cfg, uint64_t k
 	if (!n)
 		return SYZSIG_OK;
 	SynthCfg s = to_cfg(cfg);
-	k_synth_m0<<<grid_for(n, 256, 8192), 256, 0, ctx->stream>>>(s, known_sys * synth_known_per_sys(s), n, d_elems,
+	k_synth_m0<<<grid_for(n, 256, 8192), 256, 0, ctx->stream>>>(s, synth_n_known(s, known_sys), n, d_elems,
 	                                                             d_prios);
 	SYZ_HIP(hipGetLastError());
 	SYZ_HIP(hipStreamSynchronize(ctx->stream));

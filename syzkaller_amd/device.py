@@ -202,6 +202,32 @@ class Device:
                                                ctypes.byref(cnt)))
         return keep, int(cnt.value)
 
+    def minimize_split(self, ctx_off, elems, prios, nparts, part, nshards, hint_distinct=0, send=None):
+        """Data-split Minimize, source side (syzsig_minimize_split_dev): this
+        part's contexts aggregated, one winner record per distinct element,
+        grouped by owner.  -> (send int64[sum(counts)], counts)."""
+        self._check_dev(ctx_off, elems, prios, send)
+        n = ctx_off.numel() - 1
+        if send is None:
+            send = torch.empty(max(elems.numel(), 1), dtype=torch.int64, device=self.dev)
+        counts = (ctypes.c_uint64 * nshards)()
+        check(self.L.syzsig_minimize_split_dev(self.eng.h, _p(ctx_off), _p(elems), _p(prios), max(n, 0), int(nparts),
+                                               int(part), int(nshards), int(hint_distinct), _p(send), send.numel(),
+                                               counts))
+        counts = [int(c) for c in counts]
+        return send[: sum(counts)], counts
+
+    def minimize_resolve(self, ctx_off, recs):
+        """Data-split Minimize, owner side (syzsig_minimize_resolve_dev): the
+        winner records sent to this owner -> keep uint8[nctx]."""
+        self._check_dev(ctx_off, recs)
+        n = ctx_off.numel() - 1
+        keep = torch.empty(max(n, 0), dtype=torch.uint8, device=self.dev)
+        cnt = ctypes.c_uint64()
+        check(self.L.syzsig_minimize_resolve_dev(self.eng.h, _p(ctx_off), max(n, 0), _p(recs), recs.numel(),
+                                                 _p(keep), ctypes.byref(cnt)))
+        return keep, int(cnt.value)
+
     # ---------------------------------------------------------------- sharding
     def shard_partition(self, b, serial_base, levels, nshards, send, send_pos):
         lv = (ctypes.c_int8 * len(levels))(*levels)

@@ -22,7 +22,8 @@ serial index carried in every record (see triage.hip).
 import torch
 import torch.distributed as dist
 
-__all__ = ["owner_of_torch", "ShardedTriage", "GpuShardOps", "SIGNAL_PRIO_LEVELS", "sharded_minimize"]
+__all__ = ["owner_of_torch", "ShardedTriage", "GpuShardOps", "GpuMinimizeOps", "SIGNAL_PRIO_LEVELS",
+           "sharded_minimize"]
 
 _M32 = 0xFFFFFFFF
 
@@ -161,14 +162,39 @@ class ShardedTriage:
         return new_bits, call_new, st
 
 
-def sharded_minimize(minimize_shard, ctx_off, elems, prios, group=None, hint_distinct=0):
-    """signal.Minimize (pkg/signal/signal.go:138-166) sharded by element over
-    the ranks of `group`: every rank holds the corpus
-    description; rank r resolves the winners of the elements it owns
-    (minimize_shard(ctx_off, elems, prios, world, r, hint) -> (keep u8[nctx], n),
-    e.g. Device.minimize_shard) and the per-context keep flags are OR-reduced
-    (all_reduce MAX of 0/1 bytes).  Returns (keep, survivors)."""
+class GpuMinimizeOps:
+    """The device halves of the data-split Minimize (csrc/minimize.hip)."""
+
+    def __init__(self, dev):
+        self.dev = dev
+
+    def split(self, ctx_off, elems, prios, nparts, part, nshards, hint_distinct=0):
+        return self.dev.minimize_split(ctx_off, elems, prios, nparts, part, nshards, hint_distinct)
+
+    def resolve(self, ctx_off, recs):
+        return self.dev.minimize_resolve(ctx_off, recs)[0]
+
+
+def sharded_minimize(ops, ctx_off, elems, prios, group=None, hint_distinct=0):
+    """signal.Minimize (pkg/signal/signal.go:138-166) split by data over the
+    ranks of `group`: rank r takes a contiguous range of the
+    contexts in sort order (Len desc, index asc; ~total/world entries) and reads
+    only its own entries; it aggregates them to one winner record
+    (e, prio, rank) per distinct element (ops.split), the records go to
+    owner_of(e) with all_to_all_single, the owner keeps the max per element and
+    marks the winning contexts (ops.resolve), and the keep bytes are OR-reduced
+    (all_reduce MAX).  ops = GpuMinimizeOps(dev) or a restatement with the same
+    methods.  Every rank holds the corpus description (ctx_off); elems/prios
+    need only hold its own range.  Returns (keep u8[nctx], survivors)."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    keep, _ = minimize_shard(ctx_off, elems, prios, world, rank, hint_distinct // max(world, 1))
+    send, counts = ops.split(ctx_off, elems, prios, world, rank, world, hint_distinct)
+    dev = send.device
+    cnt_out = torch.tensor(counts, dtype=torch.int64, device=dev)
+    cnt_in = torch.empty_like(cnt_out)
+    dist.all_to_all_single(cnt_in, cnt_out, group=group)
+    recv_counts = cnt_in.tolist()
+    recv = torch.empty(sum(recv_counts), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv, send, recv_counts, counts, group=group)
+    keep = ops.resolve(ctx_off, recv)
     dist.all_reduce(keep, op=dist.ReduceOp.MAX, group=group)
     return keep, int(keep.to(torch.int64).sum().item())

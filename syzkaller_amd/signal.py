@@ -332,12 +332,16 @@ def manager_poll(max_signal, new_max, polls, eng=None):
     nm = (ctypes.c_void_p * max(F, 1))(*[s.handle.value or 0 for s in new_max])
     rep = (ctypes.c_void_p * max(K, 1))()
     mh = ctypes.c_void_p(max_signal.handle.value or 0)
-    check(eng.L.syzsig_manager_poll_batch(eng.h, ctypes.byref(mh), nm, F, _ptr(pf), _ptr(off), _ptr(elems),
-                                          _ptr(prios), K, rep))
-    if mh.value and max_signal.is_nil():
-        max_signal._h = mh
-    for g, s in enumerate(new_max):
-        s._h = ctypes.c_void_p(nm[g]) if nm[g] else None  # the library freed or replaced polled sets
+    try:
+        check(eng.L.syzsig_manager_poll_batch(eng.h, ctypes.byref(mh), nm, F, _ptr(pf), _ptr(off), _ptr(elems),
+                                              _ptr(prios), K, rep))
+    finally:
+        # the library replaces the polled fuzzers' sets only on success, and
+        # leaves every handle as it was on an error: mirror nm[] either way
+        if mh.value and max_signal.is_nil():
+            max_signal._h = mh
+        for g, s in enumerate(new_max):
+            s._h = ctypes.c_void_p(nm[g]) if nm[g] else None
     out = []
     for i in range(K):
         r = Signal(ctypes.c_void_p(rep[i]) if rep[i] else None, eng)

@@ -196,25 +196,56 @@ def _owner_np(e, n):
     return ((h * np.uint64(n)) >> np.uint64(32)).astype(np.int64)
 
 
-def numpy_minimize_shard(off, elems, prios, nshards, shard):
-    """Restatement of one shard's part of signal.Minimize (signal.go:138-166):
-    contexts ordered by (Len desc, index asc); for every element this shard
-    owns the winner is the earliest context of the highest prio."""
-    n = off.size - 1
-    lens = np.diff(off.astype(np.int64))
-    order = np.lexsort((np.arange(n), -lens))
-    rank = np.empty(n, np.int64)
-    rank[order] = np.arange(n)
-    ctx = np.repeat(np.arange(n), lens)
-    own = _owner_np(elems, nshards) == shard
-    e, p, r = elems[own].astype(np.int64), prios[own].astype(np.int64), rank[ctx[own]]
-    keep = np.zeros(n, np.uint8)
-    if e.size:
-        o = np.lexsort((r, -p, e))
-        first = np.ones(o.size, bool)
-        first[1:] = e[o][1:] != e[o][:-1]
-        keep[order[r[o][first]]] = 1
-    return torch.from_numpy(keep), int(keep.sum())
+class NumpyMinimizeOps:
+    """The data-split Minimize (csrc/minimize.hip syzsig_minimize_split_dev /
+    _resolve_dev) restated: the part's range of contexts in sort order (cut at
+    about total/nparts entries), per element the winner (prio, -rank) inside the
+    range as e << 32 | (prio ^ 0x80) << 24 | (0xFFFFFF - rank), grouped by
+    owner; the owner takes the max per element and marks the winners."""
+
+    @staticmethod
+    def _order(off):
+        lens = np.diff(off.astype(np.int64))
+        return np.lexsort((np.arange(lens.size), -lens)), lens
+
+    def split(self, off, elems, prios, nparts, part, nshards, hint_distinct=0):
+        order, lens = self._order(off)
+        cum = np.concatenate([[0], np.cumsum(lens[order])])  # entries of ranks < r
+        total = int(cum[-1])
+
+        def cut(k):  # first rank r with cum[r] >= k * total / nparts (nctx if none)
+            if k == 0:
+                return 0
+            if k >= nparts:
+                return order.size
+            r = int(np.searchsorted(cum[:-1], total * k // nparts, side="left"))
+            return min(r, order.size)
+
+        lo, hi = cut(part), cut(part + 1)
+        best = {}
+        for r in range(lo, hi):
+            c = int(order[r])
+            for j in range(int(off[c]), int(off[c + 1])):
+                e = int(elems[j])
+                v = ((int(prios[j]) & 0xFF) ^ 0x80) << 24 | (0xFFFFFF - r)
+                if v > best.get(e, -1):
+                    best[e] = v
+        groups = [[] for _ in range(nshards)]
+        for e, v in best.items():
+            groups[int(_owner_np([e], nshards)[0])].append((e << 32) | v)
+        send = np.array([x for g in groups for x in g], dtype=np.uint64).view(np.int64)
+        return torch.from_numpy(send.copy()), [len(g) for g in groups]
+
+    def resolve(self, off, recs):
+        order, _ = self._order(off)
+        best = {}
+        for x in recs.numpy().view(np.uint64):
+            e, v = int(x) >> 32, int(x) & 0xFFFFFFFF
+            best[e] = max(v, best.get(e, -1))
+        keep = np.zeros(order.size, np.uint8)
+        for v in best.values():
+            keep[order[0xFFFFFF - (v & 0xFFFFFF)]] = 1
+        return torch.from_numpy(keep)
 
 
 def _corpus(seed, n=300, U=2000):
@@ -227,25 +258,43 @@ def _corpus(seed, n=300, U=2000):
     return off, elems, prios
 
 
-def minimize_worker(rank, world, port, outdir, seed):
+def minimize_worker(rank, world, port, outdir, seed, hint):
     from syzkaller_amd.dist import sharded_minimize
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     off, elems, prios = _corpus(seed)
-    keep, n = sharded_minimize(lambda o, e, p, w, r, h: numpy_minimize_shard(o, e, p, w, r), off, elems, prios)
+    keep, n = sharded_minimize(NumpyMinimizeOps(), off, elems, prios, hint_distinct=hint)
     json.dump({"keep": keep.tolist(), "n": n}, open(os.path.join(outdir, f"m{rank}.json"), "w"))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("seed", [3, 4])
-def test_sharded_minimize_equals_minimize(seed):
+@pytest.mark.parametrize("seed,world,hint", [(3, 2, 0), (4, 2, 1500), (5, 3, 0), (6, 4, 1800)])
+def test_sharded_minimize_equals_minimize(seed, world, hint):
+    """Data-split Minimize over gloo (each rank reads only its range of the
+    corpus) against oracle Minimize over the whole corpus."""
     from oracle import oracle as O
 
-    world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(minimize_worker, args=(world, free_port(), d, seed), nprocs=world, start_method="spawn")
+        mp.start_processes(minimize_worker, args=(world, free_port(), d, seed, hint), nprocs=world,
+                           start_method="spawn")
         res = [json.load(open(os.path.join(d, f"m{r}.json"))) for r in range(world)]
     off, elems, prios = _corpus(seed)
     exp = O.minimize(off, elems, prios)
     for r in res:  # every rank holds the reduced result
         assert np.nonzero(np.array(r["keep"]))[0].tolist() == exp and r["n"] == len(exp)
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 5])
+def test_minimize_split_restatement_parts_cover_corpus(nparts):
+    """The part ranges tile the sort order and balance entries; the winners of
+    all parts resolved together give oracle Minimize (no collective)."""
+    from oracle import oracle as O
+
+    off, elems, prios = _corpus(9, n=500)
+    ops = NumpyMinimizeOps()
+    sends = [ops.split(off, elems, prios, nparts, k, 3) for k in range(nparts)]
+    keep = np.zeros(off.size - 1, np.uint8)
+    for g in range(3):
+        recv = torch.cat([s[g * 0 + sum(c[:g]): sum(c[: g + 1])] for s, c in sends])
+        keep |= ops.resolve(off, recv).numpy()
+    assert np.nonzero(keep)[0].tolist() == O.minimize(off, elems, prios)

@@ -115,14 +115,15 @@ def minimize_worker(rank, world, port, outdir):
     import torch.distributed as dist
 
     from syzkaller_amd.device import Device
-    from syzkaller_amd.dist import sharded_minimize
+    from syzkaller_amd.dist import GpuMinimizeOps, sharded_minimize
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     dev = Device(0)
     off, e, p = _min_corpus()
     t = lambda a, dt: torch.from_numpy(a.view(dt)).to(dev.dev)  # noqa: E731
-    keep, n = sharded_minimize(dev.minimize_shard, t(off, np.int64), t(e, np.int32), t(p, np.int8))
+    keep, n = sharded_minimize(GpuMinimizeOps(dev), t(off, np.int64), t(e, np.int32), t(p, np.int8),
+                               hint_distinct=1 << 16)
     np.save(os.path.join(outdir, f"m{rank}.npy"), keep.cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()

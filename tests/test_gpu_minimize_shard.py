@@ -240,3 +240,49 @@ def test_minimize_sharded_by_element_equals_unsharded(gpu, nshards):
     assert torch.equal(acc, keep1)
     assert tot >= n1
     assert np.nonzero(acc.cpu().numpy())[0].tolist() == O.minimize(off, e, p)
+
+
+def _split_emulated(gpu, doff, de, dp, nparts, nshards, hint=0):
+    """The data-split Minimize's exchange on one GPU: every part's winner
+    records routed to their owners, each owner resolved, keep flags OR-ed."""
+    sends = [gpu.minimize_split(doff, de, dp, nparts, k, nshards, hint) for k in range(nparts)]
+    keep = None
+    for g in range(nshards):
+        recv = torch.cat([s[sum(c[:g]): sum(c[: g + 1])] for s, c in sends])
+        k, _ = gpu.minimize_resolve(doff, recv)
+        keep = k if keep is None else torch.maximum(keep, k)
+    return keep, sends
+
+
+@pytest.mark.parametrize("nparts,nshards", [(1, 1), (2, 2), (3, 5), (8, 8)])
+def test_minimize_data_split_equals_unsharded(gpu, nparts, nshards):
+    """syzsig_minimize_split_dev / _resolve_dev (each part reads only its range
+    of the corpus) equal unsharded Minimize and the oracle."""
+    rng = np.random.default_rng(70 + nparts)
+    off, e, p = corpus(rng, 3000, 120, 20000)
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).to(gpu.dev)  # noqa: E731
+    doff, de, dp = t(off, np.int64), t(e, np.int32), t(p, np.int8)
+    keep1, _ = gpu.minimize(doff, de, dp)
+    keep, sends = _split_emulated(gpu, doff, de, dp, nparts, nshards)
+    assert torch.equal(keep, keep1)
+    assert np.nonzero(keep.cpu().numpy())[0].tolist() == O.minimize(off, e, p)
+    # every part sends at most one record per distinct element of its range
+    assert all(sum(c) <= np.unique(e).size for _, c in sends)
+
+
+def test_minimize_data_split_c3_eight_parts(gpu):
+    """BASELINE config 3 (200k contexts, ~400M entries) split over 8 parts and
+    8 owners on one GPU (the N=8 exchange emulated) against unsharded Minimize
+    and the oracle."""
+    from tests.test_gpu_configs import _corpus_dev
+
+    rng = np.random.default_rng(2018)
+    n, U = 200_000, 1 << 22
+    lens = np.minimum(rng.geometric(1.0 / 2000, size=n), U)
+    doff, de, dp = _corpus_dev(gpu.dev, n, lens, U, seed=n)
+    keep1, _ = gpu.minimize(doff, de, dp, hint_distinct=U)
+    keep, _ = _split_emulated(gpu, doff, de, dp, 8, 8, hint=U)
+    assert torch.equal(keep, keep1)
+    exp = np.array(O.minimize(doff.cpu().numpy().view(np.uint64), de.cpu().numpy().view(np.uint32),
+                              dp.cpu().numpy().view(np.int8)), np.int64)
+    np.testing.assert_array_equal(np.nonzero(keep.cpu().numpy())[0], exp)
