@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PROBE_BYTES_PER_REC = 12.0  # 4 B element read + 8 B maxSignal slot read
 # the K3 pipeline of one step on one GPU (csrc/agg.hip); roofline.avg_launch_ms is
 # their summed device time (HIP events), roofline.traffic their summed PMC bytes
-K3_KERNELS = "k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg+k_agg_finalize_x+k_fin_deferred"
+K3_KERNELS = "k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg_fin+k_fin_deferred"
 EDGE_BYTES_PER_PC = 12.0  # K1+K2: 8 B u64 PC in + 4 B u32 signal out
 # Minimize's chain on its aggregation path (csrc/minimize.hip header); the
 # keys sort and k_min_calls are negligible (200k contexts)
@@ -55,7 +55,9 @@ def parse():
     ap.add_argument("--programs", type=int, default=4096, help="programs per GPU")
     ap.add_argument("--calls", type=int, default=64)
     ap.add_argument("--pcs", type=int, default=4096)
-    ap.add_argument("--m0", type=int, default=10_000_000, help="maxSignal elements per GPU")
+    ap.add_argument("--m0", type=int, default=10_000_000, help="maxSignal elements (N=1)")
+    ap.add_argument("--m0-total", type=int, default=1_000_000_000,
+                    help="N>1: maxSignal elements over all ranks, hash-sharded (BASELINE config 4: 1B)")
     ap.add_argument("--skew", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time (s)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -69,6 +71,10 @@ def parse():
                     help="threads of the multi-core CPU baseline (the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--min-contexts", type=int, default=200_000, help="Minimize line: corpus size (BASELINE config 3)")
     ap.add_argument("--no-min", action="store_true", help="skip the Minimize line")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming line")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 per-rank line")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 line")
+    ap.add_argument("--lines-only", action="store_true", help="(experiments) only the extra lines, tiny headline")
     return ap.parse_args()
 
 
@@ -204,6 +210,208 @@ def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
                          "avg_launch_ms": t}}
 
 
+def synth_batch(dev, cfg, prog_base, P, C, L):
+    """Synthetic KCOV traces of P programs x C calls x L PCs -> K1+K2 on device.
+    Returns (sigs, call_start, sig_cnt, prio, records, pcs)."""
+    cl = torch.full((P * C,), L, dtype=torch.int32)
+    pcs, cs, cl, prio = dev.synth_traces(cfg, prog_base, P, C, cl)
+    pidx = torch.arange(P + 1, dtype=torch.int32, device=dev.dev) * C
+    sigs, cnt, comp = dev.edge_derive(pcs, cs, cl, pidx)
+    npc = pcs.numel()
+    del pcs
+    return sigs, cs, cnt, prio, int(cnt.to(torch.int64).sum().item()), npc
+
+
+def chain_ms(st):
+    return st["part_ms"] + st["probe_ms"] + st["decide_ms"]
+
+
+def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m0=10_000_000):
+    """BASELINE config 5 (sustained streaming triage, skewed PC distribution)
+    at one rank's share of an 8-GPU node: batches of `programs` x `calls` x
+    `pcs` (skew=1: Zipf-like hot syscalls, so hot edges repeat across the
+    batch), each triaged against the maxSignal/newSignal state the previous
+    batch left (syz-fuzzer/proc.go:230-247 -> fuzzer.go:494-511 per
+    execution, batched).  The sequence of `nbatches` batches starts from a
+    10M-element M0 and is replayed `reps` times (state restored between
+    replays, outside the timed region); value = records / wall time of the
+    sequence, chain = device time of the K3 kernels."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default(skew=1)
+    keep, bs = [], []
+    total = 0
+    for i in range(nbatches):
+        sigs, cs, cnt, prio, nrec, _ = synth_batch(dev, cfg, i * programs, programs, calls, pcs)
+        b, _, cnew = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
+        keep.append((sigs, cs, cnt, prio, cnew))
+        bs.append(b)
+        total += nrec
+    m0e, m0p = dev.synth_m0(cfg, 2048, m0)
+    pristine = dev.deserialize(m0e, m0p)
+    del m0e, m0p
+    walls, chains, sts = [], [], []
+    for r in range(reps + 1):
+        ms = pristine.clone()
+        ns = S.Signal.make(4_000_000, dev.eng)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        st = [dev.triage_b(ms, ns, b) for b in bs]
+        torch.cuda.synchronize()
+        if r:  # the first replay warms up
+            walls.append(time.perf_counter() - t)
+            chains.append(sum(chain_ms(x) for x in st))
+            sts = st
+    wall, chain = float(np.median(walls)), float(np.median(chains))
+    achieved = PROBE_BYTES_PER_REC * total / (chain * 1e-3) / 1e9
+    return {"metric": "signal elems triaged/sec (Diff+Merge), streaming skewed batches",
+            "value": total / wall, "unit": "elems/s", "higher_is_better": True,
+            "ms_per_batch": wall * 1e3 / nbatches, "dtype": "u32",
+            "config": {"workload": f"BASELINE config 5 at one rank's share of 8 GPUs: {nbatches} consecutive "
+                                   f"batches of {programs} programs x {calls} calls x {pcs} PCs, skew=1, each against "
+                                   f"the state the previous one left (M0 {m0})",
+                       "records": total, "batches": nbatches,
+                       "retries": [x["retries"] for x in sts], "runs": [x["runs"] for x in sts],
+                       "new_per_batch": [x["changed"] for x in sts], "distinct": [x["distinct"] for x in sts]},
+            "roofline": {"bound": "hbm", "kernel": K3_KERNELS, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": total // nbatches,
+                         "avg_launch_ms": chain / nbatches}}
+
+
+def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_000, reps=3):
+    """BASELINE config 4 seen from one rank of an 8-GPU node, on one GPU:
+    (1) the source side of a sharded step -- this rank's C2 batch aggregated per
+    element, each element's staircase records routed to its owner
+    (shard_agg_partition); (2) the owner side -- owner 0's records-mode triage
+    of the staircase records all 8 sources send it (the 8 sources' batches are
+    synthesized here one after another, program ranges r*P..), against owner
+    0's shard of a 1B-element maxSignal (125M elements).  The all-to-all
+    between them is not on one GPU: its bytes are reported.  value = this
+    rank's records / (source + owner device time)."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+    from syzkaller_amd.dist import SIGNAL_PRIO_LEVELS, owner_of_torch
+
+    cfg = synth.synth_default()
+    levels = list(SIGNAL_PRIO_LEVELS)
+    nrec0 = int(cnt.to(torch.int64).sum().item())
+
+    def ev_time(fn):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        out = fn()
+        b.record()
+        torch.cuda.synchronize()
+        return out, a.elapsed_time(b)
+
+    # owner 0's received records: every source's staircase records for shard 0
+    recv_parts, src_ms, sent = [], [], None
+    for r in range(world):
+        if r == 0:
+            s_sigs, s_cs, s_cnt, s_prio = sigs, cs, cnt, prio
+        else:
+            s_sigs, s_cs, s_cnt, s_prio, _, _ = synth_batch(dev, cfg, r * P, P, C, L)
+        b, _, _ = dev.batch(s_sigs, s_cs, s_cnt, s_prio, want_bits=False)
+        send = torch.empty(max(int(s_sigs.numel()), 1), dtype=torch.int64, device=dev.dev)
+        for rep in range(reps + 1 if r == 0 else 1):
+            (counts, st), ms_ = ev_time(lambda: dev.shard_agg_partition(b, r * P * C, levels, world, send))
+            if r == 0 and rep:
+                src_ms.append(ms_)
+        if r == 0:
+            sent = counts
+            src_st = st
+        recv_parts.append(send[: counts[0]].clone())
+        del send, b
+        if r:
+            del s_sigs, s_cs, s_cnt, s_prio
+    recv = torch.cat(recv_parts)
+    del recv_parts
+    # owner 0's shard of the 1B-element M0
+    ge, gp = dev.synth_m0(cfg, 2048, m0_total)
+    own = owner_of_torch(ge, world) == 0
+    se, sp = ge[own].contiguous(), gp[own].contiguous()
+    del ge, gp, own
+    pristine = dev.deserialize(se, sp)
+    shard_len = int(se.numel())
+    del se, sp
+    flags = torch.empty(recv.numel(), dtype=torch.uint8, device=dev.dev)
+    own_ms, ost = [], None
+    for rep in range(reps + 1):
+        shard = pristine.clone()
+        ns = S.Signal.make(4_000_000, dev.eng)
+        ost, ms_ = ev_time(lambda: dev.triage_records(shard, ns, recv, levels, flags))
+        if rep:
+            own_ms.append(ms_)
+        del shard
+    s_ms, o_ms = float(np.median(src_ms)), float(np.median(own_ms))
+    step = s_ms + o_ms
+    achieved = PROBE_BYTES_PER_REC * nrec0 / (step * 1e-3) / 1e9
+    xbytes = 8 * (sum(sent) - sent[0])
+    return {"metric": "signal elems triaged/sec (Diff+Merge) per rank of a 1B-element maxSignal over 8 GPUs",
+            "value": nrec0 / (step * 1e-3), "unit": "elems/s", "higher_is_better": True, "dtype": "u32",
+            "ms": step, "source_ms": s_ms, "owner_ms": o_ms,
+            "config": {"workload": f"BASELINE config 4, one rank of {world}: this rank's {P} x {C} x {L} batch "
+                                   f"(source aggregation + staircase routing), then owner 0's records-mode triage "
+                                   f"of what all {world} sources send it against its {shard_len}-element shard of a "
+                                   f"{m0_total}-element maxSignal",
+                       "records": nrec0, "staircase_sent": sum(sent), "sent_per_owner": sent,
+                       "owner_received": int(recv.numel()), "shard_elems": shard_len,
+                       "xgmi_bytes_out": xbytes,
+                       "xgmi_ms_at_7x153GBps": xbytes / (7 * 153e9) * 1e3,
+                       "source_distinct": src_st.get("distinct"), "owner_changed": ost.get("changed")},
+            "roofline": {"bound": "hbm", "kernel": K3_DIST_KERNELS, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": nrec0, "avg_launch_ms": step}}
+
+
+def c1_line(dev, reps=20):
+    """BASELINE config 1 (64 programs x 32 calls x 2k PCs): the reference's
+    CPU-runnable case, FromRaw/DiffRaw+Merge per call (checkNewSignal,
+    fuzzer.go:494-511) against a 200k-element maxSignal -- the oracle on one
+    core beside the GPU path on the same batch and M0."""
+    from oracle import oracle as O
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default()
+    P, C, L = 64, 32, 2048
+    sigs, cs, cnt, prio, nrec, _ = synth_batch(dev, cfg, 0, P, C, L)
+    m0e, m0p = dev.synth_m0(cfg, 2048, 200_000)
+    pristine = dev.deserialize(m0e, m0p)
+    b, _, _ = dev.batch(sigs, cs, cnt, prio, want_bits=False)
+    from syzkaller_amd import signal as S
+
+    wall = []
+    for r in range(reps + 2):
+        ms = pristine.clone()
+        ns = S.Signal(None, dev.eng)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        dev.triage_b(ms, ns, b)
+        torch.cuda.synchronize()
+        if r >= 2:
+            wall.append(time.perf_counter() - t)
+    g = float(np.median(wall))
+    h_sigs = sigs.cpu().numpy().view(np.uint32)
+    h_cs, h_cnt, h_prio = cs.cpu().numpy().view(np.uint64), cnt.cpu().numpy().view(np.uint32), prio.cpu().numpy()
+    e, p = m0e.cpu().numpy().view(np.uint32), m0p.cpu().numpy()
+    cpu = []
+    for _ in range(3):
+        oms = O.deserialize(e, p)
+        t = time.perf_counter()
+        O.triage_batch_into(oms, h_sigs, h_cs, h_cnt, h_prio)
+        cpu.append(time.perf_counter() - t)
+    c = float(np.median(cpu))
+    return {"metric": "signal elems triaged/sec (Diff+Merge), BASELINE config 1", "value": nrec / g,
+            "unit": "elems/s", "higher_is_better": True, "ms": g * 1e3, "dtype": "u32",
+            "config": {"workload": f"BASELINE config 1: {P} programs x {C} calls x {L} PCs vs a 200000-element "
+                                   "maxSignal (GPU path, wall time per batch incl. host sync)", "records": nrec},
+            "cpu": {"value": nrec / c, "unit": "elems/s", "cores": 1, "kind": "port", "ms": c * 1e3,
+                    "sample": "the whole C1 batch, oracle/oracle.c single thread (sequential checkNewSignal)"}}
+
+
 def frame_regions(sigs, cs, cnt, prio, comp, P, C):
     """The batch as executor output regions (executor.h:566-604 records, one
     region per program; errno 22 for failed calls), built with torch ops on
@@ -309,7 +517,8 @@ def main():
     if distributed:
         from syzkaller_amd.dist import SIGNAL_PRIO_LEVELS, GpuShardOps, ShardedTriage, owner_of_torch
 
-        ge, gp = dev.synth_m0(cfg, 2048, a.m0 * world)
+        # BASELINE config 4: one maxSignal of m0_total elements, hash-sharded
+        ge, gp = dev.synth_m0(cfg, 2048, a.m0_total)
         own = owner_of_torch(ge, world) == rank
         m0e, m0p = ge[own].contiguous(), gp[own].contiguous()
         del ge, gp
@@ -325,7 +534,9 @@ def main():
     # checkNewSignal's outputs: the calls with new signal, every call's DiffRaw
     # result (pairs), maxSignal and newSignal (per-record bits are not part of
     # the reference's result and are not computed)
-    pairs = torch.empty(16 << 20, dtype=torch.int64, device=dev.dev)
+    # room for every pair the run can emit (4 per distinct element, <= 2048 x 5939 distinct):
+    # the library writes them here directly instead of copying them after the run
+    pairs = torch.empty(4 * 2048 * 5939 + 64, dtype=torch.int64, device=dev.dev)
     b, bits, cnew = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
     if distributed:
         ops = GpuShardOps(dev)
@@ -397,10 +608,14 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
-            "config": {"workload": "BASELINE config 2: 1xMI355X batch triage per GPU, "
-                                   f"{P} programs x {C} calls x {L} PCs vs {a.m0} -element maxSignal"
-                                   + (f" shard (hash-sharded over {world} GPUs, RCCL all-to-all)" if distributed else ""),
-                       "programs_per_gpu": P, "calls": C, "pcs_per_call": L, "m0_per_gpu": a.m0,
+            "config": {"workload": ("BASELINE config 2: 1xMI355X batch triage, "
+                                    f"{P} programs x {C} calls x {L} PCs vs a {a.m0}-element maxSignal")
+                       if not distributed else
+                       (f"BASELINE config 4: a {a.m0_total}-element maxSignal hash-sharded over {world} GPUs "
+                        f"({m0e.numel()} elements on rank 0), each rank triaging {P} programs x {C} calls x {L} PCs "
+                        "(BASELINE config 2 per GPU), staircase records routed with RCCL all-to-all"),
+                       "programs_per_gpu": P, "calls": C, "pcs_per_call": L,
+                       "m0_per_gpu": a.m0 if not distributed else int(m0e.numel()),
                        "records_per_gpu": nrec, "pcs_per_gpu": npc, "skew": a.skew,
                        "table_slots": ms.capacity(),
                        "parallelism": f"shard{world}" if distributed else "single",
@@ -435,6 +650,12 @@ def main():
                          "bytes_per_unit": EDGE_BYTES_PER_PC, "units_per_launch": npc, "avg_launch_ms": e_ms}}}
     if rank == 0 and world == 1 and not a.no_min:
         out["lines"]["minimize"] = minimize_line(dev, a.min_contexts)
+    if rank == 0 and world == 1 and not a.no_c5:
+        out["lines"]["c5"] = c5_line(dev, pairs)
+    if rank == 0 and world == 1 and not a.no_c1:
+        out["lines"]["c1"] = c1_line(dev)
+    if rank == 0 and world == 1 and not a.no_c4:
+        out["lines"]["c4_rank"] = c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L)
     if rank == 0 and world == 1 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, C, a.cpu_seconds, a.cpu_threads)
     elif rank == 0:

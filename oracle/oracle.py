@@ -70,7 +70,10 @@ class OSig:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().orc_sig_free(self.h)
+            try:
+                lib().orc_sig_free(self.h)
+            except TypeError:  # interpreter shutdown: module globals are gone, the process frees everything
+                pass
             self.h = None
 
     @property

@@ -549,6 +549,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 		return __ballot(r[lane & (kWaves - 1)] != 0) != 0;  // lane i reads wave i's flag
 	};
 	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << ib) - 1) >> ib;  // work items
+	if (*cc.ovf)
+		return;  // the run is already void (an optimistic run's assumptions failed, or a cell spilled)
 	bool spilled = false;
 	if (kEntry) {
 		for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
@@ -821,6 +823,7 @@ struct AggCells {
 	const uint32_t* cap_cnt;
 	uint64_t nchunks;
 	uint32_t ilog, gsz;
+	const uint32_t* spill;  // nonzero: a cell spilled, the run is redone (nothing aggregated); may be null
 };
 
 // Aggregate partition p into the LDS table (every thread of the workgroup;
@@ -1053,6 +1056,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(AggCells x, AggGeom g, uint
 	__shared__ AggLds L;
 	const uint32_t* keys = reinterpret_cast<const uint32_t*>(L.kb);
 	const uint32_t P = 1u << g.pbits, lane = lane_id();
+	if (x.spill && *x.spill)
+		return;  // a cell spilled: the records are incomplete and the run is redone
 	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
 		if (!agg_partition<U, D, kCap>(L, p, x, g)) {
 			if (threadIdx.x == 0)
@@ -1378,13 +1383,16 @@ __global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
     uint32_t nregions, LevelMap lm, uint64_t c0, uint64_t* slots, uint64_t bmask, uint32_t ms_shift,
     uint64_t* ns_slots, uint64_t ns_bmask, uint32_t ns_shift, uint8_t* call_new, uint64_t* pairs,
     unsigned long long* npairs, unsigned long long* ctr, uint32_t* def_e, uint4* def_f,
-    unsigned long long* def_cnt, uint64_t* def_ns, unsigned long long* def_ns_cnt, uint32_t dbg)
+    unsigned long long* def_cnt, uint64_t* def_ns, unsigned long long* def_ns_cnt, uint32_t dbg,
+    const uint32_t* spill)
 {
 	__shared__ uint32_t claim[kFxSet];
 	__shared__ uint64_t buf[kFxBuf];
 	__shared__ uint32_t s_n;
 	__shared__ unsigned long long s_base;
-	uint64_t inserted = 0, changed = 0, ns_ins = 0;
+	if (spill && *spill)
+		return;  // a cell spilled: nothing is committed, the run is redone
+	uint64_t inserted = 0, changed = 0, ns_ins = 0, distinct = 0, novf = 0;
 	auto flush = [&](uint32_t nb) {  // every thread; nb = s_n read after a barrier
 		nb = min(nb, kFxBuf);
 		if (threadIdx.x == 0)
@@ -1413,6 +1421,11 @@ __global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
 		const uint64_t ms0 = (uint64_t)r << ms_shift, ms1 = (uint64_t)(r + 1) << ms_shift;
 		const uint64_t ns0 = (uint64_t)r << ns_shift, ns1 = (uint64_t)(r + 1) << ns_shift;
 		const uint32_t n = cnt[r];
+		if (n == kAggOverflow) {  // past the LDS table: aggregated in HBM and committed after this launch
+			novf++;
+			continue;
+		}
+		distinct += n;
 		for (uint32_t i0 = 0; i0 < n; i0 += kFxIlp * kFxThreads) {
 			uint32_t e[kFxIlp];
 			uint4 f4[kFxIlp];
@@ -1501,6 +1514,10 @@ __global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
 	block_count(&ctr[kCntInserted], inserted);
 	block_count(&ctr[kCntChanged], changed);
 	block_count(&ctr[kCntAux], ns_ins);
+	if (threadIdx.x == 0 && distinct)
+		atomicAdd(&ctr[kCntDistinct], (unsigned long long)distinct);
+	if (threadIdx.x == 0 && novf)
+		atomicAdd(&ctr[kCntAggOvf], (unsigned long long)novf);
 }
 
 // Deferred elements of k_agg_finalize_x, with the global-atomic table code
@@ -2118,8 +2135,10 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	if (entry)
 		while (g.ibits > 0 && ((c1 - c0) >> g.ibits) < 2048)
 			g.ibits--;
+	const bool counted_once = ctx->agg_counted_once;
+	ctx->agg_counted_once = false;
 	if (((entry ? ctx->cap_sd_entry : ctx->cap_sd) > 0 || (ctx->agg_dbg & SYZSIG_DEBUG_CAP_SPILL)) &&
-	    !(ctx->agg_dbg & SYZSIG_DEBUG_EXACT_CELLS)) {
+	    !(ctx->agg_dbg & SYZSIG_DEBUG_EXACT_CELLS) && !counted_once) {
 		bool done = false;
 		SYZ_TRY(agg_capped(ctx, b, c0, c1, lm, run_recs, g, xp, st, out, &done));
 		if (done)
@@ -2257,6 +2276,21 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	return SYZSIG_OK;
 }
 
+// An optimistic run's assumptions, checked on device from the presence pass
+// (mask[8], total, bad at `presence`): prios in 0..3, at most `guess` records,
+// valid call ranges.  Otherwise *ovf = 2 and the run commits nothing.
+__global__ void k_fast_check(const uint32_t* __restrict__ presence, uint64_t guess, uint32_t* ovf)
+{
+	if (threadIdx.x != 0)
+		return;
+	uint32_t other = presence[0] & ~0xFu;
+	for (int i = 1; i < 8; i++)
+		other |= presence[i];
+	const uint64_t total = ((const uint64_t*)presence)[4], bad = ((const uint64_t*)presence)[5];
+	if (other || bad || total > guess)
+		*ovf = 2u;
+}
+
 // The fused fast path of one triage run (k_agg_fin): scatter into capped
 // cells, then aggregation + finalize in one launch, with one host
 // synchronisation at the end.  maxSignal and newSignal are reserved for the
@@ -2267,9 +2301,12 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 // counted-cell path (a cell spilled; the slack is doubled for the next run).
 static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0,
                             uint64_t c1, const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st,
-                            uint64_t** pairs_out, uint64_t* npairs_io, bool* done)
+                            uint64_t** pairs_out, uint64_t* npairs_io, bool* done, const void* presence = nullptr,
+                            bool* assumed_bad = nullptr)
 {
 	*done = false;
+	if (assumed_bad)
+		*assumed_bad = false;
 	AggGeom g = agg_geom_for(ctx, run_recs, 0);
 	g.ibits = g.cbits();  // work items are whole chunks
 	const uint32_t S = 1u << g.pbits, P = S;
@@ -2310,7 +2347,11 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	uint32_t* ccnt = ccap + nchunks;
 	uint32_t* ovf = ccnt + (uint64_t)S * nchunks;
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
-	SYZ_TRY(ws_grow_keep(ctx, 15, (*npairs_io + 4 * d_max) * 8 + 64, *npairs_io * 8, &pr));
+	if (presence && *npairs_io == 0 && b->new_pairs && b->new_pairs_cap >= 4 * d_max) {
+		pr = b->new_pairs;  // every possible pair fits the caller's buffer: no copy afterwards
+	} else {
+		SYZ_TRY(ws_grow_keep(ctx, 15, (*npairs_io + 4 * d_max) * 8 + 64, *npairs_io * 8, &pr));
+	}
 	*pairs_out = (uint64_t*)pr;
 	SYZ_TRY(ws_get(ctx, 32, d_max * 20 + 64, &dd));
 	SYZ_TRY(ws_get(ctx, 33, d_max * 8 + 64, &dn));
@@ -2321,6 +2362,8 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
 	SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
+	if (presence)
+		k_fast_check<<<1, 64, 0, s>>>((const uint32_t*)presence, run_recs, ovf);
 	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.ibits, sizes);
 	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap);
 	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
@@ -2351,11 +2394,31 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	fa.def_ns_cnt = &ctx->d_cnt[kCntDeferNs];
 	fa.spill = ovf;
 	fa.dbg = ctx->agg_dbg;
-	const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks)};
-	k_agg_fin<kAggU, kAggD><<<P, kAggThreads, 0, s>>>(xc, g, fa, (uint32_t*)dc);
-	SYZ_HIP(hipGetLastError());
-	if (ctx->timing)
-		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
+	const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),
+	                  ovf};
+	if (ctx->agg_variant == 7) {  // aggregation and finalize in one launch
+		k_agg_fin<kAggU, kAggD><<<P, kAggThreads, 0, s>>>(xc, g, fa, (uint32_t*)dc);
+		SYZ_HIP(hipGetLastError());
+		if (ctx->timing)
+			SYZ_HIP(hipEventRecord(ctx->ev[2], s));
+	} else {
+		// k_agg's distinct lists through HBM (5 M x 20 B at C2), then the
+		// slice-exclusive finalize: a workgroup of the finalize is small, so
+		// many run per CU and their random probes overlap (the one-launch form
+		// holds a CU's LDS through its probes)
+		void *de, *df;
+		SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
+		SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
+		k_agg<kAggU, kAggD, true><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+		SYZ_HIP(hipGetLastError());
+		if (ctx->timing)
+			SYZ_HIP(hipEventRecord(ctx->ev[2], s));
+		k_agg_finalize_x<2><<<P, kFxThreads, 0, s>>>(
+		    (const uint32_t*)de, (const uint4*)df, (const uint32_t*)dc, P, lm, c0, fa.slots, fa.bmask, fa.ms_shift,
+		    fa.ns_slots, fa.ns_bmask, fa.ns_shift, fa.call_new, fa.pairs, fa.npairs, ctx->d_cnt, fa.def_e, fa.def_f,
+		    fa.def_cnt, fa.def_ns, fa.def_ns_cnt, ctx->agg_dbg, ovf);
+		SYZ_HIP(hipGetLastError());
+	}
 	k_fin_deferred<<<2 * kDeferBlocks, 256, 0, s>>>(fa.def_e, fa.def_f, fa.def_cnt, lm, c0, ms->slots, ms->nbuckets - 1,
 	                                                nsp->slots, nsp->nbuckets - 1, b->call_new, (uint64_t*)pr,
 	                                                fa.npairs, ctx->d_cnt, fa.def_ns, fa.def_ns_cnt);
@@ -2373,6 +2436,14 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		st->part_ms += t0;
 		st->probe_ms += t1;
 		st->decide_ms += t2;
+	}
+	if (*hov & 2) {  // an optimistic run's assumptions failed: nothing committed
+		*assumed_bad = true;
+		if (fresh_ns) {
+			syzsig_set_free(nsp);
+			*ns = nullptr;
+		}
+		return SYZSIG_OK;
 	}
 	if (*hov) {  // a cell spilled: nothing committed, redo with counted cells
 		st->retries++;
@@ -2485,11 +2556,15 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
                    const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs_out,
                    uint64_t* npairs_io)
 {
-	if (ctx->cap_sd > 0 && !(ctx->agg_dbg & (SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL | 16))) {
+	if (ctx->cap_sd > 0 && !(ctx->agg_dbg & (SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL | 16)) &&
+	    !ctx->agg_counted_once) {
 		bool done = false;
+		const uint64_t retries0 = st->retries;
 		SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, c0, c1, lm, run_recs, st, pairs_out, npairs_io, &done));
 		if (done)
 			return SYZSIG_OK;
+		// a spilled cell: this run is redone with counted cells, not capped ones again
+		ctx->agg_counted_once = st->retries != retries0;
 	}
 	AggOut a;
 	SYZ_TRY(agg_aggregate(ctx, b, c0, c1, lm, run_recs, st, &a));
@@ -2534,7 +2609,7 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 		fin<<<a.nregions, kFxThreads, 0, s>>>(
 		    a.dist_e, a.dist_f, a.cnt, a.nregions, lm, c0, ms->slots, ms->nbuckets - 1, ms_shift, nsp->slots,
 		    nsp->nbuckets - 1, ns_shift, b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2], ctx->d_cnt, def_e, def_f,
-		    &ctx->d_cnt[kCntDefer], (uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], ctx->agg_dbg);
+		    &ctx->d_cnt[kCntDefer], (uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], ctx->agg_dbg, nullptr);
 		k_fin_deferred<<<2 * kDeferBlocks, 256, 0, s>>>(def_e, def_f, &ctx->d_cnt[kCntDefer], lm, c0, ms->slots,
 		                                                ms->nbuckets - 1, nsp->slots, nsp->nbuckets - 1, b->call_new,
 		                                                (uint64_t*)pr, &ctx->d_cnt[kCntAux2], ctx->d_cnt,
@@ -2569,6 +2644,24 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 		nsp->len += ctx->h_cnt[kCntAux];
 	*npairs_io = ctx->h_cnt[kCntAux2];
 	st->runs++;
+	return SYZSIG_OK;
+}
+
+int agg_triage_optimistic(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b,
+                          const void* presence, syzsig_batch_stats* st, uint64_t** pairs, uint64_t* npairs, bool* done)
+{
+	*done = false;
+	if (ctx->cap_sd <= 0 || ctx->agg_counted_once ||
+	    (ctx->agg_dbg & (SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL | 16)))
+		return SYZSIG_OK;
+	LevelMap lm;
+	const int8_t lv[4] = {0, 1, 2, 3};
+	SYZ_TRY(level_map_from_levels(lv, 4, &lm));
+	bool bad = false;
+	const uint64_t retries0 = st->retries;
+	SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, 0, b->ncalls, lm, b->nrec, st, pairs, npairs, done, presence, &bad));
+	// a spilled cell: the planned path redoes the batch with counted cells
+	ctx->agg_counted_once = !*done && st->retries != retries0;
 	return SYZSIG_OK;
 }
 

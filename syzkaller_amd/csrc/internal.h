@@ -104,6 +104,8 @@ struct syzsig_ctx {
 	double agg_distinct_ratio = 0;        // distinct/records of the last aggregated run (sizes the next)
 	float cap_sd = syz::kCapSdDefault;    // capped-cell slack in standard deviations (agg.hip; 0 = counted cells)
 	float cap_sd_entry = syz::kCapSdDefault;  // the same for Minimize's runs
+	bool agg_counted_once = false;
+	int edge_impl = 0;                    // K1+K2 kernel: 0 conflict rounds, 1 lane-owned slot ranges (SYZSIG_EDGE_IMPL)        // the next agg_aggregate takes counted cells (a fused run spilled)
 	uint32_t edge_waves = 4;              // waves per program of k_edge_dedup (4 or 8; SYZSIG_EDGE_WAVES)
 	uint32_t agg_variant = 0;             // k_agg pipeline variant (SYZSIG_AGG_VARIANT; tuning)
 	uint32_t agg_dbg = 0;                 // SYZSIG_DEBUG_* path flags; timing-only bits need -DSYZ_EXPERIMENTS
@@ -191,6 +193,15 @@ int batch_total_records(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t* total,
 int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,
                    const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs,
                    uint64_t* npairs);
+// The whole batch as one aggregation run without waiting for its prio
+// presence pass: levels 0..3 (signalPrio's range, fuzzer.go:513-521) and
+// b->nrec records are assumed, the presence results (device, `presence`:
+// mask[8], total, bad) are checked on device before the scatter, and the run
+// commits nothing when they do not hold.  One host synchronisation.  *done =
+// false: take the planned path (*assumed_ok tells whether the assumptions held).
+int agg_triage_optimistic(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b,
+                          const void* presence, syzsig_batch_stats* st, uint64_t** pairs, uint64_t* npairs,
+                          bool* done);
 int agg_mark_bits(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const uint64_t* pairs,
                   uint64_t p0, uint64_t p1);
 int pairs_from_bits(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* bits, uint64_t c0, uint64_t c1,

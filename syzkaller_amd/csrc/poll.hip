@@ -113,10 +113,9 @@ __global__ void k_poll_walk(const uint64_t* __restrict__ sk, const uint32_t* __r
 
 // maxSignal.Merge(newMax_i) for every poll: the events, max-merged (an
 // element's last event carries its final max, the earlier ones are below it).
-__global__ void k_poll_commit(const uint64_t* __restrict__ ev, const unsigned long long* __restrict__ nev,
-                              uint64_t* ms, uint64_t ms_bmask, unsigned long long* ctr)
+__global__ void k_poll_commit(const uint64_t* __restrict__ ev, uint64_t n, uint64_t* ms, uint64_t ms_bmask,
+                              unsigned long long* ctr)
 {
-	const uint64_t n = *nev;
 	uint64_t ins = 0, ovf = 0;
 	for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < n; x += (uint64_t)gridDim.x * blockDim.x) {
 		const uint64_t w = ev[x];
@@ -342,9 +341,10 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 	SYZ_TRY(ws_get(ctx, 39, ((uint64_t)K + F) * sizeof(PollTarget) + 64, &dtg));
 	SYZ_HIP(hipMemcpyAsync(dtg, tg.data(), ((uint64_t)K + F) * sizeof(PollTarget), hipMemcpyHostToDevice, s));
 	// ---- commit: maxSignal.Merge of the events, the targets filled ----
+	// (the event count is passed by value: the counter reset clears *nev)
 	SYZ_TRY(counters_reset(ctx));
 	if (E)
-		k_poll_commit<<<grid_for(E, 256, 8192), 256, 0, s>>>((const uint64_t*)dev, nev, ms->slots, ms->nbuckets - 1,
+		k_poll_commit<<<grid_for(E, 256, 8192), 256, 0, s>>>((const uint64_t*)dev, E, ms->slots, ms->nbuckets - 1,
 		                                                     ctx->d_cnt);
 	k_poll_scatter<<<grid_for(C, 256, 8192), 256, 0, s>>>((const uint64_t*)dT, C, (const PollTarget*)dtg, tins,
 	                                                      ctx->d_cnt);

@@ -617,13 +617,33 @@ int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const sy
 	}
 	std::vector<Run> runs;
 	uint64_t total = 0;
+	uint64_t* pairs = nullptr;
+	uint64_t npairs = 0;
+	if (b->ncalls <= kSerialMask && use_agg(ctx, b->nrec, b->nrec) && !b->new_bits) {
+		// a large batch: one aggregation run that does not wait for the
+		// presence pass (levels 0..3 assumed and checked on device)
+		void* dmask;
+		SYZ_TRY(ws_get(ctx, 6, 64, &dmask));
+		SYZ_HIP(hipMemsetAsync(dmask, 0, 48, ctx->stream));
+		k_prio_presence<<<grid_for(b->ncalls, 256, 256), 256, 0, ctx->stream>>>(
+		    b->call_prio, b->call_len, b->call_start, b->ncalls, b->nrec, (uint32_t*)dmask,
+		    (unsigned long long*)((char*)dmask + 32), (unsigned long long*)((char*)dmask + 40));
+		SYZ_HIP(hipGetLastError());
+		uint32_t* hmask = (uint32_t*)(ctx->h_pin + kPinMask);
+		SYZ_HIP(hipMemcpyAsync(hmask, dmask, 48, hipMemcpyDeviceToHost, ctx->stream));
+		bool done = false;
+		SYZ_TRY(agg_triage_optimistic(ctx, ms, ns, b, dmask, st, &pairs, &npairs, &done));
+		if (done) {
+			memcpy(&st->records, &hmask[8], 8);  // (the run synchronised: the copy has landed)
+			goto finish;
+		}
+	}
 	SYZ_TRY(plan_runs(ctx, b, &runs, &total));
 	st->records = total;
+	{
 	uint64_t maxrun = 0;
 	for (auto& r : runs)
 		maxrun = std::max(maxrun, r.c1 - r.c0);
-	uint64_t* pairs = nullptr;
-	uint64_t npairs = 0;
 	for (auto& r : runs) {
 		const uint64_t run_recs = runs.size() == 1 ? total : b->nrec;  // bound
 		if (use_agg(ctx, run_recs, b->nrec)) {
@@ -663,14 +683,17 @@ int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const sy
 		SYZ_TRY(triage_run<CallsIn>(ctx, ms, ns, prep, r.lm, (uint32_t*)cs, (uint32_t*)cm, (uint32_t*)cc, st));
 		SYZ_TRY(pairs_from_bits(ctx, b, bits, r.c0, r.c1, run_recs, &pairs, &npairs));
 	}
+	}
+finish:
 	if ((double)ms->len > kMaxLoad * (double)ms->nslots())
 		SYZ_TRY(set_rehash(ms, buckets_for(ms->len), false));
 	st->new_signal_len = syzsig_len(*ns);
 	st->new_pairs = npairs;
-	if (b->new_pairs && npairs)
+	if (b->new_pairs && npairs && pairs != b->new_pairs) {
 		SYZ_HIP(hipMemcpyAsync(b->new_pairs, pairs, std::min(npairs, b->new_pairs_cap) * 8, hipMemcpyDeviceToDevice,
 		                       ctx->stream));
-	SYZ_HIP(hipStreamSynchronize(ctx->stream));
+	}
+	SYZ_HIP(hipStreamSynchronize(ctx->stream));  // (idle unless a copy or a rehash is queued)
 	return SYZSIG_OK;
 }
 

@@ -43,9 +43,12 @@ def oracle_pairs(hs, hcs, hcnt, obits):
     return np.unique((call << np.uint64(32)) | hs[r].astype(np.uint64))
 
 
-def compare(gpu, m0, hb, db, new0=None, ms_hint=None, agg=1, parts=0, reset=True):
+def compare(gpu, m0, hb, db, new0=None, ms_hint=None, agg=1, parts=0, reset=True, want_bits=True, pairs_cap=None):
     """agg: 0 = per-call path, 1 = auto, 2 = aggregation path (parts fixed if > 0).
-    reset=False keeps the engine's path settings (and its adaptive state) as they are."""
+    reset=False keeps the engine's path settings (and its adaptive state) as they are.
+    want_bits=False: no per-record bits (what checkNewSignal returns; a large
+    batch then takes the one-sync optimistic run); pairs_cap: the new_pairs
+    buffer's size (default: one per record)."""
     from syzkaller_amd import signal as S
 
     hs, hcs, hcnt, hprio = hb
@@ -54,17 +57,18 @@ def compare(gpu, m0, hb, db, new0=None, ms_hint=None, agg=1, parts=0, reset=True
     np.testing.assert_array_equal(_u(dprio, np.uint8), hprio)
     ms = S.Serial(*m0).Deserialize(gpu.eng) if m0[0].size else S.Signal.make(ms_hint or 0, gpu.eng)
     ns = S.Serial(*new0).Deserialize(gpu.eng) if new0 is not None else S.Signal(None, gpu.eng)
-    pairs = torch.full((int(hcnt.sum()) + 1,), -1, dtype=torch.int64, device=gpu.dev)
+    pairs = torch.full((pairs_cap or int(hcnt.sum()) + 1,), -1, dtype=torch.int64, device=gpu.dev)
     if reset:
         gpu.eng.set_agg(agg, parts)
     try:
-        bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio, new_pairs=pairs)
+        bits, cnew, st = gpu.triage(ms, ns, ds, dcs, dcnt, dprio, new_pairs=pairs, want_bits=want_bits)
     finally:
         if reset:
             gpu.eng.set_agg(1, 0)
     oms, ons, obits, ocnew = O.triage_batch(m0[0], m0[1], hs, hcs, hcnt, hprio, new0)
     np.testing.assert_array_equal(_u(cnew, np.uint8), ocnew)
-    np.testing.assert_array_equal(_u(bits, np.uint32), obits)
+    if want_bits:
+        np.testing.assert_array_equal(_u(bits, np.uint32), obits)
     op = oracle_pairs(hs, hcs, hcnt, obits)
     assert st["new_pairs"] == op.size
     np.testing.assert_array_equal(np.sort(_u(pairs[: op.size], np.uint64)), op)
@@ -92,18 +96,73 @@ def test_triage_c1_vs_oracle(gpu, over, known, nm0, agg):
     assert (st["parts"] > 0) == (agg == 2)
 
 
+@pytest.mark.parametrize("want_bits,direct", [(True, False), (False, False), (False, True)])
 @pytest.mark.parametrize("skew", [0, 1])
-def test_triage_agg_auto_vs_oracle(gpu, skew):
+def test_triage_agg_auto_vs_oracle(gpu, skew, want_bits, direct):
     """A 5M-element maxSignal and a batch big enough (128 x 32 x 2k) to take
-    the aggregation path by itself."""
+    the aggregation path by itself; without per-record bits it is the one-sync
+    optimistic run, and with a new_pairs buffer of 4 entries per record its
+    pairs are written there directly."""
     from syzkaller_amd import synth
 
     cfg = synth.synth_default(skew=skew)
     nprog, cpp = 128, 32
     cl = synth.call_lengths(nprog, cpp, 2048)
     m0 = synth.m0(cfg, 2048, 5_000_000)
-    st = compare(gpu, m0, host_batch(cfg, nprog, cpp, cl), dev_batch(gpu, cfg, nprog, cpp, cl))
+    hb = host_batch(cfg, nprog, cpp, cl)
+    st = compare(gpu, m0, hb, dev_batch(gpu, cfg, nprog, cpp, cl), want_bits=want_bits,
+                 pairs_cap=4 * int(hb[2].sum()) + 64 if direct else None)
     assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
+
+
+@pytest.mark.parametrize("case", ["prio7", "prio_neg", "five_levels"])
+def test_triage_optimistic_assumptions_fail(gpu, case):
+    """The one-sync run assumes prios 0..3; a batch with another prio (a
+    DiffRaw prio is any uint8, compared as int8: signal.go:90-102) voids it on
+    device before anything is written, and the planned path (presence pass,
+    level runs) must give the oracle's result."""
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default()
+    nprog, cpp = 128, 32
+    cl = synth.call_lengths(nprog, cpp, 2048)
+    m0 = synth.m0(cfg, 2048, 2_000_000)
+    hs, hcs, hcnt, hprio = host_batch(cfg, nprog, cpp, cl)
+    hprio = hprio.copy()
+    rng = np.random.default_rng(3)
+    pick = rng.choice(hprio.size, 40, replace=False)
+    hprio[pick] = {"prio7": 7, "prio_neg": 0xFF, "five_levels": 4}[case]
+    if case == "five_levels":
+        hprio[pick[:20]] = 0x80  # -128
+    ds, dcs, dcnt, _ = dev_batch(gpu, cfg, nprog, cpp, cl)
+    dprio = torch.from_numpy(hprio).to(gpu.dev)
+    st = compare(gpu, m0, (hs, hcs, hcnt, hprio), (ds, dcs, dcnt, dprio), want_bits=False)
+    assert st["records"] == int(hcnt.sum()) and st["runs"] >= 1
+
+
+def test_triage_optimistic_bad_range_leaves_state(gpu):
+    """A call range outside the record space, in a batch large enough for the
+    optimistic run: EINVAL (triage.hip batch_total_records), and maxSignal,
+    newSignal and the pairs are untouched."""
+    from syzkaller_amd import _lib
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default()
+    nprog, cpp = 128, 32
+    cl = synth.call_lengths(nprog, cpp, 2048)
+    m0 = synth.m0(cfg, 2048, 1_000_000)
+    ds, dcs, dcnt, dprio = dev_batch(gpu, cfg, nprog, cpp, cl)
+    dcs = dcs.clone()
+    dcs[77] = ds.numel() - 3  # runs past the end
+    ms = S.Serial(*m0).Deserialize(gpu.eng)
+    ns = S.Signal(None, gpu.eng)
+    before = ms.to_dict()
+    pairs = torch.full((1024,), -1, dtype=torch.int64, device=gpu.dev)
+    with pytest.raises(_lib.SyzsigError):
+        gpu.triage(ms, ns, ds, dcs, dcnt, dprio, new_pairs=pairs, want_bits=False)
+    assert ms.to_dict() == before and ns.is_nil()
+    assert bool((pairs == -1).all())
 
 
 AGG_LIMIT = 7424 * 4 // 5  # csrc/agg.hip kAggLimit (kAggSlots * 4 / 5): distinct elements an LDS partition holds
