@@ -824,6 +824,7 @@ struct AggCells {
 	uint64_t nchunks;
 	uint32_t ilog, gsz;
 	const uint32_t* spill;  // nonzero: a cell spilled, the run is redone (nothing aggregated); may be null
+	unsigned long long* ctr;  // if set: distinct elements (kCntDistinct) and overflowed partitions (kCntAggOvf)
 };
 
 // Aggregate partition p into the LDS table (every thread of the workgroup;
@@ -1060,8 +1061,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(AggCells x, AggGeom g, uint
 		return;  // a cell spilled: the records are incomplete and the run is redone
 	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
 		if (!agg_partition<U, D, kCap>(L, p, x, g)) {
-			if (threadIdx.x == 0)
+			if (threadIdx.x == 0) {
 				cnt[p] = kAggOverflow;
+				if (x.ctr)
+					atomicAdd(&x.ctr[kCntAggOvf], 1ull);
+			}
 			__syncthreads();
 			continue;
 		}
@@ -1083,8 +1087,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(AggCells x, AggGeom g, uint
 			}
 		}
 		__syncthreads();
-		if (threadIdx.x == 0)
+		if (threadIdx.x == 0) {
 			cnt[p] = L.s_out;
+			if (x.ctr && L.s_out)
+				atomicAdd(&x.ctr[kCntDistinct], (unsigned long long)L.s_out);
+		}
 		__syncthreads();
 	}
 }
@@ -1384,7 +1391,7 @@ __global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
     uint64_t* ns_slots, uint64_t ns_bmask, uint32_t ns_shift, uint8_t* call_new, uint64_t* pairs,
     unsigned long long* npairs, unsigned long long* ctr, uint32_t* def_e, uint4* def_f,
     unsigned long long* def_cnt, uint64_t* def_ns, unsigned long long* def_ns_cnt, uint32_t dbg,
-    const uint32_t* spill)
+    const uint32_t* spill, const unsigned long long* ovf_gate, uint32_t gate_max)
 {
 	__shared__ uint32_t claim[kFxSet];
 	__shared__ uint64_t buf[kFxBuf];
@@ -1392,7 +1399,9 @@ __global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
 	__shared__ unsigned long long s_base;
 	if (spill && *spill)
 		return;  // a cell spilled: nothing is committed, the run is redone
-	uint64_t inserted = 0, changed = 0, ns_ins = 0, distinct = 0, novf = 0;
+	if (ovf_gate && *ovf_gate > gate_max)
+		return;  // the partitions were too few for the run's distinct elements: redone with more
+	uint64_t inserted = 0, changed = 0, ns_ins = 0;
 	auto flush = [&](uint32_t nb) {  // every thread; nb = s_n read after a barrier
 		nb = min(nb, kFxBuf);
 		if (threadIdx.x == 0)
@@ -1421,11 +1430,8 @@ __global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
 		const uint64_t ms0 = (uint64_t)r << ms_shift, ms1 = (uint64_t)(r + 1) << ms_shift;
 		const uint64_t ns0 = (uint64_t)r << ns_shift, ns1 = (uint64_t)(r + 1) << ns_shift;
 		const uint32_t n = cnt[r];
-		if (n == kAggOverflow) {  // past the LDS table: aggregated in HBM and committed after this launch
-			novf++;
-			continue;
-		}
-		distinct += n;
+		if (n == kAggOverflow)
+			continue;  // past the LDS table: aggregated in HBM and committed after this launch
 		for (uint32_t i0 = 0; i0 < n; i0 += kFxIlp * kFxThreads) {
 			uint32_t e[kFxIlp];
 			uint4 f4[kFxIlp];
@@ -1514,10 +1520,6 @@ __global__ __launch_bounds__(kFxThreads) void k_agg_finalize_x(
 	block_count(&ctr[kCntInserted], inserted);
 	block_count(&ctr[kCntChanged], changed);
 	block_count(&ctr[kCntAux], ns_ins);
-	if (threadIdx.x == 0 && distinct)
-		atomicAdd(&ctr[kCntDistinct], (unsigned long long)distinct);
-	if (threadIdx.x == 0 && novf)
-		atomicAdd(&ctr[kCntAggOvf], (unsigned long long)novf);
 }
 
 // Deferred elements of k_agg_finalize_x, with the global-atomic table code
@@ -2302,9 +2304,13 @@ __global__ void k_fast_check(const uint32_t* __restrict__ presence, uint64_t gue
 static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0,
                             uint64_t c1, const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st,
                             uint64_t** pairs_out, uint64_t* npairs_io, bool* done, const void* presence = nullptr,
-                            bool* assumed_bad = nullptr)
+                            bool* assumed_bad = nullptr, bool* regeom = nullptr)
 {
 	*done = false;
+	bool regeom_local = false;
+	if (!regeom)
+		regeom = &regeom_local;
+	*regeom = false;
 	if (assumed_bad)
 		*assumed_bad = false;
 	AggGeom g = agg_geom_for(ctx, run_recs, 0);
@@ -2395,7 +2401,10 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	fa.spill = ovf;
 	fa.dbg = ctx->agg_dbg;
 	const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),
-	                  ovf};
+	                  ovf, ctx->agg_variant == 7 ? nullptr : ctx->d_cnt};
+	// more overflowed partitions than this and the split path commits nothing:
+	// the run is redone with partitions sized from what k_agg counted
+	const uint32_t gate = P / 8;
 	if (ctx->agg_variant == 7) {  // aggregation and finalize in one launch
 		k_agg_fin<kAggU, kAggD><<<P, kAggThreads, 0, s>>>(xc, g, fa, (uint32_t*)dc);
 		SYZ_HIP(hipGetLastError());
@@ -2416,7 +2425,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		k_agg_finalize_x<2><<<P, kFxThreads, 0, s>>>(
 		    (const uint32_t*)de, (const uint4*)df, (const uint32_t*)dc, P, lm, c0, fa.slots, fa.bmask, fa.ms_shift,
 		    fa.ns_slots, fa.ns_bmask, fa.ns_shift, fa.call_new, fa.pairs, fa.npairs, ctx->d_cnt, fa.def_e, fa.def_f,
-		    fa.def_cnt, fa.def_ns, fa.def_ns_cnt, ctx->agg_dbg, ovf);
+		    fa.def_cnt, fa.def_ns, fa.def_ns_cnt, ctx->agg_dbg, ovf, &ctx->d_cnt[kCntAggOvf], gate);
 		SYZ_HIP(hipGetLastError());
 	}
 	k_fin_deferred<<<2 * kDeferBlocks, 256, 0, s>>>(fa.def_e, fa.def_f, fa.def_cnt, lm, c0, ms->slots, ms->nbuckets - 1,
@@ -2460,6 +2469,20 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	uint64_t inserted = ctx->h_cnt[kCntInserted], changed = ctx->h_cnt[kCntChanged], ns_ins = ctx->h_cnt[kCntAux];
 	uint64_t npairs = ctx->h_cnt[kCntAux2];
 	const uint64_t novf = ctx->h_cnt[kCntAggOvf];
+	if (ctx->agg_variant != 7 && novf > gate) {
+		// too few partitions (the distinct-ratio guess was low): nothing was
+		// committed; the next attempt sizes them for at least what was seen
+		// (an overflowed partition held more than kAggLimit)
+		const double seen = (double)D + 2.0 * (double)novf * kAggLimit;
+		ctx->agg_distinct_ratio = std::max(ctx->agg_distinct_ratio, seen / (double)std::max<uint64_t>(run_recs, 1));
+		st->retries++;
+		if (fresh_ns) {
+			syzsig_set_free(nsp);
+			*ns = nullptr;
+		}
+		*regeom = true;
+		return SYZSIG_OK;
+	}
 	if (novf) {
 		// partitions past the LDS table: aggregated in HBM from their cells,
 		// then finalized with the atomic code (their elements are disjoint from
@@ -2558,9 +2581,14 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 {
 	if (ctx->cap_sd > 0 && !(ctx->agg_dbg & (SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL | 16)) &&
 	    !ctx->agg_counted_once) {
-		bool done = false;
-		const uint64_t retries0 = st->retries;
-		SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, c0, c1, lm, run_recs, st, pairs_out, npairs_io, &done));
+		bool done = false, regeom = false;
+		uint64_t retries0 = st->retries;
+		SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, c0, c1, lm, run_recs, st, pairs_out, npairs_io, &done, nullptr,
+		                         nullptr, &regeom));
+		if (regeom) {  // once more with partitions for what the first attempt counted
+			retries0 = st->retries;
+			SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, c0, c1, lm, run_recs, st, pairs_out, npairs_io, &done));
+		}
 		if (done)
 			return SYZSIG_OK;
 		// a spilled cell: this run is redone with counted cells, not capped ones again
@@ -2609,7 +2637,7 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 		fin<<<a.nregions, kFxThreads, 0, s>>>(
 		    a.dist_e, a.dist_f, a.cnt, a.nregions, lm, c0, ms->slots, ms->nbuckets - 1, ms_shift, nsp->slots,
 		    nsp->nbuckets - 1, ns_shift, b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2], ctx->d_cnt, def_e, def_f,
-		    &ctx->d_cnt[kCntDefer], (uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], ctx->agg_dbg, nullptr);
+		    &ctx->d_cnt[kCntDefer], (uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], ctx->agg_dbg, nullptr, nullptr, 0);
 		k_fin_deferred<<<2 * kDeferBlocks, 256, 0, s>>>(def_e, def_f, &ctx->d_cnt[kCntDefer], lm, c0, ms->slots,
 		                                                ms->nbuckets - 1, nsp->slots, nsp->nbuckets - 1, b->call_new,
 		                                                (uint64_t*)pr, &ctx->d_cnt[kCntAux2], ctx->d_cnt,
@@ -2657,9 +2685,14 @@ int agg_triage_optimistic(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, cons
 	LevelMap lm;
 	const int8_t lv[4] = {0, 1, 2, 3};
 	SYZ_TRY(level_map_from_levels(lv, 4, &lm));
-	bool bad = false;
-	const uint64_t retries0 = st->retries;
-	SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, 0, b->ncalls, lm, b->nrec, st, pairs, npairs, done, presence, &bad));
+	bool bad = false, regeom = false;
+	uint64_t retries0 = st->retries;
+	SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, 0, b->ncalls, lm, b->nrec, st, pairs, npairs, done, presence, &bad,
+	                         &regeom));
+	if (regeom) {  // once more with partitions for what the first attempt counted
+		retries0 = st->retries;
+		SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, 0, b->ncalls, lm, b->nrec, st, pairs, npairs, done, presence, &bad));
+	}
 	// a spilled cell: the planned path redoes the batch with counted cells
 	ctx->agg_counted_once = !*done && st->retries != retries0;
 	return SYZSIG_OK;

@@ -278,233 +278,6 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 }
 
 
-// ---------------------------------------------------------------- lane-owned
-// K2 without conflict rounds.  One wave per program.  Lane L owns the dedup
-// table's slots [128 L, 128 L + 128): a signal whose window {h..h+3} (h = sig
-// mod 8192) lies inside one lane's range only ever meets signals of that same
-// lane, so every lane replays its own signals one by one in trace order --
-// dedup() of executor.h:692-706 literally, nothing to detect or retry.  A
-// window that crosses into lane L+1 (h mod 128 >= 125: a "straddler", 3/128 of
-// the signals) is listed in both lanes; the lower lane executes it in the step
-// where both have it at the head of their lists.  The earliest pending
-// straddler always has (every earlier entry of either lane is done), so the
-// walk never stalls, and each lane's slots see their signals in trace order:
-// the result is the sequential one.
-// Per call, chunks of up to kLnChunk signals:
-//   A) load the PCs (the next chunk's loads in flight), K1 (sig_i = pc_i ^
-//      hash(pc_{i-1}), 0 before a call's first PC), cover_check, and an
-//      order-preserving split of the chunk into the 64 lane lists in LDS: per
-//      group of 64 signals, each signal ORs its lane bit into its owner's peer
-//      mask (ds_or_b64), so its rank among the group's signals of that owner
-//      is the popcount of the mask below it; a list that would pass kLnCap
-//      runs the walk on what is listed first;
-//   B) the walk: every lane takes its list's head each step, emit bits go to
-//      a bitmap by chunk position;
-//   C) the emitted signals, read back by position, to the output in trace
-//      order.
-// No workgroup barrier anywhere (one wave); LDS table in lane-interleaved
-// order (slot t at (t mod 128) * 64 + t / 128), so the lanes' table accesses
-// fall on 64 different banks.
-constexpr uint32_t kLnChunk = 1024, kLnGroups = kLnChunk / 64, kLnCap = 32;
-constexpr uint32_t kLnSlots = kDedupSize / 64;  // slots per lane
-constexpr uint32_t kLnRight = 0x8000u;          // list entry: a straddler's copy in the upper lane
-constexpr uint32_t kLnPosMask = 0x7FFFu;
-static_assert(kLnChunk <= kLnPosMask, "list positions");
-
-__device__ __forceinline__ uint32_t ln_addr(uint32_t t)
-{
-	return (t & (kLnSlots - 1)) * 64 + (t >> 7);
-}
-
-__global__ __launch_bounds__(64) void k_edge_lanes(const uint64_t* __restrict__ pcs, uint64_t npc,
-                                                   const uint64_t* __restrict__ call_start,
-                                                   const uint32_t* __restrict__ call_len, uint64_t ncalls,
-                                                   const uint32_t* __restrict__ prog_call, uint64_t nprog,
-                                                   uint32_t* sigs, uint32_t* sig_cnt, uint32_t* completed,
-                                                   unsigned long long* cnt)
-{
-	__shared__ uint32_t tab[kDedupSize];           // lane-interleaved dedup table
-	__shared__ uint32_t lsig[kLnCap * 64];         // entry k of lane L's list at k * 64 + L
-	__shared__ uint16_t lpos[kLnCap * 64];         // its chunk position (| kLnRight)
-	__shared__ uint32_t sbuf[kLnChunk];            // the chunk's signals by position
-	__shared__ uint32_t emitm[kLnChunk / 32];      // emitted, by position
-	__shared__ unsigned long long peer[64];        // per owner: lanes of the group listing into it
-	const uint32_t lane = lane_id();
-	const uint64_t below = (1ull << lane) - 1;
-	uint64_t err = 0;
-	peer[lane] = 0;
-	for (uint64_t p = blockIdx.x; p < nprog; p += gridDim.x) {
-		const uint64_t cb = prog_call[p], ce = prog_call[p + 1];
-		if (cb > ce || ce > ncalls) {
-			err += lane == 0;
-			continue;
-		}
-		// fresh table per program (common_linux.h:1995-2030: fork zeroes it)
-		for (uint32_t i = lane; i < kDedupSize / 4; i += 64)
-			reinterpret_cast<uint4*>(tab)[i] = make_uint4(0, 0, 0, 0);
-		__builtin_amdgcn_wave_barrier();
-		uint64_t done = ce - cb;
-		for (uint64_t c = cb; c < ce; c++) {
-			const uint64_t start = call_start[c];
-			const uint32_t len = call_len[c];
-			if (len >= kCoverSize || start > npc || len > npc - start) {
-				// executor_linux.cc:186-187 fail("too much cover") / malformed input
-				err += lane == 0;
-				done = c - cb;
-				break;
-			}
-			uint32_t nsig = 0, carry = 0;  // carry: hash of the previous group's last PC (0 at the call start)
-			const uint64_t last = start + (len ? len - 1 : 0);
-			const uint32_t nch = (len + kLnChunk - 1) / kLnChunk;
-			bool aborted = false;
-			// loads are unconditional (index clamped into the call)
-			uint64_t buf[kLnGroups];
-			if (len) {
-#pragma unroll
-				for (uint32_t g = 0; g < kLnGroups; g++)
-					buf[g] = pcs[min<uint64_t>(start + g * 64 + lane, last)];
-			}
-			for (uint32_t q = 0; q < nch; q++) {
-				const uint32_t clen = min(len - q * kLnChunk, kLnChunk);
-				uint64_t cur[kLnGroups];
-#pragma unroll
-				for (uint32_t g = 0; g < kLnGroups; g++)
-					cur[g] = buf[g];
-				if (q + 1 < nch) {  // the next chunk's loads fly during this one
-#pragma unroll
-					for (uint32_t g = 0; g < kLnGroups; g++)
-						buf[g] = pcs[min<uint64_t>(start + (uint64_t)(q + 1) * kLnChunk + g * 64 + lane, last)];
-				}
-				for (uint32_t i = lane; i < kLnChunk / 32; i += 64)
-					emitm[i] = 0;
-				uint32_t fill = 0;  // entries in this lane's list
-				// B) the walk over what is listed
-				auto walk = [&]() {
-					uint32_t idx = 0;
-					for (;;) {
-						const bool has = idx < fill;
-						if (!__ballot(has))
-							break;
-						const uint32_t at = (has ? idx : 0) * 64 + lane;
-						const uint32_t e = lsig[at];
-						const uint32_t ps = has ? (uint32_t)lpos[at] : 0xFFFFFFFFu;
-						const uint32_t up = __shfl(ps, (lane + 1) & 63, 64), dn = __shfl(ps, (lane - 1) & 63, 64);
-						const bool right = ps & kLnRight;
-						const bool strad = ((e & (kLnSlots - 1)) >= kLnSlots - 3) && !right;
-						// a straddler goes once both lanes have it at the head
-						const bool ready = has && (right ? dn == (ps & kLnPosMask) : !strad || up == (ps | kLnRight));
-						if (ready && !right) {
-							uint32_t eqm = 0, zm = 0;
-#pragma unroll
-							for (uint32_t i = 0; i < 4; i++) {
-								const uint32_t t = tab[ln_addr((e + i) & (kDedupSize - 1))];
-								eqm |= (uint32_t)(t == e) << i;
-								zm |= (uint32_t)(t == 0) << i;
-							}
-							const uint32_t first = __builtin_ctz(eqm | zm | 16u);
-							if (!((eqm >> first) & 1)) {  // a write: insert, or the forced overwrite at h
-								tab[ln_addr((e + (first & 3)) & (kDedupSize - 1))] = e;
-								const uint32_t pp = ps & kLnPosMask;
-								atomicOr(&emitm[pp >> 5], 1u << (pp & 31));
-							}
-						}
-						idx += ready;
-					}
-					fill = 0;
-					__builtin_amdgcn_wave_barrier();
-				};
-				// A) K1 + cover_check + the split into the lane lists
-#pragma unroll
-				for (uint32_t g = 0; g < kLnGroups; g++) {
-					if (g * 64 < clen) {  // (uniform)
-						const uint32_t pos = g * 64 + lane;
-						const bool valid = pos < clen;
-						const uint64_t pc = valid ? cur[g] : 0;
-						const uint32_t h = exec_hash((uint32_t)pc);
-						uint32_t up = __shfl_up(h, 1, 64);
-						if (lane == 0)
-							up = carry;
-						carry = __shfl(h, 63, 64);
-						// cover_check (executor_linux.cc:196-204): doexit(0), this call and
-						// the rest of the program publish nothing
-						if (__ballot(valid && !cover_check(pc))) {
-							aborted = true;
-							break;
-						}
-						const uint32_t sig = (uint32_t)pc ^ up;
-						sbuf[pos] = sig;
-						const uint32_t t0 = sig & (kDedupSize - 1), own = t0 >> 7, own2 = (own + 1) & 63;
-						const bool strad = (t0 & (kLnSlots - 1)) >= kLnSlots - 3;
-						// the lanes in S list their signals (and straddler copies); false
-						// if some list would take more than kLnCap of them at once
-						auto list = [&](uint64_t S) -> bool {
-							const bool in = valid && ((S >> lane) & 1);
-							if (in)
-								atomicOr(&peer[own], 1ull << lane);
-							if (in && strad)
-								atomicOr(&peer[own2], 1ull << lane);
-							__builtin_amdgcn_wave_barrier();
-							const uint64_t m1 = peer[own], m2 = peer[own2], mine = peer[lane];
-							const uint32_t add = (uint32_t)__popcll(mine);
-							__builtin_amdgcn_wave_barrier();
-							peer[lane] = 0;
-							__builtin_amdgcn_wave_barrier();
-							if (__ballot(fill + add > kLnCap))
-								walk();  // a list is full: walk what is listed (all earlier in trace order)
-							if (__ballot(add > kLnCap))
-								return false;  // (>= 33 signals of the group in one list: half a group at a time)
-							const uint32_t b1 = __shfl(fill, own, 64), b2 = __shfl(fill, own2, 64);
-							if (in) {
-								const uint32_t k = (b1 + (uint32_t)__popcll(m1 & below)) * 64 + own;
-								lsig[k] = sig;
-								lpos[k] = (uint16_t)pos;
-							}
-							if (in && strad) {
-								const uint32_t k = (b2 + (uint32_t)__popcll(m2 & below)) * 64 + own2;
-								lsig[k] = sig;
-								lpos[k] = (uint16_t)(pos | kLnRight);
-							}
-							fill += add;
-							__builtin_amdgcn_wave_barrier();
-							return true;
-						};
-						if (!list(~0ull)) {
-							list(0xFFFFFFFFull);
-							list(0xFFFFFFFF00000000ull);
-						}
-					}
-				}
-				if (aborted)
-					break;
-				walk();
-				// C) emitted signals in trace order
-				for (uint32_t g = 0; g * 64 < clen; g++) {
-					const uint32_t pos = g * 64 + lane;
-					const bool on = pos < clen && ((emitm[pos >> 5] >> (pos & 31)) & 1);
-					const uint64_t m = __ballot(on);
-					if (on)
-						sigs[start + nsig + lane_rank(m)] = sbuf[pos];
-					nsig += (uint32_t)__popcll(m);
-				}
-				__builtin_amdgcn_wave_barrier();
-			}
-			if (aborted) {
-				done = c - cb;
-				break;
-			}
-			if (lane == 0)
-				sig_cnt[c] = nsig;
-		}
-		// calls not published (aborted and later) report no signal (ipc.go:362-365)
-		for (uint64_t c = cb + done + lane; c < ce; c += 64)
-			sig_cnt[c] = 0;
-		if (lane == 0)
-			completed[p] = (uint32_t)done;
-		__builtin_amdgcn_wave_barrier();
-	}
-	if (lane == 0 && err)
-		atomicAdd(&cnt[kCntError], err);
-}
 }  // namespace syz
 
 using namespace syz;
@@ -525,11 +298,7 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 	const int grid = (int)std::min<uint64_t>(nprog, 256 * 4);
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
-	if (ctx->edge_impl == 1)
-		k_edge_lanes<<<(int)std::min<uint64_t>(nprog, 65535), 64, 0, ctx->stream>>>(
-		    d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call, nprog, d_sigs, d_sig_cnt, d_completed,
-		    ctx->d_cnt);
-	else if (ctx->edge_waves == 8)
+	if (ctx->edge_waves == 8)
 		k_edge_dedup<8><<<grid, 512, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	else if (ctx->edge_waves == 2)

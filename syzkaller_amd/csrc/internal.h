@@ -104,8 +104,7 @@ struct syzsig_ctx {
 	double agg_distinct_ratio = 0;        // distinct/records of the last aggregated run (sizes the next)
 	float cap_sd = syz::kCapSdDefault;    // capped-cell slack in standard deviations (agg.hip; 0 = counted cells)
 	float cap_sd_entry = syz::kCapSdDefault;  // the same for Minimize's runs
-	bool agg_counted_once = false;
-	int edge_impl = 0;                    // K1+K2 kernel: 0 conflict rounds, 1 lane-owned slot ranges (SYZSIG_EDGE_IMPL)        // the next agg_aggregate takes counted cells (a fused run spilled)
+	bool agg_counted_once = false;        // the next agg_aggregate takes counted cells (a fused run spilled)
 	uint32_t edge_waves = 4;              // waves per program of k_edge_dedup (4 or 8; SYZSIG_EDGE_WAVES)
 	uint32_t agg_variant = 0;             // k_agg pipeline variant (SYZSIG_AGG_VARIANT; tuning)
 	uint32_t agg_dbg = 0;                 // SYZSIG_DEBUG_* path flags; timing-only bits need -DSYZ_EXPERIMENTS

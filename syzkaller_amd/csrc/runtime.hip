@@ -129,8 +129,6 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 		c->agg_dbg &= syz::kDebugResultPreserving;
 #endif
 	}
-	if (const char* v = getenv("SYZSIG_EDGE_IMPL"))
-		c->edge_impl = atoi(v) == 1 ? 1 : 0;
 	if (const char* v = getenv("SYZSIG_EDGE_WAVES"))
 		c->edge_waves = atoi(v) == 8 ? 8 : atoi(v) == 2 ? 2 : atoi(v) == 1 ? 1 : 4;
 	if (const char* v = getenv("SYZSIG_AGG_PARTS")) {
