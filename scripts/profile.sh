@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 # PROF_CMD=scripts/min_only.py for the Minimize line alone -- one workload per
 # profile, so per-kernel averages never mix two workloads' launches
 CMD=${PROF_CMD:-bench.py}
-ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu --no-min}
+ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu --no-min --no-c5 --no-c4 --no-c1}
 [ "$CMD" != bench.py ] && ARGS=${BENCH_ARGS:-}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- python3 $CMD $ARGS > "$OUT/trace.log" 2>&1
 echo "[trace] exit $?" | tee -a "$OUT/status.log"

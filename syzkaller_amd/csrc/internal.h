@@ -96,7 +96,7 @@ struct syzsig_ctx {
 	// small state, 7-10 host uploads of minimize, 11-14 triage partitions and
 	// minimize internals and triage pairs (13-15), 16-23 + 30-31 triage aggregation,
 	// 24-29 check_new_signal uploads, 32-33 the finalize's deferred lists, 40-47 manager poll
-	syz::Workspace ws[48];
+	syz::Workspace ws[56];
 	bool timing = false;                  // HIP events around triage kernels
 	// tuning knobs (defaults; SYZSIG_* environment overrides read at ctx creation)
 	int part_mode = 1;                    // 0 = never use the aggregation path (agg.hip)

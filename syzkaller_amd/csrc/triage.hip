@@ -26,6 +26,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "internal.h"
 
 namespace syz {
@@ -712,6 +714,145 @@ int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm)
 	return SYZSIG_OK;
 }
 
+// ---- records mode by sorting (the owner side of a sharded step, large
+// inputs): the records sorted by (element, serial) -- one radix sort, the
+// record's index carried -- so each element's records are a contiguous run in
+// serial order, and one thread per run replays checkNewSignal for it: the
+// running maximum starts at M0[e] (one shard probe per distinct element, not
+// per record), a record is new iff its prio exceeds it (and so is a duplicate
+// of a new record in the same call, as DiffRaw collapses duplicates); the
+// run's final maximum, when raised, is merged into the shard and newSignal.
+// Sort key: e << 24 | serial (bits 0..55, the sorted ones) | level << 56.
+__global__ void k_recs_keys(const uint64_t* __restrict__ recs, uint64_t n, uint32_t nlev, uint64_t* keys,
+                            uint32_t* vals, unsigned long long* bad)
+{
+	uint64_t nbad = 0;
+	for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t x = recs[r];
+		const uint64_t l = (x >> 24) & 0xff;
+		nbad += l >= nlev;
+		keys[r] = ((x >> 32) << 24) | (x & kSerialMask) | (l << 56);
+		vals[r] = (uint32_t)r;
+	}
+	block_count(bad, nbad);
+}
+
+__global__ void k_recs_walk(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ order, uint64_t n,
+                            LevelMap lm, uint64_t* ms, uint64_t ms_bmask, uint64_t* ns, uint64_t ns_bmask,
+                            uint8_t* flags, unsigned long long* ctr)
+{
+	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0, distinct = 0;
+	constexpr uint64_t kElemSerial = (1ull << 56) - 1;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t ki = sk[i];
+		const uint32_t e = (uint32_t)((ki & kElemSerial) >> 24);
+		if (i > 0 && (uint32_t)((sk[i - 1] & kElemSerial) >> 24) == e)
+			continue;  // not the head of e's run
+		distinct++;
+		uint64_t v = 0;
+		const bool present = tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v);
+		const int m0 = present ? (int)slot_prio(v) : -1000;  // absent: below every prio (signal.go:93-95)
+		int m = m0;
+		uint32_t last_new = 0xFFFFFFFFu;
+		for (uint64_t j = i; j < n; j++) {
+			const uint64_t kj = sk[j];
+			if ((uint32_t)((kj & kElemSerial) >> 24) != e)
+				break;
+			const uint32_t k = (uint32_t)kj & kSerialMask;
+			const int p = lm.val[(kj >> 56) & 3];
+			if (p > m || k == last_new) {
+				flags[order[j]] = 1;
+				m = max(m, p);
+				last_new = k;
+			}
+		}
+		if (m > m0) {  // maxSignal.Merge / newSignal.Merge of the element's final prio
+			changed++;
+			inserted += !present;
+			ovf += tbl_merge(ms, ms_bmask, e, (int8_t)m) < 0;
+			const int r = tbl_merge(ns, ns_bmask, e, (int8_t)m);
+			ns_ins += r == 1;
+			ovf += r < 0;
+		}
+	}
+	block_count(&ctr[kCntInserted], inserted);
+	block_count(&ctr[kCntChanged], changed);
+	block_count(&ctr[kCntAux], ns_ins);
+	block_count(&ctr[kCntOverflow], ovf);
+	block_count(&ctr[kCntDistinct], distinct);
+}
+
+__global__ void k_recs_heads(const uint64_t* __restrict__ sk, uint64_t n, unsigned long long* heads)
+{
+	constexpr uint64_t kElem = ((1ull << 56) - 1) & ~(uint64_t)kSerialMask;
+	uint64_t h = 0;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+		h += i == 0 || ((sk[i] ^ sk[i - 1]) & kElem) != 0;
+	block_count(heads, h);
+}
+
+static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t n,
+                                 const LevelMap& lm, uint8_t* new_flags, syzsig_batch_stats* st)
+{
+	const hipStream_t s = ctx->stream;
+	void *dk, *dtmp;
+	SYZ_TRY(ws_get(ctx, 48, n * 24 + 256, &dk));
+	uint64_t* keys = (uint64_t*)dk;
+	uint64_t* keys2 = keys + n;
+	uint32_t* vals = (uint32_t*)(keys2 + n);
+	uint32_t* order = vals + n;
+	size_t tmp_bytes = 0;
+	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
+	SYZ_TRY(ws_get(ctx, 49, tmp_bytes + 64, &dtmp));
+	SYZ_TRY(counters_reset(ctx));
+	k_recs_keys<<<grid_for(n, 256, 8192), 256, 0, s>>>(recs, n, lm.n, keys, vals, &ctx->d_cnt[kCntError]);
+	SYZ_HIP(hipGetLastError());
+	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
+	k_recs_heads<<<grid_for(n, 256, 4096), 256, 0, s>>>(keys2, n, &ctx->d_cnt[kCntDistinct]);
+	SYZ_HIP(hipGetLastError());
+	SYZ_TRY(counters_fetch(ctx));
+	if (ctx->h_cnt[kCntError])
+		return fail(SYZSIG_EINVAL, "triage_records: a record's prio level is out of range");
+	// room for every distinct element changing
+	const uint64_t D = ctx->h_cnt[kCntDistinct];
+	SYZ_TRY(set_reserve(ms, D));
+	const bool fresh_ns = !*ns;
+	if (fresh_ns)
+		SYZ_TRY(syzsig_set_make(ctx, D, ns));  // newSignal.Merge allocates a nil receiver (signal.go:121-125)
+	syzsig_set* nsp = *ns;
+	SYZ_TRY(set_reserve_load(nsp, D, kHardLoad));
+	SYZ_TRY(counters_reset(ctx));
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
+	k_recs_walk<<<grid_for(n, 256, 8192), 256, 0, s>>>(keys2, order, n, lm, ms->slots, ms->nbuckets - 1, nsp->slots,
+	                                                   nsp->nbuckets - 1, new_flags, ctx->d_cnt);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[3], s));
+	SYZ_TRY(counters_fetch(ctx));
+	if (ctx->timing) {
+		float t = 0;
+		SYZ_HIP(hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]));
+		st->decide_ms += t;
+	}
+	if (ctx->h_cnt[kCntOverflow])
+		return fail(SYZSIG_EIO, "triage_records: table overflow after reserve (internal error)");
+	const uint64_t changed = ctx->h_cnt[kCntChanged];
+	ms->len += ctx->h_cnt[kCntInserted];
+	nsp->len += ctx->h_cnt[kCntAux];
+	if (fresh_ns && changed == 0) {
+		syzsig_set_free(nsp);
+		*ns = nullptr;
+	}
+	st->inserted += ctx->h_cnt[kCntInserted];
+	st->changed += changed;
+	st->candidates += changed;
+	st->distinct += ctx->h_cnt[kCntDistinct];
+	st->survivors += ctx->h_cnt[kCntDistinct];
+	st->runs++;
+	return SYZSIG_OK;
+}
+
 int triage_records_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t nrec,
                         const int8_t* levels, uint32_t nlevels, uint8_t* new_flags, syzsig_batch_stats* st)
 {
@@ -721,6 +862,13 @@ int triage_records_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const 
 	if (nrec == 0)
 		return SYZSIG_OK;
 	SYZ_HIP(hipMemsetAsync(new_flags, 0, nrec, ctx->stream));
+	if (nrec >= (1ull << 20) && nrec < (1ull << 31) && ctx->part_mode != 0) {
+		SYZ_TRY(triage_records_sorted(ctx, ms, ns, recs, nrec, lm, new_flags, st));
+		if ((double)ms->len > kMaxLoad * (double)ms->nslots())
+			SYZ_TRY(set_rehash(ms, buckets_for(ms->len), false));
+		st->new_signal_len = syzsig_len(*ns);
+		return SYZSIG_OK;
+	}
 	SYZ_TRY(set_ensure_triage_state(ms));
 	const uint64_t nseg = (nrec + kSegRecs - 1) / kSegRecs;
 	void *cs, *cm, *cc;

@@ -406,3 +406,50 @@ def test_triage_c2_properties(gpu):
     n_before = ms.Len()
     bits3, cnew3, st3 = gpu.triage(ms, ns3, ds, dcs, dcnt, dprio)
     assert int(cnew3.sum()) == 0 and int(bits3.count_nonzero()) == 0 and ns3.is_nil() and ms.Len() == n_before
+
+
+@pytest.mark.parametrize("agg", [1, 0])
+def test_records_mode_vs_oracle(gpu, agg):
+    """Records mode (the owner side of a sharded step, triage.hip
+    triage_records_impl): ~1.2M records (e, level, serial) in a shuffled order,
+    each serial one call of up to 6 distinct elements at one level, against a
+    1M-element shard.  agg=1 takes the sorted path (records sorted by
+    (element, serial), one thread per element), agg=0 the per-record probe path; both
+    must flag exactly the records the oracle's sequential checkNewSignal over
+    the calls in serial order marks new, and leave the same shard and
+    newSignal."""
+    from syzkaller_amd import signal as S
+
+    rng = np.random.default_rng(77)
+    pool = np.unique(rng.integers(0, 1 << 32, 2_500_000, dtype=np.uint64).astype(np.uint32))
+    ncall = 300_000
+    clen = rng.integers(1, 7, ncall).astype(np.uint32)
+    nrec = int(clen.sum())
+    assert nrec >= 1 << 20
+    cs = np.zeros(ncall, np.uint64)
+    cs[1:] = np.cumsum(clen[:-1].astype(np.uint64))
+    # distinct elements inside a call: consecutive picks of a random walk through the pool
+    start = rng.integers(0, pool.size, ncall)
+    idx = (np.repeat(start, clen) + (np.arange(nrec) - np.repeat(cs.astype(np.int64), clen)) * 7919) % pool.size
+    sigs = pool[idx]
+    lvl = rng.integers(0, 4, ncall).astype(np.uint8)
+    serial = np.repeat(np.arange(ncall, dtype=np.uint64), clen)
+    rec = (sigs.astype(np.uint64) << np.uint64(32)) | (np.repeat(lvl, clen).astype(np.uint64) << np.uint64(24)) | serial
+    perm = rng.permutation(nrec)
+    m0e = np.unique(rng.choice(pool, 1_000_000))
+    m0p = rng.integers(0, 4, m0e.size).astype(np.int8)
+    ms = S.Serial(m0e, m0p).Deserialize(gpu.eng)
+    ns = S.Signal(None, gpu.eng)
+    drec = torch.from_numpy(rec[perm].view(np.int64)).to(gpu.dev)
+    flags = torch.zeros(nrec, dtype=torch.uint8, device=gpu.dev)
+    gpu.eng.set_agg(agg, 0)
+    try:
+        st = gpu.triage_records(ms, ns, drec, [0, 1, 2, 3], flags)
+    finally:
+        gpu.eng.set_agg(1, 0)
+    oms, ons, obits, _ = O.triage_batch(m0e, m0p, sigs, cs, clen, lvl)
+    onew = np.unpackbits(obits.view(np.uint8), bitorder="little")[:nrec].astype(np.uint8)
+    np.testing.assert_array_equal(_u(flags, np.uint8), onew[perm])
+    assert ms.to_dict() == oms.to_dict()
+    assert ns.to_dict() == ons.to_dict()
+    assert (st["distinct"] > 0) == (agg == 1), st  # the sorted path counts distinct elements
