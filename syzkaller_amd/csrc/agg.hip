@@ -754,8 +754,8 @@ __global__ __launch_bounds__(256) void k_chunk_sizes(const uint32_t* __restrict_
 		sizes[ch] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-__global__ __launch_bounds__(1024) void k_cell_plan(const uint64_t* __restrict__ sizes, uint64_t nchunks, uint32_t P,
-                                                    float sd, uint64_t* base, uint32_t* cap)
+__device__ __forceinline__ void cell_plan(const uint64_t* __restrict__ sizes, uint64_t nchunks, uint32_t P, float sd,
+                                          uint64_t* base, uint32_t* cap)
 {
 	__shared__ uint64_t wsum[16];
 	uint64_t run = 0;
@@ -790,6 +790,92 @@ __global__ __launch_bounds__(1024) void k_cell_plan(const uint64_t* __restrict__
 		run += tot;
 		__syncthreads();
 	}
+}
+
+__global__ __launch_bounds__(1024) void k_cell_plan(const uint64_t* __restrict__ sizes, uint64_t nchunks, uint32_t P,
+                                                    float sd, uint64_t* base, uint32_t* cap)
+{
+	cell_plan(sizes, nchunks, P, sd, base, cap);
+}
+
+// The one-sync triage run's first pass, one block per chunk of calls: the
+// chunk's records (for k_cell_plan_fast), call ranges checked, whether a
+// prio outside 0..3 occurs, and call_new zeroed.  part[2 ch] = records,
+// part[2 ch + 1] = bad ranges | other prio << 63.
+__global__ __launch_bounds__(256) void k_fast_prep(const uint64_t* __restrict__ call_start,
+                                                   const uint32_t* __restrict__ call_len,
+                                                   const uint8_t* __restrict__ call_prio, uint64_t c0, uint64_t c1,
+                                                   uint32_t ibits, uint64_t nrec_space, uint64_t* sizes,
+                                                   uint64_t* part, uint8_t* call_new)
+{
+	const uint64_t ch = blockIdx.x, cbeg = c0 + (ch << ibits), cend = min<uint64_t>(c1, cbeg + (1ull << ibits));
+	uint64_t tot = 0, bad = 0, other = 0;
+	for (uint64_t c = cbeg + threadIdx.x; c < cend; c += blockDim.x) {
+		const uint64_t st = call_start[c];
+		const uint32_t ln = call_len[c];
+		tot += ln;
+		bad += st > nrec_space || ln > nrec_space - st || ln > kSerialMask;
+		other |= call_prio[c] > 3;
+		call_new[c] = 0;
+	}
+	tot = wave_sum_u64(tot);
+	bad = wave_sum_u64(bad);
+	other = wave_sum_u64(other);
+	__shared__ uint64_t ws[4][3];
+	if (lane_id() == 0) {
+		ws[threadIdx.x >> 6][0] = tot;
+		ws[threadIdx.x >> 6][1] = bad;
+		ws[threadIdx.x >> 6][2] = other;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		uint64_t t = 0, b = 0, o = 0;
+		for (int w = 0; w < 4; w++) {
+			t += ws[w][0];
+			b += ws[w][1];
+			o += ws[w][2];
+		}
+		sizes[ch] = t;
+		part[2 * ch] = t;
+		part[2 * ch + 1] = b | (o ? 1ull << 63 : 0);
+	}
+}
+
+// k_cell_plan for the one-sync run: the counters are zeroed here (npairs
+// preset), the assumptions checked from k_fast_prep's partials -- prios in
+// 0..3, valid ranges, at most `guess` records -- and the run's void flag
+// (ctr[kCntSpill]) set before anything reads it.
+__global__ __launch_bounds__(1024) void k_cell_plan_fast(const uint64_t* __restrict__ sizes, uint64_t nchunks,
+                                                         uint32_t P, float sd, uint64_t* base, uint32_t* cap,
+                                                         const uint64_t* __restrict__ part, uint64_t guess,
+                                                         uint64_t npairs0, unsigned long long* ctr)
+{
+	__shared__ unsigned long long s_tot, s_flag;
+	if (threadIdx.x == 0) {
+		s_tot = 0;
+		s_flag = 0;
+	}
+	if (threadIdx.x < kNumCounters)
+		ctr[threadIdx.x] = threadIdx.x == kCntAux2 ? npairs0 : 0;
+	__syncthreads();
+	uint64_t t = 0, f = 0;
+	for (uint64_t c = threadIdx.x; c < nchunks; c += blockDim.x) {
+		t += part[2 * c];
+		f |= part[2 * c + 1];
+	}
+	t = wave_sum_u64(t);
+	for (int o = 32; o > 0; o >>= 1)
+		f |= __shfl_xor(f, o, 64);
+	if (lane_id() == 0) {
+		atomicAdd(&s_tot, (unsigned long long)t);
+		atomicOr(&s_flag, (unsigned long long)f);
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		ctr[kCntRecords] = s_tot;
+		ctr[kCntSpill] = s_flag || s_tot > guess ? 2u : 0u;
+	}
+	cell_plan(sizes, nchunks, P, sd, base, cap);
 }
 
 // ---------------------------------------------------------------- aggregation
@@ -2278,21 +2364,6 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	return SYZSIG_OK;
 }
 
-// An optimistic run's assumptions, checked on device from the presence pass
-// (mask[8], total, bad at `presence`): prios in 0..3, at most `guess` records,
-// valid call ranges.  Otherwise *ovf = 2 and the run commits nothing.
-__global__ void k_fast_check(const uint32_t* __restrict__ presence, uint64_t guess, uint32_t* ovf)
-{
-	if (threadIdx.x != 0)
-		return;
-	uint32_t other = presence[0] & ~0xFu;
-	for (int i = 1; i < 8; i++)
-		other |= presence[i];
-	const uint64_t total = ((const uint64_t*)presence)[4], bad = ((const uint64_t*)presence)[5];
-	if (other || bad || total > guess)
-		*ovf = 2u;
-}
-
 // The fused fast path of one triage run (k_agg_fin): scatter into capped
 // cells, then aggregation + finalize in one launch, with one host
 // synchronisation at the end.  maxSignal and newSignal are reserved for the
@@ -2303,7 +2374,7 @@ __global__ void k_fast_check(const uint32_t* __restrict__ presence, uint64_t gue
 // counted-cell path (a cell spilled; the slack is doubled for the next run).
 static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0,
                             uint64_t c1, const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st,
-                            uint64_t** pairs_out, uint64_t* npairs_io, bool* done, const void* presence = nullptr,
+                            uint64_t** pairs_out, uint64_t* npairs_io, bool* done, bool fast = false,
                             bool* assumed_bad = nullptr, bool* regeom = nullptr)
 {
 	*done = false;
@@ -2353,7 +2424,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	uint32_t* ccnt = ccap + nchunks;
 	uint32_t* ovf = ccnt + (uint64_t)S * nchunks;
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
-	if (presence && *npairs_io == 0 && b->new_pairs && b->new_pairs_cap >= 4 * d_max) {
+	if (fast && *npairs_io == 0 && b->new_pairs && b->new_pairs_cap >= 4 * d_max) {
 		pr = b->new_pairs;  // every possible pair fits the caller's buffer: no copy afterwards
 	} else {
 		SYZ_TRY(ws_grow_keep(ctx, 15, (*npairs_io + 4 * d_max) * 8 + 64, *npairs_io * 8, &pr));
@@ -2362,16 +2433,27 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	SYZ_TRY(ws_get(ctx, 32, d_max * 20 + 64, &dd));
 	SYZ_TRY(ws_get(ctx, 33, d_max * 8 + 64, &dn));
 	const hipStream_t s = ctx->stream;
-	SYZ_TRY(counters_reset(ctx));
-	memcpy(ctx->h_pin + kPinPairs, npairs_io, 8);  // consumed before the counters_fetch below
-	SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], ctx->h_pin + kPinPairs, 8, hipMemcpyHostToDevice, s));
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
-	SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
-	if (presence)
-		k_fast_check<<<1, 64, 0, s>>>((const uint32_t*)presence, run_recs, ovf);
-	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.ibits, sizes);
-	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap);
+	if (fast) {
+		// two launches before the scatter: per-chunk sizes and checks (call_new
+		// zeroed too), then the cell plan, which also zeroes the counters and
+		// sets the run's void flag (ovf = the low word of ctr[kCntSpill])
+		void* dpart;
+		SYZ_TRY(ws_get(ctx, 54, nchunks * 16 + 64, &dpart));
+		ovf = (uint32_t*)&ctx->d_cnt[kCntSpill];
+		k_fast_prep<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_start, b->call_len, b->call_prio, c0, c1, g.ibits, b->nrec,
+		                                              sizes, (uint64_t*)dpart, b->call_new);
+		k_cell_plan_fast<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap, (const uint64_t*)dpart, run_recs,
+		                                    *npairs_io, ctx->d_cnt);
+	} else {
+		SYZ_TRY(counters_reset(ctx));
+		memcpy(ctx->h_pin + kPinPairs, npairs_io, 8);  // consumed before the counters_fetch below
+		SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], ctx->h_pin + kPinPairs, 8, hipMemcpyHostToDevice, s));
+		SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
+		k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.ibits, sizes);
+		k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap);
+	}
 	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
 	k_agg_scatter_blk<false><<<(int)std::min<uint64_t>(nchunks, 2048), kAggThreads, 0, s>>>(
 	    b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, g, AggSrc{nullptr, 1, 0, 0}, cc,
@@ -2428,6 +2510,8 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		    fa.def_cnt, fa.def_ns, fa.def_ns_cnt, ctx->agg_dbg, ovf, &ctx->d_cnt[kCntAggOvf], gate);
 		SYZ_HIP(hipGetLastError());
 	}
+	// (the deferred lists in a launch of their own: taken by the finalize's last
+	// block instead, they made the finalize 1.03 ms instead of 0.27 at C2)
 	k_fin_deferred<<<2 * kDeferBlocks, 256, 0, s>>>(fa.def_e, fa.def_f, fa.def_cnt, lm, c0, ms->slots, ms->nbuckets - 1,
 	                                                nsp->slots, nsp->nbuckets - 1, b->call_new, (uint64_t*)pr,
 	                                                fa.npairs, ctx->d_cnt, fa.def_ns, fa.def_ns_cnt);
@@ -2435,8 +2519,13 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[3], s));
 	uint32_t* hov = (uint32_t*)(ctx->h_pin + kPinCounts);
-	SYZ_HIP(hipMemcpyAsync(hov, ovf, 4, hipMemcpyDeviceToHost, s));
+	if (!fast)
+		SYZ_HIP(hipMemcpyAsync(hov, ovf, 4, hipMemcpyDeviceToHost, s));
 	SYZ_TRY(counters_fetch(ctx));  // the run's one synchronisation
+	if (fast) {
+		*hov = (uint32_t)ctx->h_cnt[kCntSpill];
+		st->records = ctx->h_cnt[kCntRecords];
+	}
 	if (ctx->timing) {
 		float t0 = 0, t1 = 0, t2 = 0;
 		SYZ_HIP(hipEventElapsedTime(&t0, ctx->ev[0], ctx->ev[1]));
@@ -2583,7 +2672,7 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 	    !ctx->agg_counted_once) {
 		bool done = false, regeom = false;
 		uint64_t retries0 = st->retries;
-		SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, c0, c1, lm, run_recs, st, pairs_out, npairs_io, &done, nullptr,
+		SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, c0, c1, lm, run_recs, st, pairs_out, npairs_io, &done, false,
 		                         nullptr, &regeom));
 		if (regeom) {  // once more with partitions for what the first attempt counted
 			retries0 = st->retries;
@@ -2676,7 +2765,7 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 }
 
 int agg_triage_optimistic(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b,
-                          const void* presence, syzsig_batch_stats* st, uint64_t** pairs, uint64_t* npairs, bool* done)
+                          syzsig_batch_stats* st, uint64_t** pairs, uint64_t* npairs, bool* done)
 {
 	*done = false;
 	if (ctx->cap_sd <= 0 || ctx->agg_counted_once ||
@@ -2687,11 +2776,11 @@ int agg_triage_optimistic(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, cons
 	SYZ_TRY(level_map_from_levels(lv, 4, &lm));
 	bool bad = false, regeom = false;
 	uint64_t retries0 = st->retries;
-	SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, 0, b->ncalls, lm, b->nrec, st, pairs, npairs, done, presence, &bad,
+	SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, 0, b->ncalls, lm, b->nrec, st, pairs, npairs, done, true, &bad,
 	                         &regeom));
 	if (regeom) {  // once more with partitions for what the first attempt counted
 		retries0 = st->retries;
-		SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, 0, b->ncalls, lm, b->nrec, st, pairs, npairs, done, presence, &bad));
+		SYZ_TRY(agg_triage_fused(ctx, ms, ns, b, 0, b->ncalls, lm, b->nrec, st, pairs, npairs, done, true, &bad));
 	}
 	// a spilled cell: the planned path redoes the batch with counted cells
 	ctx->agg_counted_once = !*done && st->retries != retries0;

@@ -57,6 +57,8 @@ enum Counter : int {
 	kCntDeferNs,        // triage finalize: newSignal merges deferred to the atomic path
 	kCntDistinct,       // fused triage: distinct elements aggregated
 	kCntAggOvf,         // fused triage: partitions that overflowed the LDS table
+	kCntSpill,          // one-sync triage run: its void flag (low 32 bits; 1 = a cell spilled, 2 = assumptions)
+	kCntRecords,        // one-sync triage run: the batch's records
 	kNumCounters = 16,
 };
 
@@ -192,15 +194,14 @@ int batch_total_records(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t* total,
 int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0, uint64_t c1,
                    const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st, uint64_t** pairs,
                    uint64_t* npairs);
-// The whole batch as one aggregation run without waiting for its prio
-// presence pass: levels 0..3 (signalPrio's range, fuzzer.go:513-521) and
-// b->nrec records are assumed, the presence results (device, `presence`:
-// mask[8], total, bad) are checked on device before the scatter, and the run
-// commits nothing when they do not hold.  One host synchronisation.  *done =
-// false: take the planned path (*assumed_ok tells whether the assumptions held).
+// The whole batch as one aggregation run without a presence pass and its
+// host round trip: levels 0..3 (signalPrio's range, fuzzer.go:513-521) and at
+// most b->nrec records are assumed, checked on device before the scatter
+// (k_fast_prep, k_cell_plan_fast), and the run commits nothing when they do not
+// hold.  Zeroes b->call_new.  One host synchronisation; stats.records is set.
+// *done = false: take the planned path.
 int agg_triage_optimistic(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b,
-                          const void* presence, syzsig_batch_stats* st, uint64_t** pairs, uint64_t* npairs,
-                          bool* done);
+                          syzsig_batch_stats* st, uint64_t** pairs, uint64_t* npairs, bool* done);
 int agg_mark_bits(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const uint64_t* pairs,
                   uint64_t p0, uint64_t p1);
 int pairs_from_bits(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* bits, uint64_t c0, uint64_t c1,

@@ -609,6 +609,18 @@ static bool use_agg(const syzsig_ctx* ctx, uint64_t run_recs, uint64_t nrec_spac
 int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b,
                       syzsig_batch_stats* st)
 {
+	std::vector<Run> runs;
+	uint64_t total = 0;
+	uint64_t* pairs = nullptr;
+	uint64_t npairs = 0;
+	if (b->ncalls && b->nrec && b->ncalls <= kSerialMask && use_agg(ctx, b->nrec, b->nrec) && !b->new_bits) {
+		// a large batch: one aggregation run without the presence pass's round
+		// trip (levels 0..3 assumed and checked on device)
+		bool done = false;
+		SYZ_TRY(agg_triage_optimistic(ctx, ms, ns, b, st, &pairs, &npairs, &done));
+		if (done)
+			goto finish;
+	}
 	if (b->new_bits)
 		SYZ_HIP(hipMemsetAsync(b->new_bits, 0, ((b->nrec + 31) / 32) * 4, ctx->stream));
 	if (b->ncalls)
@@ -616,29 +628,6 @@ int triage_batch_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const sy
 	if (b->ncalls == 0 || b->nrec == 0) {
 		SYZ_HIP(hipStreamSynchronize(ctx->stream));
 		return SYZSIG_OK;
-	}
-	std::vector<Run> runs;
-	uint64_t total = 0;
-	uint64_t* pairs = nullptr;
-	uint64_t npairs = 0;
-	if (b->ncalls <= kSerialMask && use_agg(ctx, b->nrec, b->nrec) && !b->new_bits) {
-		// a large batch: one aggregation run that does not wait for the
-		// presence pass (levels 0..3 assumed and checked on device)
-		void* dmask;
-		SYZ_TRY(ws_get(ctx, 6, 64, &dmask));
-		SYZ_HIP(hipMemsetAsync(dmask, 0, 48, ctx->stream));
-		k_prio_presence<<<grid_for(b->ncalls, 256, 256), 256, 0, ctx->stream>>>(
-		    b->call_prio, b->call_len, b->call_start, b->ncalls, b->nrec, (uint32_t*)dmask,
-		    (unsigned long long*)((char*)dmask + 32), (unsigned long long*)((char*)dmask + 40));
-		SYZ_HIP(hipGetLastError());
-		uint32_t* hmask = (uint32_t*)(ctx->h_pin + kPinMask);
-		SYZ_HIP(hipMemcpyAsync(hmask, dmask, 48, hipMemcpyDeviceToHost, ctx->stream));
-		bool done = false;
-		SYZ_TRY(agg_triage_optimistic(ctx, ms, ns, b, dmask, st, &pairs, &npairs, &done));
-		if (done) {
-			memcpy(&st->records, &hmask[8], 8);  // (the run synchronised: the copy has landed)
-			goto finish;
-		}
 	}
 	SYZ_TRY(plan_runs(ctx, b, &runs, &total));
 	st->records = total;
