@@ -11,9 +11,10 @@
       exchange (shard_agg_partition -> owners' records-mode triage ->
       shard_agg_unpartition), against the same batch on the unsharded 1B table;
       plus the oracle on a program prefix (M0 restricted to the prefix's keys).
-  C5  streaming, skewed: two consecutive batches of 4096 programs x 64 x 1k
-      (skew=1, hot syscalls) triaged against the state the previous batch left,
-      against the oracle over both batches in order.
+  C5  streaming, skewed: two consecutive batches of 8192 programs x 64 x 1k
+      (one rank's share of 64k programs per batch on 8 GPUs; skew=1, hot
+      syscalls) triaged against the state the previous batch left, against the
+      oracle over both batches in order.
 
 References: syz-fuzzer/fuzzer.go:494-511 (checkNewSignal), pkg/signal/signal.go
 :73-166 (Diff/DiffRaw/Merge/Minimize).
@@ -228,7 +229,7 @@ def test_c5_streaming_skewed_vs_oracle(gpu):
     from syzkaller_amd import synth
 
     cfg = synth.synth_default(skew=1)
-    P, C, L = 4096, 64, 1024
+    P, C, L = 8192, 64, 1024  # one rank's share of C5's 64k programs per batch on 8 GPUs
     m0e, m0p = gpu.synth_m0(cfg, 1024, 10_000_000)
     ms = gpu.deserialize(m0e, m0p)
     ns = S.Signal(None, gpu.eng)
