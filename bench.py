@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PROBE_BYTES_PER_REC = 12.0  # 4 B element read + 8 B maxSignal slot read
 # the K3 pipeline of one step on one GPU (csrc/agg.hip); roofline.avg_launch_ms is
 # their summed device time (HIP events), roofline.traffic their summed PMC bytes
-K3_KERNELS = "k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg_fin+k_fin_deferred"
+K3_KERNELS = "k_fast_prep+k_cell_plan_fast+k_agg_scatter_blk+k_agg+k_agg_finalize_x+k_fin_deferred"
 EDGE_BYTES_PER_PC = 12.0  # K1+K2: 8 B u64 PC in + 4 B u32 signal out
 # Minimize's chain on its aggregation path (csrc/minimize.hip header); the
 # keys sort and k_min_calls are negligible (200k contexts)
@@ -44,7 +44,8 @@ MIN_KERNELS = ("k_min_prio_mask+k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_ag
                "+k_min_from_dist+k_count_u8")
 MIN_BYTES_PER_ENTRY, MIN_BYTES_PER_DISTINCT = 5.0, 4.0  # Minimize: (elem, prio) entry + covered[e]
 # N > 1: the source's aggregation, then the owner's records-mode triage of the staircases
-K3_DIST_KERNELS = "k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg+k_probe+k_decide"
+K3_DIST_KERNELS = ("k_prio_presence+k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg+k_stair_count+k_stair_scatter"
+                   "+k_recs_keys+k_recs_heads+k_recs_walk")
 
 
 def parse():
@@ -265,17 +266,18 @@ def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m
             sts = st
     wall, chain = float(np.median(walls)), float(np.median(chains))
     achieved = PROBE_BYTES_PER_REC * total / (chain * 1e-3) / 1e9
+    wl = (f"BASELINE config 5 at one rank's share of 8 GPUs: {nbatches} consecutive batches of {programs} programs "
+          f"x {calls} calls x {pcs} PCs, skew=1, each against the state the previous one left (M0 {m0})")
+    traffic, src = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], {"workload": wl}, ("workload",))
     return {"metric": "signal elems triaged/sec (Diff+Merge), streaming skewed batches",
             "value": total / wall, "unit": "elems/s", "higher_is_better": True,
             "ms_per_batch": wall * 1e3 / nbatches, "dtype": "u32",
-            "config": {"workload": f"BASELINE config 5 at one rank's share of 8 GPUs: {nbatches} consecutive "
-                                   f"batches of {programs} programs x {calls} calls x {pcs} PCs, skew=1, each against "
-                                   f"the state the previous one left (M0 {m0})",
+            "config": {"workload": wl,
                        "records": total, "batches": nbatches,
                        "retries": [x["retries"] for x in sts], "runs": [x["runs"] for x in sts],
                        "new_per_batch": [x["changed"] for x in sts], "distinct": [x["distinct"] for x in sts]},
             "roofline": {"bound": "hbm", "kernel": K3_KERNELS, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
                          "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": total // nbatches,
                          "avg_launch_ms": chain / nbatches}}
 
@@ -350,20 +352,21 @@ def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_
     step = s_ms + o_ms
     achieved = PROBE_BYTES_PER_REC * nrec0 / (step * 1e-3) / 1e9
     xbytes = 8 * (sum(sent) - sent[0])
+    wl = (f"BASELINE config 4, one rank of {world}: this rank's {P} x {C} x {L} batch (source aggregation + staircase "
+          f"routing), then owner 0's records-mode triage of what all {world} sources send it against its "
+          f"{shard_len}-element shard of a {m0_total}-element maxSignal")
+    traffic, src = pmc_traffic(["syz::" + k for k in K3_DIST_KERNELS.split("+")], {"workload": wl}, ("workload",))
     return {"metric": "signal elems triaged/sec (Diff+Merge) per rank of a 1B-element maxSignal over 8 GPUs",
             "value": nrec0 / (step * 1e-3), "unit": "elems/s", "higher_is_better": True, "dtype": "u32",
             "ms": step, "source_ms": s_ms, "owner_ms": o_ms,
-            "config": {"workload": f"BASELINE config 4, one rank of {world}: this rank's {P} x {C} x {L} batch "
-                                   f"(source aggregation + staircase routing), then owner 0's records-mode triage "
-                                   f"of what all {world} sources send it against its {shard_len}-element shard of a "
-                                   f"{m0_total}-element maxSignal",
+            "config": {"workload": wl,
                        "records": nrec0, "staircase_sent": sum(sent), "sent_per_owner": sent,
                        "owner_received": int(recv.numel()), "shard_elems": shard_len,
                        "xgmi_bytes_out": xbytes,
                        "xgmi_ms_at_7x153GBps": xbytes / (7 * 153e9) * 1e3,
                        "source_distinct": src_st.get("distinct"), "owner_changed": ost.get("changed")},
             "roofline": {"bound": "hbm", "kernel": K3_DIST_KERNELS, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
                          "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": nrec0, "avg_launch_ms": step}}
 
 

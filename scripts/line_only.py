@@ -1,0 +1,26 @@
+"""Run one of bench.py's extra lines alone (c5, c4, c1), for profiling: the
+line's JSON object on stdout."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from syzkaller_amd import synth  # noqa: E402
+from syzkaller_amd.device import Device  # noqa: E402
+
+which = sys.argv[1] if len(sys.argv) > 1 else "c5"
+dev = Device(0)
+dev.L.syzsig_ctx_set_timing(dev.eng.h, 1)
+pairs = torch.empty(4 * 2048 * 5939 + 64, dtype=torch.int64, device=dev.dev)
+if which == "c5":
+    out = bench.c5_line(dev, pairs)
+elif which == "c1":
+    out = bench.c1_line(dev)
+else:
+    P, C, L = 4096, 64, 4096
+    sigs, cs, cnt, prio, _, _ = bench.synth_batch(dev, synth.synth_default(), 0, P, C, L)
+    out = bench.c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L)
+print(json.dumps(out), flush=True)

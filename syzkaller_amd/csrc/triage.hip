@@ -813,6 +813,7 @@ static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** n
 	SYZ_TRY(counters_reset(ctx));
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
+	// (one thread per record position measured slower: 1.09 vs 0.44 ms for 7.3M records)
 	k_recs_walk<<<grid_for(n, 256, 8192), 256, 0, s>>>(keys2, order, n, lm, ms->slots, ms->nbuckets - 1, nsp->slots,
 	                                                   nsp->nbuckets - 1, new_flags, ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
