@@ -375,6 +375,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
 	const uint64_t ncalls = c1 - c0, nitems = (ncalls + (1ull << ib) - 1) >> ib;
 	const uint32_t per_t = (P + blockDim.x - 1) / blockDim.x;
+	bool badlv = false;
 	for (uint64_t ch = blockIdx.x; ch < nitems; ch += gridDim.x) {  // ch: work item (of 2^ibits calls)
 		const uint64_t cbeg = ch << ib;
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
@@ -441,8 +442,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 					const uint32_t h = fmix32(ev[u]), p = g.part(h);
 					const uint32_t r = atomicAdd(&hist[p], 1u);
 					uint32_t meta = c_meta[w + (loc[u] >> 24) * kWaves];
-					if (kEntry)
-						meta |= (uint32_t)s_lvl[(uint8_t)pv[kEntry ? u : 0]] << cb;
+					if (kEntry) {
+						const uint32_t lv = s_lvl[(uint8_t)pv[kEntry ? u : 0]];
+						badlv |= lv == 0xff;
+						meta |= (lv & 3) << cb;
+					}
 					ev[u] = g.rec(h, meta);
 					loc[u] = p | (r << 16);
 				} else {
@@ -490,6 +494,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 				break;
 		}
 	}
+	if (kEntry && x.bad_level && __ballot(badlv) && lane == 0)
+		atomicOr(x.bad_level, 1u);
 }
 
 // Capped cells written in whole 64-B blocks (the triage runs' scatter).
@@ -551,7 +557,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << ib) - 1) >> ib;  // work items
 	if (*cc.ovf)
 		return;  // the run is already void (an optimistic run's assumptions failed, or a cell spilled)
-	bool spilled = false;
+	bool spilled = false, badlv = false;
 	if (kEntry) {
 		for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
 			s_lvl[kEntry ? i : 0] = lm.lvl[i];
@@ -658,10 +664,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 				const uint32_t h = fmix32(ev[u]);
 				pt[u] = g.part(h);
 				uint32_t meta = c_meta[w + (loc[u] >> 24) * kWaves];
-				if (kEntry)
-					meta |= (uint32_t)s_lvl[pv[kEntry ? u : 0]] << cb;
-				rec[u] = g.rec(h, meta);
 				const bool keep = !kEntry || x.nshards == 1 || owner_of(ev[u], x.nshards) == x.shard;
+				if (kEntry) {
+					const uint32_t lv = s_lvl[pv[kEntry ? u : 0]];
+					badlv |= u * 64 + lane < n && keep && lv == 0xff;
+					meta |= (lv & 3) << cb;
+				}
+				rec[u] = g.rec(h, meta);
 				pend |= (uint32_t)(u * 64 + lane < n && keep) << u;
 			}
 			return dbg & 2 ? 0u : pend;  // dbg & 2: timing only, records loaded and dropped
@@ -731,6 +740,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 	}
 	if (spilled)
 		*cc.ovf = 1u;
+	if (kEntry && x.bad_level && __ballot(badlv) && lane == 0)
+		atomicOr(x.bad_level, 1u);
 }
 
 // Capped cells of a run: records per chunk -> cell capacity and chunk base.

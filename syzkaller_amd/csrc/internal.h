@@ -186,6 +186,7 @@ struct AggSrc {
 	const int8_t* elem_prio;  // per-record prio, parallel to sigs (level lm.lvl[prio]); nullptr = the call's
 	uint32_t nshards, shard;  // keep only the records whose element this shard owns (owner_of)
 	double distinct_hint;     // expected distinct elements (0: the batch-ratio policy)
+	unsigned int* bad_level = nullptr;  // if set: |= 1 when a record's prio has no level (lm.lvl[prio] == 0xff)
 };
 int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const LevelMap& lm,
                   uint64_t run_recs, syzsig_batch_stats* st, AggOut* out, const AggSrc* x = nullptr);

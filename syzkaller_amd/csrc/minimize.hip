@@ -293,37 +293,48 @@ using namespace syz;
 
 // The aggregation path (header).  *used = false: the atomic path must run
 // (more than 4 distinct prios, or a context of >= 2^24 entries).
-static int minimize_agg(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
-                        uint64_t nctx, uint64_t total, uint32_t nshards, uint32_t shard, uint64_t hint,
-                        const uint32_t* order, uint8_t* d_keep, bool* used)
+// exact: find the prios present first (one pass over them and a host round
+// trip); else assume signalPrio's 0..3 (fuzzer.go:513-521) and let the
+// scatter flag a prio outside them (*redo: nothing usable, call again exact).
+static int minimize_agg_run(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
+                            uint64_t nctx, uint64_t total, uint32_t nshards, uint32_t shard, uint64_t hint,
+                            const uint32_t* order, uint8_t* d_keep, bool exact, bool* used, bool* redo)
 {
 	*used = false;
+	*redo = false;
 	hipStream_t st = ctx->stream;
 	void* vb;
 	SYZ_TRY(ws_get(ctx, 34, nctx * 12 + 128, &vb));
-	uint32_t* dmask = (uint32_t*)vb;
+	uint32_t* dmask = (uint32_t*)vb;                               // [0, 32)
+	uint32_t* dflag = (uint32_t*)((char*)vb + 48);                 // a prio without a level (optimistic run)
+	unsigned long long* dbad = (unsigned long long*)((char*)vb + 56);  // contexts of >= 2^24 entries
 	uint64_t* cstart = (uint64_t*)((char*)vb + 64);
 	uint32_t* clen = (uint32_t*)(cstart + nctx);
-	SYZ_TRY(counters_reset(ctx));
-	SYZ_HIP(hipMemsetAsync(dmask, 0, 32, st));
-	k_min_calls<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, order, nctx, cstart, clen, &ctx->d_cnt[kCntAux]);
-	k_min_prio_mask<<<grid_for(total / 16 + 1, 256, 2048), 256, 0, st>>>((const uint8_t*)d_prios, total, dmask);
-	SYZ_HIP(hipGetLastError());
-	uint32_t* hmask = (uint32_t*)(ctx->h_pin + kPinMask);
-	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 32, hipMemcpyDeviceToHost, st));
-	SYZ_TRY(counters_fetch(ctx));  // synchronizes the stream
-	if (ctx->h_cnt[kCntAux])
-		return SYZSIG_OK;
-	int8_t levels[4];
-	uint32_t nl = 0;
-	for (int v = -128; v <= 127; v++) {
-		const uint8_t u = (uint8_t)(int8_t)v;
-		if ((hmask[u >> 5] >> (u & 31)) & 1) {
-			if (nl == 4)
-				return SYZSIG_OK;
-			levels[nl++] = (int8_t)v;
+	SYZ_HIP(hipMemsetAsync(vb, 0, 64, st));
+	k_min_calls<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, order, nctx, cstart, clen, dbad);
+	int8_t levels[4] = {0, 1, 2, 3};
+	uint32_t nl = 4;
+	if (exact) {
+		k_min_prio_mask<<<grid_for(total / 16 + 1, 256, 2048), 256, 0, st>>>((const uint8_t*)d_prios, total, dmask);
+		SYZ_HIP(hipGetLastError());
+		uint32_t* hmask = (uint32_t*)(ctx->h_pin + kPinMask);
+		SYZ_HIP(hipMemcpyAsync(hmask, vb, 64, hipMemcpyDeviceToHost, st));
+		SYZ_HIP(hipStreamSynchronize(st));
+		uint64_t nbad;
+		memcpy(&nbad, (char*)hmask + 56, 8);
+		if (nbad)
+			return SYZSIG_OK;
+		nl = 0;
+		for (int v = -128; v <= 127; v++) {
+			const uint8_t u = (uint8_t)(int8_t)v;
+			if ((hmask[u >> 5] >> (u & 31)) & 1) {
+				if (nl == 4)
+					return SYZSIG_OK;
+				levels[nl++] = (int8_t)v;
+			}
 		}
 	}
+	SYZ_HIP(hipGetLastError());
 	LevelMap lm;
 	SYZ_TRY(level_map_from_levels(levels, nl, &lm));
 	syzsig_batch b = {};
@@ -332,14 +343,42 @@ static int minimize_agg(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* 
 	b.call_len = clen;
 	b.ncalls = nctx;
 	b.nrec = total;
-	const AggSrc x{d_prios, nshards, shard, (double)(hint ? hint : total)};  // distinct <= entries
+	AggSrc x{d_prios, nshards, shard, (double)(hint ? hint : total)};  // distinct <= entries
+	if (!exact)
+		x.bad_level = dflag;
 	syzsig_batch_stats bst = {};
 	AggOut a;
 	SYZ_TRY(agg_aggregate(ctx, &b, 0, nctx, lm, total, &bst, &a, &x));
+	if (!exact) {  // (agg_aggregate synchronised: the flags are final)
+		uint32_t* hf = (uint32_t*)(ctx->h_pin + kPinMask);
+		SYZ_HIP(hipMemcpyAsync(hf, vb, 64, hipMemcpyDeviceToHost, st));
+		SYZ_HIP(hipStreamSynchronize(st));
+		uint64_t nbad;
+		memcpy(&nbad, (char*)hf + 56, 8);
+		if (nbad)
+			return SYZSIG_OK;  // a context too long for the serial: the atomic path
+		if (hf[12]) {
+			*redo = true;
+			return SYZSIG_OK;
+		}
+	}
 	SYZ_HIP(hipMemsetAsync(d_keep, 0, nctx, st));
 	k_min_from_dist<<<std::min<uint32_t>(a.nregions, 8192), 256, 0, st>>>(a.dist_f, a.cnt, a.nregions, order, d_keep);
 	SYZ_HIP(hipGetLastError());
 	*used = true;
+	return SYZSIG_OK;
+}
+
+static int minimize_agg(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* d_elems, const int8_t* d_prios,
+                        uint64_t nctx, uint64_t total, uint32_t nshards, uint32_t shard, uint64_t hint,
+                        const uint32_t* order, uint8_t* d_keep, bool* used)
+{
+	bool redo = false;
+	SYZ_TRY(minimize_agg_run(ctx, d_off, d_elems, d_prios, nctx, total, nshards, shard, hint, order, d_keep, false, used,
+	                         &redo));
+	if (redo)
+		SYZ_TRY(minimize_agg_run(ctx, d_off, d_elems, d_prios, nctx, total, nshards, shard, hint, order, d_keep, true,
+		                         used, &redo));
 	return SYZSIG_OK;
 }
 
