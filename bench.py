@@ -549,8 +549,17 @@ def main():
         lv = sharded.levels(prio)
         sharded.fixed_levels = sorted(set(lv) | set(SIGNAL_PRIO_LEVELS)) if len(set(lv) | set(SIGNAL_PRIO_LEVELS)) <= 4 else lv
 
+    def reset():
+        # back to M0: a copy of the whole table, or -- when that moves more bytes,
+        # as for a 1B/N-element shard -- only the slots of the elements the
+        # previous step changed (exactly newSignal's, cleared after each step)
+        if ms.capacity() * 16 <= ns.capacity() * 16 + ns.Len() * 256:
+            ms.copy_from(pristine)
+        else:
+            ms.restore_keys(pristine, ns)
+
     def step():
-        ms.copy_from(pristine)
+        reset()
         ns.clear()
         if distributed:
             st = dict(sharded.step((b, bits, cnew), prio, rank * P * C)[2])
@@ -577,6 +586,10 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     total_rec = nrec
+    reset()  # (outside the timed region: the reset brought back M0 exactly)
+    restore_ok = ms.equal(pristine)
+    if not restore_ok:
+        raise SystemExit("bench: maxSignal was not restored to M0 between steps")
     if distributed:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev.dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -634,6 +647,9 @@ def main():
                        "edge_pcs_per_s": npc / (np.median(edge_ms) * 1e-3),
                        "ingest_ms": ingest_ms, "ingest_check": ingest_ok},
             "triage": {k: v for k, v in s0.items() if k not in ("probe_ms", "decide_ms", "part_ms")},
+            "state_reset": "maxSignal back to M0 before every step: a table copy, or the slots of the previous "
+                           "step's newSignal elements (syzsig_set_restore_keys) when that moves fewer bytes; "
+                           "checked equal to M0 after the timed steps",
         }
     if rank == 0:
         traffic, src = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], out["config"])

@@ -95,6 +95,14 @@ int syzsig_set_clone(syzsig_ctx* ctx, const syzsig_set* s, syzsig_set** out);
 int syzsig_set_clear(syzsig_ctx* ctx, syzsig_set* s);
 /* Copy src's contents over dst (same capacity required); for snapshot/restore. */
 int syzsig_set_copy_from(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src);
+/* Restore dst to the snapshot src it was copied from, given `keys`: a set
+ * holding every element whose slot in dst changed since (the newSignal of the
+ * batches triaged since, when it was empty at the snapshot).  Only those slots
+ * are copied back, so the cost follows the changes, not the table.  Same
+ * capacity required (SYZSIG_EINVAL if dst grew).  Stream-ordered. */
+int syzsig_set_restore_keys(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src, const syzsig_set* keys);
+/* *equal = 1 iff a and b have the same capacity, length and slot words. */
+int syzsig_set_equal(syzsig_ctx* ctx, const syzsig_set* a, const syzsig_set* b, int* equal);
 /* Len / Empty, signal.go:23-29. */
 uint64_t syzsig_len(const syzsig_set* s);
 int syzsig_empty(const syzsig_set* s);

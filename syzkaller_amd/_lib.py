@@ -76,6 +76,8 @@ SIGNATURES = {
     "syzsig_set_clone": (c_int, [_P, _P, _PP]),
     "syzsig_set_clear": (c_int, [_P, _P]),
     "syzsig_set_copy_from": (c_int, [_P, _P, _P]),
+    "syzsig_set_restore_keys": (c_int, [_P, _P, _P, _P]),
+    "syzsig_set_equal": (c_int, [_P, _P, _P, ctypes.POINTER(c_int)]),
     "syzsig_len": (c_uint64, [_P]),
     "syzsig_empty": (c_int, [_P]),
     "syzsig_capacity": (c_uint64, [_P]),

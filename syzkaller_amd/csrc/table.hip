@@ -198,6 +198,41 @@ __global__ void k_merge_pairs(uint64_t* dst, uint64_t d_bmask, const uint64_t* _
 
 // Serialize (signal.go:42-57) in three passes: per-chunk live counts, an
 // exclusive scan of the (<= 2048) chunk counts, ordered per-chunk writes.
+// Snapshot restore by keys (syzsig_set_restore_keys): the slot of every key of
+// `keys` in dst, found before anything is written (a restored slot may go
+// empty and would cut the probe sequences of later lookups), then src's word
+// copied into each.
+__global__ void k_restore_find(const uint64_t* __restrict__ dst, uint64_t d_bmask, const uint64_t* __restrict__ keys,
+                               uint64_t k_nslots, int64_t* idx)
+{
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < k_nslots;
+	     i += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t w = keys[i];
+		uint64_t v = 0;
+		idx[i] = slot_live(w) ? tbl_lookup(dst, d_bmask, slot_key(w), v) : -1;
+	}
+}
+
+__global__ void k_restore_apply(uint64_t* dst, const uint64_t* __restrict__ src, const int64_t* __restrict__ idx,
+                                uint64_t k_nslots)
+{
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < k_nslots;
+	     i += (uint64_t)gridDim.x * blockDim.x) {
+		const int64_t j = idx[i];
+		if (j >= 0)
+			dst[j] = src[j];
+	}
+}
+
+__global__ void k_slots_differ(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, uint64_t n,
+                               unsigned long long* ndiff)
+{
+	uint64_t d = 0;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+		d += a[i] != b[i];
+	block_count(ndiff, d);
+}
+
 __global__ void k_count_live(const uint64_t* __restrict__ slots, uint64_t nslots, uint64_t chunk,
                              unsigned long long* counts)
 {
@@ -453,6 +488,43 @@ int syzsig_set_copy_from(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src
 	SYZ_HIP(hipMemcpyAsync(dst->slots, src->slots, src->nslots() * sizeof(uint64_t), hipMemcpyDeviceToDevice,
 	                       ctx->stream));
 	dst->len = src->len;
+	return SYZSIG_OK;
+}
+
+int syzsig_set_restore_keys(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src, const syzsig_set* keys)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !dst || !src)
+		return fail(SYZSIG_EINVAL, "set_restore_keys: NULL argument");
+	if (dst->nbuckets != src->nbuckets)
+		return fail(SYZSIG_EINVAL, "set_restore_keys: capacity mismatch (dst grew since the snapshot)");
+	if (keys && keys->len) {
+		void* ib;
+		SYZ_TRY(ws_get(ctx, 11, keys->nslots() * 8 + 64, &ib));
+		const int g = grid_for(keys->nslots(), 256, 8192);
+		k_restore_find<<<g, 256, 0, ctx->stream>>>(dst->slots, dst->nbuckets - 1, keys->slots, keys->nslots(),
+		                                           (int64_t*)ib);
+		k_restore_apply<<<g, 256, 0, ctx->stream>>>(dst->slots, src->slots, (const int64_t*)ib, keys->nslots());
+		SYZ_HIP(hipGetLastError());
+	}
+	dst->len = src->len;
+	return SYZSIG_OK;
+}
+
+int syzsig_set_equal(syzsig_ctx* ctx, const syzsig_set* a, const syzsig_set* b, int* equal)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !a || !b || !equal)
+		return fail(SYZSIG_EINVAL, "set_equal: NULL argument");
+	*equal = 0;
+	if (a->nbuckets != b->nbuckets || a->len != b->len)
+		return SYZSIG_OK;
+	SYZ_TRY(counters_reset(ctx));
+	k_slots_differ<<<grid_for(a->nslots(), 256, 8192), 256, 0, ctx->stream>>>(a->slots, b->slots, a->nslots(),
+	                                                                        &ctx->d_cnt[kCntAux]);
+	SYZ_HIP(hipGetLastError());
+	SYZ_TRY(counters_fetch(ctx));
+	*equal = ctx->h_cnt[kCntAux] == 0;
 	return SYZSIG_OK;
 }
 

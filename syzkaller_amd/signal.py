@@ -179,6 +179,18 @@ class Signal:
     def copy_from(self, src):
         check(self._e.L.syzsig_set_copy_from(self._e.h, self.handle, src.handle))
 
+    def restore_keys(self, src, keys):
+        """Back to the snapshot src this set was copied from, copying only the
+        slots of the elements in `keys` (every element changed since: the
+        newSignal of the batches since, if it was empty at the snapshot)."""
+        check(self._e.L.syzsig_set_restore_keys(self._e.h, self.handle, src.handle, keys.handle))
+
+    def equal(self, other):
+        """Same capacity, length and slot words (a snapshot check)."""
+        eq = ctypes.c_int(0)
+        check(self._e.L.syzsig_set_equal(self._e.h, self.handle, other.handle, ctypes.byref(eq)))
+        return bool(eq.value)
+
 
 class Cover:
     """type Cover map[uint32]struct{} (pkg/cover/cover.go:7), device-resident;

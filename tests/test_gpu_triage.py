@@ -453,3 +453,43 @@ def test_records_mode_vs_oracle(gpu, agg):
     assert ms.to_dict() == oms.to_dict()
     assert ns.to_dict() == ons.to_dict()
     assert (st["distinct"] > 0) == (agg == 1), st  # the sorted path counts distinct elements
+
+
+def test_restore_keys_brings_back_the_snapshot(gpu):
+    """syzsig_set_restore_keys: after a batch on the one-sync aggregation path
+    and one in records mode, copying back only newSignal's slots from the
+    snapshot gives the snapshot exactly (slot for slot); a table that grew
+    since is refused."""
+    from syzkaller_amd import _lib
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default()
+    nprog, cpp = 128, 32
+    cl = synth.call_lengths(nprog, cpp, 2048)
+    m0e, m0p = synth.m0(cfg, 2048, 1_000_000)
+    ms = S.Signal.make(16_000_000, gpu.eng)  # room for the batches' growth: no rehash after the snapshot
+    ms.Merge(S.Serial(m0e, m0p).Deserialize(gpu.eng))
+    snap = ms.clone()
+    ds, dcs, dcnt, dprio = dev_batch(gpu, cfg, nprog, cpp, cl)
+    ns = S.Signal.make(100_000, gpu.eng)
+    for _ in range(2):
+        gpu.triage(ms, ns, ds, dcs, dcnt, dprio, want_bits=False)
+        assert ns.Len() > 0 and not ms.equal(snap)
+        ms.restore_keys(snap, ns)
+        assert ms.equal(snap)
+        ns.clear()
+    # records mode (the owner side), >= 2^20 records: the sorted path
+    rng = np.random.default_rng(5)
+    e = rng.choice(np.unique(np.concatenate([m0e, rng.integers(0, 1 << 32, 600_000, dtype=np.uint64).astype(np.uint32)])),
+                   1_200_000)
+    rec = (e.astype(np.uint64) << np.uint64(32)) | (rng.integers(0, 4, e.size).astype(np.uint64) << np.uint64(24)) | \
+        rng.integers(0, 1 << 20, e.size).astype(np.uint64)
+    flags = torch.zeros(e.size, dtype=torch.uint8, device=gpu.dev)
+    gpu.triage_records(ms, ns, torch.from_numpy(rec.view(np.int64)).to(gpu.dev), [0, 1, 2, 3], flags)
+    assert ns.Len() > 0
+    ms.restore_keys(snap, ns)
+    assert ms.equal(snap)
+    big = S.Signal.make(100_000_000, gpu.eng)  # (a different capacity)
+    with pytest.raises(_lib.SyzsigError):
+        big.restore_keys(snap, ns)
