@@ -43,6 +43,7 @@
 //       from the exact distinct count, so nothing is ever retried.
 //   k_pairs_mark (optional) per-record new bits from the pairs.
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "internal.h"
@@ -51,7 +52,13 @@ namespace syz {
 
 constexpr uint32_t kAggThreads = 1024;
 constexpr uint32_t kAggSlots = 7424;               // LDS slots per workgroup (+ 8 KB of first-sight queues)
-constexpr uint32_t kAggBuckets = kAggSlots / 4;    // 4-key buckets (one ds_read_b128 per probe)
+// keys per LDS bucket: 4 (one ds_read_b128 per probe) or 2 (ds_read_b64)
+#ifndef SYZ_AGG_BW
+#define SYZ_AGG_BW 4
+#endif
+constexpr uint32_t kAggBW = SYZ_AGG_BW;
+using KBucket = std::conditional_t<kAggBW == 4, uint4, uint2>;
+constexpr uint32_t kAggBuckets = kAggSlots / kAggBW;
 constexpr uint32_t kAggNoSlot = 0xFFFFFFFFu;
 static_assert(kAggRegion == kAggSlots, "distinct-list region per partition (internal.h)");
 constexpr uint32_t kAggLimit = kAggSlots * 4 / 5;  // distinct elements before a partition overflows
@@ -130,11 +137,19 @@ __device__ __forceinline__ uint32_t bucket_find(uint4 B, uint32_t e)
 {
 	return B.x == e ? 0 : B.y == e ? 1 : B.z == e ? 2 : B.w == e ? 3 : 4;
 }
+__device__ __forceinline__ uint32_t bucket_find(uint2 B, uint32_t e)
+{
+	return B.x == e ? 0 : B.y == e ? 1 : kAggBW;
+}
 
 // position of the first empty key in a 4-key bucket, 4 if full
 __device__ __forceinline__ uint32_t bucket_first_empty(uint4 B)
 {
 	return B.x == kAggEmpty ? 0 : B.y == kAggEmpty ? 1 : B.z == kAggEmpty ? 2 : B.w == kAggEmpty ? 3 : 4;
+}
+__device__ __forceinline__ uint32_t bucket_first_empty(uint2 B)
+{
+	return B.x == kAggEmpty ? 0 : B.y == kAggEmpty ? 1 : kAggBW;
 }
 
 // Find-or-insert e in the LDS key buckets, bucket-linear from its home bucket
@@ -144,21 +159,21 @@ __device__ __forceinline__ uint32_t bucket_first_empty(uint4 B)
 // bucket only when another lane took that slot first.  Returns the slot
 // (ins incremented if this call inserted e), or kAggNoSlot if the probe sequence ran
 // through the whole table (the partition is then redone in HBM).
-__device__ uint32_t agg_find_insert(uint4* kb, uint32_t e, uint32_t b, uint4 B, uint32_t* s_ovf, uint32_t& ins)
+__device__ uint32_t agg_find_insert(KBucket* kb, uint32_t e, uint32_t b, KBucket B, uint32_t* s_ovf, uint32_t& ins)
 {
 	uint32_t* keys = reinterpret_cast<uint32_t*>(kb);
 	for (uint32_t step = 0; step < kAggBuckets;) {
 		const uint32_t f = bucket_find(B, e);
-		if (f < 4)
-			return b * 4 + f;
+		if (f < kAggBW)
+			return b * kAggBW + f;
 		const uint32_t j = bucket_first_empty(B);
-		if (j == 4) {
+		if (j == kAggBW) {
 			b = b + 1 == kAggBuckets ? 0 : b + 1;
 			B = kb[b];
 			step++;
 			continue;
 		}
-		const uint32_t i = b * 4 + j;
+		const uint32_t i = b * kAggBW + j;
 		const uint32_t key = atomicCAS(&keys[i], kAggEmpty, e);
 		if (key == kAggEmpty) {
 			ins++;
@@ -904,7 +919,7 @@ __global__ __launch_bounds__(1024) void k_cell_plan_fast(const uint64_t* __restr
 // home bucket (first sight, or a probe chain), gathered across batches and
 // resolved 64 at a time with every lane busy: (residual, level << 24 | serial).
 struct AggLds {
-	uint4 kb[kAggBuckets];
+	KBucket kb[kAggBuckets];
 	uint32_t fl[4][kAggSlots];
 	uint2 q[kAggThreads / 64][64];
 	uint32_t s_n, s_ovf, s_out, s_next;
@@ -930,7 +945,7 @@ struct AggCells {
 template <uint32_t U, uint32_t D, bool kCap>
 __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCells& x, const AggGeom& g)
 {
-	uint4* kb = L.kb;
+	KBucket* kb = L.kb;
 	auto& fl = L.fl;
 	const uint32_t* __restrict__ recs = x.recs;
 	const uint64_t* __restrict__ rec_base = x.rec_base;
@@ -962,8 +977,8 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 	};
 	const uint64_t ngroups = (nchunks + gsz - 1) / gsz;
 	for (uint32_t i = threadIdx.x; i < kAggSlots; i += blockDim.x) {
-		if (i < kAggBuckets)
-			kb[i] = make_uint4(kAggEmpty, kAggEmpty, kAggEmpty, kAggEmpty);
+		if (i < kAggSlots)
+			reinterpret_cast<uint32_t*>(kb)[i] = kAggEmpty;
 		fl[0][i] = fl[1][i] = fl[2][i] = fl[3][i] = kAggNone;
 	}
 	if (threadIdx.x == 0) {
@@ -1078,8 +1093,8 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 				lv[u] = g.level(r);
 				hb[u] = __umulhi(r & ~((1u << g.pbits) - 1), kAggBuckets);
 			}
-			// home buckets of all U records in flight together (ds_read_b128 each)
-			uint4 B[U];
+			// home buckets of all U records in flight together (ds_read_b128 / b64 each)
+			KBucket B[U];
 #pragma unroll
 			for (uint32_t u = 0; u < U; u++)
 				B[u] = kb[hb[u]];
@@ -1087,8 +1102,8 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 #pragma unroll
 			for (uint32_t u = 0; u < U; u++) {
 				const uint32_t f = bucket_find(B[u], key[u]);
-				slot[u] = f < 4 ? hb[u] * 4 + f : kAggNoSlot;
-				any_need |= f >= 4;
+				slot[u] = f < kAggBW ? hb[u] * kAggBW + f : kAggNoSlot;
+				any_need |= f >= kAggBW;
 			}
 			// first sight of an element, or a chain past its home bucket: to the
 			// wave's queue (the record's own level first is taken there)
