@@ -2588,7 +2588,9 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		// too few partitions (the distinct-ratio guess was low): nothing was
 		// committed; the next attempt sizes them for at least what was seen
 		// (an overflowed partition held more than kAggLimit)
-		const double seen = (double)D + 2.0 * (double)novf * kAggLimit;
+		// (most partitions overflowed: what they held is unknown, so size for the
+		// worst case, one distinct element per record)
+		const double seen = novf * 2 >= P ? (double)run_recs : (double)D + 2.0 * (double)novf * kAggLimit;
 		ctx->agg_distinct_ratio = std::max(ctx->agg_distinct_ratio, seen / (double)std::max<uint64_t>(run_recs, 1));
 		st->retries++;
 		if (fresh_ns) {

@@ -493,3 +493,33 @@ def test_restore_keys_brings_back_the_snapshot(gpu):
     big = S.Signal.make(100_000_000, gpu.eng)  # (a different capacity)
     with pytest.raises(_lib.SyzsigError):
         big.restore_keys(snap, ns)
+
+
+def test_one_sync_run_geometry_miss_redo(gpu):
+    """The one-sync run sizes its partitions from the distinct/records ratio of
+    the previous large batch.  After a batch of a few hot elements (ratio ~0),
+    a batch of all-distinct elements overflows most LDS partitions: the run
+    must commit nothing, redo itself once with partitions for what it counted,
+    and give the oracle's result."""
+    from syzkaller_amd import signal as S
+
+    rng = np.random.default_rng(9)
+    ncalls, per = 1024, 1100
+    hot = rng.integers(0, 1 << 32, 64, dtype=np.uint64).astype(np.uint32)
+    cs = (np.arange(ncalls, dtype=np.uint64) * per).astype(np.uint64)
+    cnt = np.full(ncalls, per, np.uint32)
+    prio = rng.integers(0, 4, ncalls).astype(np.uint8)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(gpu.dev)  # noqa: E731
+    for kind in ("hot", "distinct"):
+        if kind == "hot":
+            sigs = rng.choice(hot, ncalls * per)
+        else:
+            sigs = np.unique(rng.integers(0, 1 << 32, ncalls * per * 2, dtype=np.uint64).astype(np.uint32))
+            sigs = rng.permutation(sigs)[: ncalls * per]
+        m0e = np.unique(rng.integers(0, 1 << 32, 50_000, dtype=np.uint64).astype(np.uint32))
+        m0p = rng.integers(0, 4, m0e.size).astype(np.int8)
+        st = compare(gpu, (m0e, m0p), (sigs, cs, cnt, prio),
+                     (t(sigs, np.int32), t(cs, np.int64), t(cnt, np.int32), t(prio, np.uint8)), want_bits=False,
+                     reset=False)
+        if kind == "distinct":
+            assert st["retries"] >= 1 and st["overflow_parts"] == 0, st
