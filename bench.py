@@ -387,9 +387,11 @@ def c1_line(dev, reps=20):
     from syzkaller_amd import signal as S
 
     wall = []
+    ms = pristine.clone()
+    ns = S.Signal.make(1 << 20, dev.eng)  # newSignal grabbed before every batch (storage kept: syzsig_set_clear)
     for r in range(reps + 2):
-        ms = pristine.clone()
-        ns = S.Signal(None, dev.eng)
+        ms.copy_from(pristine)
+        ns.clear()
         torch.cuda.synchronize()
         t = time.perf_counter()
         dev.triage_b(ms, ns, b)

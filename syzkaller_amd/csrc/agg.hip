@@ -1732,21 +1732,12 @@ __global__ __launch_bounds__(256) void k_fin_deferred(const uint32_t* __restrict
 		ns_deferred(def_ns, def_ns_cnt, ns_slots, ns_bmask, ctr, gridDim.x - kDeferBlocks, blockIdx.x - kDeferBlocks);
 }
 
-// ---------------------------------------------------------------- fused
-// The fast path of a triage run: aggregation and finalize in one launch.  A
-// workgroup aggregates partition p in its LDS table (agg_partition), takes
-// the distinct elements into registers (slot t + k * 1024 of the table for
-// thread t), and then resolves them exactly as k_agg_finalize_x does --
-// maxSignal and newSignal slice p without device-scope atomics, claims in an
-// LDS set, pairs through an LDS buffer -- with the freed table as its LDS.  The
-// distinct lists never go to HBM, and the random slice probes of one
-// workgroup overlap the LDS-bound aggregation of the others.  Tables are
-// reserved for the run's largest possible distinct count before the launch,
-// so nothing here waits for the host.  A partition whose distinct elements
-// overflow the LDS table commits nothing (cnt[p] = kAggOverflow; the host
-// aggregates it in HBM afterwards: partitions hold disjoint elements, so
-// the order of commits does not matter); a spilled cell (*spill, set by the
-// scatter) makes every workgroup commit nothing and the run is redone.
+// ---------------------------------------------------------------- one-sync run
+// The arguments of the finalize of a one-sync triage run (agg_triage_fused).
+// (Round 3 measured aggregation and finalize in one launch -- the distinct
+// elements kept in registers, the freed LDS as claim set -- at 1.18 ms against
+// 0.64 + 0.27 for the two launches at C2, and removed it: one 1024-thread
+// workgroup per CU held the LDS through its random probes.)
 struct FinArgs {
 	LevelMap lm;
 	uint64_t c0;
@@ -1769,164 +1760,7 @@ struct FinArgs {
 	uint32_t dbg;
 };
 
-#ifndef SYZ_AF_ILP
-#define SYZ_AF_ILP 2
-#endif
-constexpr uint32_t kAfBuf = 8192;                                          // pair buffer (64 KB of the freed LDS)
-constexpr uint32_t kAfPer = (kAggSlots + kAggThreads - 1) / kAggThreads;  // table slots per thread
-constexpr uint32_t kAfIlp = SYZ_AF_ILP;                                    // elements resolved together
-static_assert(sizeof(AggLds) >= kFxSet * 4 + kAfBuf * 8, "the finalize reuses the aggregation LDS");
-static_assert(kAfPer % kAfIlp == 0, "finalize rounds");
-
-template <uint32_t U, uint32_t D>
-__global__ __launch_bounds__(kAggThreads) void k_agg_fin(AggCells x, AggGeom g, FinArgs fa, uint32_t* cnt)
-{
-	__shared__ AggLds L;
-	__shared__ uint32_t s_n;
-	__shared__ unsigned long long s_base;
-	uint32_t* claim = reinterpret_cast<uint32_t*>(&L);
-	uint64_t* buf = reinterpret_cast<uint64_t*>(claim + kFxSet);
-	const uint32_t* keys = reinterpret_cast<const uint32_t*>(L.kb);
-	const uint32_t P = 1u << g.pbits;
-	if (*fa.spill)
-		return;  // a cell overflowed: the run is redone with counted cells, nothing committed
-	uint32_t inserted = 0, changed = 0, ns_ins = 0, distinct = 0, novf = 0;  // (per thread: < 2^32)
-	auto flush = [&](uint32_t nb) {  // every thread; nb = s_n read after a barrier
-		nb = min(nb, kAfBuf);
-		if (threadIdx.x == 0)
-			s_base = atomicAdd(fa.npairs, (unsigned long long)nb);
-		__syncthreads();
-		for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x)
-			fa.pairs[s_base + t] = buf[t];
-		__syncthreads();
-		if (threadIdx.x == 0)
-			s_n = 0;
-		__syncthreads();
-	};
-	auto emit = [&](uint64_t v) {
-		const uint32_t k = atomicAdd(&s_n, 1u);
-		if (k < kAfBuf)
-			buf[k] = v;
-		else
-			fa.pairs[atomicAdd(fa.npairs, 1ull)] = v;
-	};
-	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
-		if (!agg_partition<U, D, true>(L, p, x, g)) {
-			if (threadIdx.x == 0) {
-				cnt[p] = kAggOverflow;
-				novf++;
-			}
-			__syncthreads();
-			continue;
-		}
-		// this thread's distinct elements into registers, elements restored from (p, residual)
-		const uint32_t hp = p << g.rbits();
-		uint32_t ge[kAfPer];
-		uint4 gf[kAfPer];
-		uint32_t valid = 0;
-#pragma unroll
-		for (uint32_t k = 0; k < kAfPer; k++) {
-			const uint32_t i = threadIdx.x + k * kAggThreads;
-			const uint32_t key = i < kAggSlots ? keys[i] : kAggEmpty;
-			valid |= (uint32_t)(key != kAggEmpty) << k;
-			ge[k] = fmix32_inv(hp | key);
-			gf[k] = i < kAggSlots ? make_uint4(L.fl[0][i], L.fl[1][i], L.fl[2][i], L.fl[3][i])
-			                      : make_uint4(kAggNone, kAggNone, kAggNone, kAggNone);
-		}
-		distinct += __popc(valid);
-		if (threadIdx.x == 0)
-			cnt[p] = (uint32_t)L.s_n;  // (the table's insert count: the partition's distinct elements)
-		__syncthreads();  // the table is read: its LDS is the claim set and the pair buffer now
-		for (uint32_t i = threadIdx.x; i < kFxSet; i += blockDim.x)
-			claim[i] = 0;
-		if (threadIdx.x == 0)
-			s_n = 0;
-		__syncthreads();
-		const uint64_t ms0 = (uint64_t)p << fa.ms_shift, ms1 = (uint64_t)(p + 1) << fa.ms_shift;
-		const uint64_t ns0 = (uint64_t)p << fa.ns_shift, ns1 = (uint64_t)(p + 1) << fa.ns_shift;
-#pragma unroll
-		for (uint32_t k0 = 0; k0 < kAfPer; k0 += kAfIlp) {
-			int top[kAfIlp];
-			Bucket bm[kAfIlp], bn[kAfIlp];
-#pragma unroll
-			for (uint32_t j = 0; j < kAfIlp; j++) {
-				const uint32_t k = k0 + j;
-				const uint32_t f[4] = {gf[k].x, gf[k].y, gf[k].z, gf[k].w};
-				top[j] = -1;
-#pragma unroll
-				for (int l = 0; l < 4; l++)
-					if (((valid >> k) & 1) && l < (int)fa.lm.n && f[l] != kAggNone)
-						top[j] = l;
-				if (top[j] >= 0) {
-					bm[j] = load_bucket(fa.slots + (home_bucket(ge[k], fa.bmask) << kBucketShift));
-					bn[j] = load_bucket(fa.ns_slots + (home_bucket(ge[k], fa.ns_bmask) << kBucketShift));
-				}
-			}
-#pragma unroll
-			for (uint32_t j = 0; j < kAfIlp; j++) {
-				if (top[j] < 0)
-					continue;
-				const uint32_t k = k0 + j, e = ge[k];
-				const uint32_t f[4] = {gf[k].x, gf[k].y, gf[k].z, gf[k].w};
-				const int8_t Pv = fa.lm.val[top[j]];
-				const uint64_t word = make_slot(e, Pv);
-				uint64_t old = 0;
-				// (dbg & 32, tests: defer every walk that leaves the home bucket)
-				const uint64_t hm = home_bucket(e, fa.bmask), hn = home_bucket(e, fa.ns_bmask);
-				const int64_t idx = fx_walk(fa.slots, hm, fa.dbg & 32 ? hm + 1 : ms1, ms0 << kBucketShift, e, bm[j],
-				                            claim, 0, old);
-				if (idx < 0) {  // the atomic path takes the whole element
-					const uint64_t d = atomicAdd(fa.def_cnt, 1ull);
-					fa.def_e[d] = e;
-					fa.def_f[d] = gf[k];
-					continue;
-				}
-				const bool present = slot_live(old);
-				const int p0 = present ? (int)slot_prio(old) : -1000;
-				if ((int)Pv <= p0)
-					continue;  // (a claimed slot always has Pv > p0)
-				fa.slots[idx] = word;  // the block's own slice: no other writer
-				inserted += !present;
-				changed++;
-				uint64_t nold = 0;
-				const int64_t nidx = fx_walk(fa.ns_slots, hn, fa.dbg & 32 ? hn + 1 : ns1, ns0 << kBucketShift, e,
-				                             bn[j], claim, 1, nold);
-				if (nidx < 0) {
-					fa.def_ns[atomicAdd(fa.def_ns_cnt, 1ull)] = ((uint64_t)e << 32) | prio_biased(Pv);
-				} else if (nold == 0 || nold < word) {
-					fa.ns_slots[nidx] = word;
-					ns_ins += nold == 0;
-				}
-				// the staircase: first records of strictly rising level above M0[e]
-				uint32_t mk = kAggNone;
-#pragma unroll
-				for (int l = 3; l >= 0; l--) {
-					if (l > top[j] || f[l] == kAggNone)
-						continue;
-					if ((int)fa.lm.val[l] <= p0)
-						break;
-					if (f[l] < mk) {
-						mk = f[l];
-						const uint64_t c = fa.c0 + f[l];
-						fa.call_new[c] = 1;
-						emit((c << 32) | e);
-					}
-				}
-			}
-			__syncthreads();
-			const uint32_t nb = s_n;
-			if (nb > (k0 + kAfIlp < kAfPer ? kAfBuf / 2 : 0))
-				flush(nb);
-		}
-	}
-	block_count(&fa.ctr[kCntInserted], inserted);
-	block_count(&fa.ctr[kCntChanged], changed);
-	block_count(&fa.ctr[kCntAux], ns_ins);
-	block_count(&fa.ctr[kCntDistinct], distinct);
-	block_count(&fa.ctr[kCntAggOvf], novf);
-}
-
-// Fallback of the fused path: the records of the partitions that overflowed
+// Fallback of the one-sync run: the records of the partitions that overflowed
 // the LDS table, aggregated in one HBM table keyed by h (as k_agg_global) from
 // their capped cells.  One wave per (partition, chunk).
 __global__ __launch_bounds__(256) void k_agg_global_cap(const uint32_t* __restrict__ recs,
@@ -2390,14 +2224,16 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	return SYZSIG_OK;
 }
 
-// The fused fast path of one triage run (k_agg_fin): scatter into capped
-// cells, then aggregation + finalize in one launch, with one host
-// synchronisation at the end.  maxSignal and newSignal are reserved for the
-// run's largest possible distinct count D_max = min(records, P * kAggLimit)
+// One triage run with one host synchronisation at the end ("the
+// one-sync triage run"): scatter into capped cells, k_agg, the slice-exclusive
+// finalize and the deferred lists.  maxSignal and newSignal are reserved for
+// the run's largest possible distinct count D_max = min(records, P * kAggLimit)
 // (a growth only when len + D_max would pass 90 % of the table; the usual
 // policy loads apply to the expected count), so the kernels never wait for
-// the host.  *done = false: nothing was committed and the caller takes the
-// counted-cell path (a cell spilled; the slack is doubled for the next run).
+// the host.  fast: the caller skipped the presence pass (k_fast_prep checks its
+// assumptions).  *done = false: nothing was committed (*assumed_bad: the
+// assumptions failed; *regeom: too few partitions, redo; else a cell spilled:
+// counted cells next, the slack doubled).
 static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsig_batch* b, uint64_t c0,
                             uint64_t c1, const LevelMap& lm, uint64_t run_recs, syzsig_batch_stats* st,
                             uint64_t** pairs_out, uint64_t* npairs_io, bool* done, bool fast = false,
@@ -2414,7 +2250,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	g.ibits = g.cbits();  // work items are whole chunks
 	const uint32_t S = 1u << g.pbits, P = S;
 	const uint64_t nchunks = (c1 - c0 + (1ull << g.ibits) - 1) >> g.ibits;
-	// distinct elements the fused kernel can commit: an LDS partition holds at
+	// distinct elements the run can commit: an LDS partition holds at
 	// most kAggLimit (one that overflows is committed after the sync)
 	const uint64_t d_max = std::min<uint64_t>(run_recs, (uint64_t)P * kAggLimit);
 	const double ratio = ctx->agg_distinct_ratio > 0 ? ctx->agg_distinct_ratio : 1.0 / 32;
@@ -2509,20 +2345,14 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	fa.spill = ovf;
 	fa.dbg = ctx->agg_dbg;
 	const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),
-	                  ovf, ctx->agg_variant == 7 ? nullptr : ctx->d_cnt};
+	                  ovf, ctx->d_cnt};
 	// more overflowed partitions than this and the split path commits nothing:
 	// the run is redone with partitions sized from what k_agg counted
 	const uint32_t gate = P / 8;
-	if (ctx->agg_variant == 7) {  // aggregation and finalize in one launch
-		k_agg_fin<kAggU, kAggD><<<P, kAggThreads, 0, s>>>(xc, g, fa, (uint32_t*)dc);
-		SYZ_HIP(hipGetLastError());
-		if (ctx->timing)
-			SYZ_HIP(hipEventRecord(ctx->ev[2], s));
-	} else {
+	{
 		// k_agg's distinct lists through HBM (5 M x 20 B at C2), then the
 		// slice-exclusive finalize: a workgroup of the finalize is small, so
-		// many run per CU and their random probes overlap (the one-launch form
-		// holds a CU's LDS through its probes)
+		// many run per CU and their random probes overlap
 		void *de, *df;
 		SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 		SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));

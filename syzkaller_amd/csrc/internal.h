@@ -55,8 +55,8 @@ enum Counter : int {
 	kCntAux2,
 	kCntDefer,          // triage finalize: elements deferred to the atomic path
 	kCntDeferNs,        // triage finalize: newSignal merges deferred to the atomic path
-	kCntDistinct,       // fused triage: distinct elements aggregated
-	kCntAggOvf,         // fused triage: partitions that overflowed the LDS table
+	kCntDistinct,       // one-sync triage run / records mode: distinct elements
+	kCntAggOvf,         // one-sync triage run: partitions that overflowed the LDS table
 	kCntSpill,          // one-sync triage run: its void flag (low 32 bits; 1 = a cell spilled, 2 = assumptions)
 	kCntRecords,        // one-sync triage run: the batch's records
 	kNumCounters = 16,
@@ -94,7 +94,7 @@ struct syzsig_ctx {
 	// pinned staging for the small per-batch copies (a pageable copy is staged
 	// and synchronous): syz::kPin* offsets
 	char* h_pin = nullptr;
-	// grow-only scratch buffers by role (35: the fused triage fallback): 0-2 set ops, 3-6 triage candidates and
+	// grow-only scratch buffers by role (35: the one-sync run's fallback): 0-2 set ops, 3-6 triage candidates and
 	// small state, 7-10 host uploads of minimize, 11-14 triage partitions and
 	// minimize internals and triage pairs (13-15), 16-23 + 30-31 triage aggregation,
 	// 24-29 check_new_signal uploads, 32-33 the finalize's deferred lists, 40-47 manager poll
@@ -106,7 +106,7 @@ struct syzsig_ctx {
 	double agg_distinct_ratio = 0;        // distinct/records of the last aggregated run (sizes the next)
 	float cap_sd = syz::kCapSdDefault;    // capped-cell slack in standard deviations (agg.hip; 0 = counted cells)
 	float cap_sd_entry = syz::kCapSdDefault;  // the same for Minimize's runs
-	bool agg_counted_once = false;        // the next agg_aggregate takes counted cells (a fused run spilled)
+	bool agg_counted_once = false;        // the next agg_aggregate takes counted cells (a one-sync run spilled)
 	uint32_t edge_waves = 4;              // waves per program of k_edge_dedup (4 or 8; SYZSIG_EDGE_WAVES)
 	uint32_t agg_variant = 0;             // k_agg pipeline variant (SYZSIG_AGG_VARIANT; tuning)
 	uint32_t agg_dbg = 0;                 // SYZSIG_DEBUG_* path flags; timing-only bits need -DSYZ_EXPERIMENTS
