@@ -387,10 +387,9 @@ def c1_line(dev, reps=20):
     from syzkaller_amd import signal as S
 
     wall = []
-    ms = pristine.clone()
     ns = S.Signal.make(1 << 20, dev.eng)  # newSignal grabbed before every batch (storage kept: syzsig_set_clear)
     for r in range(reps + 2):
-        ms.copy_from(pristine)
+        ms = pristine.clone()  # (the batch grows maxSignal's table: a fresh copy of M0 each time)
         ns.clear()
         torch.cuda.synchronize()
         t = time.perf_counter()
