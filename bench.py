@@ -553,8 +553,14 @@ def main():
     def reset():
         # back to M0: a copy of the whole table, or -- when that moves more bytes,
         # as for a 1B/N-element shard -- only the slots of the elements the
-        # previous step changed (exactly newSignal's, cleared after each step)
-        if ms.capacity() * 16 <= ns.capacity() * 16 + ns.Len() * 256:
+        # previous step changed (exactly newSignal's, cleared after each step);
+        # a table that grew in the step is replaced by a fresh copy of M0
+        nonlocal ms
+        if ms.capacity() != pristine.capacity():
+            ms = pristine.clone()
+            if distributed:
+                sharded.shard = ms
+        elif ms.capacity() * 16 <= ns.capacity() * 16 + ns.Len() * 256:
             ms.copy_from(pristine)
         else:
             ms.restore_keys(pristine, ns)
