@@ -771,6 +771,90 @@ __global__ void k_recs_walk(const uint64_t* __restrict__ sk, const uint32_t* __r
 	block_count(&ctr[kCntDistinct], distinct);
 }
 
+// SYZSIG_DEBUG_RECS_WAVE: one wave per 64 consecutive sorted positions.  Every
+// lane loads its record, the run heads probe the shard in parallel, and a head
+// walks its run through the wave's registers (uniform shuffles); a run that
+// leaves the wave continues with loads.  Same results as k_recs_walk.
+__global__ __launch_bounds__(256) void k_recs_walk_wave(const uint64_t* __restrict__ sk,
+                                                        const uint32_t* __restrict__ order, uint64_t n, LevelMap lm,
+                                                        uint64_t* ms, uint64_t ms_bmask, uint64_t* ns,
+                                                        uint64_t ns_bmask, uint8_t* flags, unsigned long long* ctr)
+{
+	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0, distinct = 0;
+	constexpr uint64_t kElemSerial = (1ull << 56) - 1;
+	const uint32_t lane = lane_id();
+	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	for (uint64_t base = (blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < n;
+	     base += nwaves * 64) {
+		const uint64_t i = base + lane;
+		const bool valid = i < n;
+		const uint64_t ki = valid ? sk[i] : 0;
+		const uint32_t oi = valid ? order[i] : 0;
+		const uint32_t e = (uint32_t)((ki & kElemSerial) >> 24);
+		uint64_t kprev = __shfl_up(ki, 1, 64);
+		if (lane == 0)
+			kprev = base > 0 ? sk[base - 1] : 0;
+		const bool head = valid && (i == 0 || (uint32_t)((kprev & kElemSerial) >> 24) != e);
+		bool present = false;
+		int m0 = -1000;  // absent: below every prio (signal.go:93-95)
+		if (head) {
+			uint64_t v = 0;
+			present = tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v);
+			m0 = present ? (int)slot_prio(v) : -1000;
+			distinct++;
+		}
+		int m = m0;
+		uint32_t last_new = 0xFFFFFFFFu;
+		auto take = [&](uint64_t kj, uint32_t oj) {
+			const uint32_t k = (uint32_t)kj & kSerialMask;
+			const int p = lm.val[(kj >> 56) & 3];
+			if (p > m || k == last_new) {
+				flags[oj] = 1;
+				m = max(m, p);
+				last_new = k;
+			}
+		};
+		bool walking = head, beyond = false;
+		for (uint32_t t = 0; __ballot(walking); t++) {
+			const uint32_t src = (lane + t) & 63;
+			const uint64_t kj = __shfl(ki, src, 64);
+			const uint32_t oj = __shfl(oi, src, 64);
+			const int vj = __shfl((int)valid, src, 64);
+			if (walking) {
+				if (lane + t >= 64) {  // the run goes on past this wave's positions
+					walking = false;
+					beyond = true;
+				} else if (!vj || (uint32_t)((kj & kElemSerial) >> 24) != e) {
+					walking = false;
+				} else {
+					take(kj, oj);
+				}
+			}
+		}
+		if (beyond) {
+			for (uint64_t j = base + 64; j < n; j++) {
+				const uint64_t kj = sk[j];
+				if ((uint32_t)((kj & kElemSerial) >> 24) != e)
+					break;
+				take(kj, order[j]);
+			}
+		}
+		if (head && m > m0) {  // maxSignal.Merge / newSignal.Merge of the element's final prio
+			changed++;
+			inserted += !present;
+			ovf += tbl_merge(ms, ms_bmask, e, (int8_t)m) < 0;
+			const int r = tbl_merge(ns, ns_bmask, e, (int8_t)m);
+			ns_ins += r == 1;
+			ovf += r < 0;
+		}
+	}
+	block_count(&ctr[kCntInserted], inserted);
+	block_count(&ctr[kCntChanged], changed);
+	block_count(&ctr[kCntAux], ns_ins);
+	block_count(&ctr[kCntOverflow], ovf);
+	block_count(&ctr[kCntDistinct], distinct);
+}
+
 __global__ void k_recs_heads(const uint64_t* __restrict__ sk, uint64_t n, unsigned long long* heads)
 {
 	constexpr uint64_t kElem = ((1ull << 56) - 1) & ~(uint64_t)kSerialMask;
@@ -814,8 +898,9 @@ static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** n
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
 	// (one thread per record position measured slower: 1.09 vs 0.44 ms for 7.3M records)
-	k_recs_walk<<<grid_for(n, 256, 8192), 256, 0, s>>>(keys2, order, n, lm, ms->slots, ms->nbuckets - 1, nsp->slots,
-	                                                   nsp->nbuckets - 1, new_flags, ctx->d_cnt);
+	auto walk = (ctx->agg_dbg & SYZSIG_DEBUG_RECS_WAVE) ? k_recs_walk_wave : k_recs_walk;
+	walk<<<grid_for(n, 256, 8192), 256, 0, s>>>(keys2, order, n, lm, ms->slots, ms->nbuckets - 1, nsp->slots,
+	                                            nsp->nbuckets - 1, new_flags, ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[3], s));

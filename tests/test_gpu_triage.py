@@ -408,20 +408,24 @@ def test_triage_c2_properties(gpu):
     assert int(cnew3.sum()) == 0 and int(bits3.count_nonzero()) == 0 and ns3.is_nil() and ms.Len() == n_before
 
 
-@pytest.mark.parametrize("agg", [1, 0])
-def test_records_mode_vs_oracle(gpu, agg):
+@pytest.mark.parametrize("agg,npool", [(1, 2_500_000), (0, 2_500_000), ("wave", 2_500_000), (1, 20_000),
+                                       ("wave", 20_000)])
+def test_records_mode_vs_oracle(gpu, agg, npool):
     """Records mode (the owner side of a sharded step, triage.hip
     triage_records_impl): ~1.2M records (e, level, serial) in a shuffled order,
     each serial one call of up to 6 distinct elements at one level, against a
-    1M-element shard.  agg=1 takes the sorted path (records sorted by
-    (element, serial), one thread per element), agg=0 the per-record probe path; both
-    must flag exactly the records the oracle's sequential checkNewSignal over
-    the calls in serial order marks new, and leave the same shard and
-    newSignal."""
+    shard holding part of the pool.  agg=1 takes the sorted path (records
+    sorted by (element, serial), one thread per element run; "wave": the same
+    with SYZSIG_DEBUG_RECS_WAVE, one wave per 64 sorted positions), agg=0 the
+    per-record probe path.  npool=20k gives ~60 records per element, so runs
+    cross the wave walk's 64-position windows.  All must flag exactly the
+    records the oracle's sequential checkNewSignal over the calls in serial
+    order marks new, and leave the same shard and newSignal."""
     from syzkaller_amd import signal as S
 
     rng = np.random.default_rng(77)
-    pool = np.unique(rng.integers(0, 1 << 32, 2_500_000, dtype=np.uint64).astype(np.uint32))
+    pool = np.unique(rng.integers(0, 1 << 32, npool, dtype=np.uint64).astype(np.uint32))
+    assert all((7919 * k) % pool.size for k in range(1, 7))  # a call's elements are distinct
     ncall = 300_000
     clen = rng.integers(1, 7, ncall).astype(np.uint32)
     nrec = int(clen.sum())
@@ -442,17 +446,21 @@ def test_records_mode_vs_oracle(gpu, agg):
     ns = S.Signal(None, gpu.eng)
     drec = torch.from_numpy(rec[perm].view(np.int64)).to(gpu.dev)
     flags = torch.zeros(nrec, dtype=torch.uint8, device=gpu.dev)
-    gpu.eng.set_agg(agg, 0)
+    from syzkaller_amd._lib import SYZSIG_DEBUG_RECS_WAVE
+
+    gpu.eng.set_agg(0 if agg == 0 else 1, 0)
+    gpu.eng.set_debug(SYZSIG_DEBUG_RECS_WAVE if agg == "wave" else 0)
     try:
         st = gpu.triage_records(ms, ns, drec, [0, 1, 2, 3], flags)
     finally:
         gpu.eng.set_agg(1, 0)
+        gpu.eng.set_debug(0)
     oms, ons, obits, _ = O.triage_batch(m0e, m0p, sigs, cs, clen, lvl)
     onew = np.unpackbits(obits.view(np.uint8), bitorder="little")[:nrec].astype(np.uint8)
     np.testing.assert_array_equal(_u(flags, np.uint8), onew[perm])
     assert ms.to_dict() == oms.to_dict()
     assert ns.to_dict() == ons.to_dict()
-    assert (st["distinct"] > 0) == (agg == 1), st  # the sorted path counts distinct elements
+    assert (st["distinct"] > 0) == (agg != 0), st  # the sorted path counts distinct elements
 
 
 def test_restore_keys_brings_back_the_snapshot(gpu):
