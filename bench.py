@@ -75,7 +75,6 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming line")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 per-rank line")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 line")
-    ap.add_argument("--lines-only", action="store_true", help="(experiments) only the extra lines, tiny headline")
     return ap.parse_args()
 
 
