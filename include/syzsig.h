@@ -77,14 +77,14 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
  * cells (count pass + scan) instead of capped cells;
  * SYZSIG_DEBUG_CAP_SPILL = capped cells of 64 records, so that dense runs
  * overflow them and take the redo with counted cells;
- * SYZSIG_DEBUG_RECS_WAVE = records mode's sorted walk runs one wave per 64
- * sorted positions (runs walked through shuffles) instead of one thread per
- * element run. */
+ * SYZSIG_DEBUG_RECS_SCAN = records mode's sorted walk runs one thread per
+ * sorted position (the run heads among them walk their runs) instead of one
+ * thread per compacted run head. */
 #define SYZSIG_DEBUG_FIN_DEFER 32u
 #define SYZSIG_DEBUG_MIN_ATOMIC 64u
 #define SYZSIG_DEBUG_EXACT_CELLS 128u
 #define SYZSIG_DEBUG_CAP_SPILL 256u
-#define SYZSIG_DEBUG_RECS_WAVE 512u
+#define SYZSIG_DEBUG_RECS_SCAN 512u
 int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
 
 /* ---- pkg/signal/signal.go ---- */

@@ -726,9 +726,74 @@ __global__ void k_recs_keys(const uint64_t* __restrict__ recs, uint64_t n, uint3
 	block_count(bad, nbad);
 }
 
-__global__ void k_recs_walk(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ order, uint64_t n,
-                            LevelMap lm, uint64_t* ms, uint64_t ms_bmask, uint64_t* ns, uint64_t ns_bmask,
-                            uint8_t* flags, unsigned long long* ctr)
+// The replay of one element run from its head i: checkNewSignal's rule over
+// the run's records in serial order, from M0[e]; then the element's final prio
+// merged into the shard and newSignal.
+struct RecsWalk {
+	const uint64_t* __restrict__ sk;
+	const uint32_t* __restrict__ order;
+	uint64_t n;
+	LevelMap lm;
+	uint64_t *ms, ms_bmask, *ns, ns_bmask;
+	uint8_t* flags;
+	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0, distinct = 0;
+	static constexpr uint64_t kElemSerial = (1ull << 56) - 1;
+
+	__device__ void run(uint64_t i)
+	{
+		const uint32_t e = (uint32_t)((sk[i] & kElemSerial) >> 24);
+		distinct++;
+		uint64_t v = 0;
+		const bool present = tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v);
+		const int m0 = present ? (int)slot_prio(v) : -1000;  // absent: below every prio (signal.go:93-95)
+		int m = m0;
+		uint32_t last_new = 0xFFFFFFFFu;
+		for (uint64_t j = i; j < n; j++) {
+			const uint64_t kj = sk[j];
+			if ((uint32_t)((kj & kElemSerial) >> 24) != e)
+				break;
+			const uint32_t k = (uint32_t)kj & kSerialMask;
+			const int p = lm.val[(kj >> 56) & 3];
+			if (p > m || k == last_new) {
+				flags[order[j]] = 1;
+				m = max(m, p);
+				last_new = k;
+			}
+		}
+		if (m > m0) {  // maxSignal.Merge / newSignal.Merge of the element's final prio
+			changed++;
+			inserted += !present;
+			ovf += tbl_merge(ms, ms_bmask, e, (int8_t)m) < 0;
+			const int r = tbl_merge(ns, ns_bmask, e, (int8_t)m);
+			ns_ins += r == 1;
+			ovf += r < 0;
+		}
+	}
+	__device__ void count(unsigned long long* ctr)
+	{
+		block_count(&ctr[kCntInserted], inserted);
+		block_count(&ctr[kCntChanged], changed);
+		block_count(&ctr[kCntAux], ns_ins);
+		block_count(&ctr[kCntOverflow], ovf);
+		block_count(&ctr[kCntDistinct], distinct);
+	}
+};
+
+// One thread per element run, over the heads k_recs_heads compacted: every
+// lane of a wave holds a run, so 64 shard probes and merges are in flight per
+// wave.
+__global__ void k_recs_walk(const uint32_t* __restrict__ heads, uint64_t nh, RecsWalk rw, unsigned long long* ctr)
+{
+	for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nh; t += (uint64_t)gridDim.x * blockDim.x)
+		rw.run(heads[t]);
+	rw.count(ctr);
+}
+
+// SYZSIG_DEBUG_RECS_SCAN: one thread per sorted position, the heads among them
+// walking their runs (a wave waits for its slowest head each step).
+__global__ void k_recs_walk_scan(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ order, uint64_t n,
+                                 LevelMap lm, uint64_t* ms, uint64_t ms_bmask, uint64_t* ns, uint64_t ns_bmask,
+                                 uint8_t* flags, unsigned long long* ctr)
 {
 	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0, distinct = 0;
 	constexpr uint64_t kElemSerial = (1ull << 56) - 1;
@@ -771,97 +836,36 @@ __global__ void k_recs_walk(const uint64_t* __restrict__ sk, const uint32_t* __r
 	block_count(&ctr[kCntDistinct], distinct);
 }
 
-// SYZSIG_DEBUG_RECS_WAVE: one wave per 64 consecutive sorted positions.  Every
-// lane loads its record, the run heads probe the shard in parallel, and a head
-// walks its run through the wave's registers (uniform shuffles); a run that
-// leaves the wave continues with loads.  Same results as k_recs_walk.
-__global__ __launch_bounds__(256) void k_recs_walk_wave(const uint64_t* __restrict__ sk,
-                                                        const uint32_t* __restrict__ order, uint64_t n, LevelMap lm,
-                                                        uint64_t* ms, uint64_t ms_bmask, uint64_t* ns,
-                                                        uint64_t ns_bmask, uint8_t* flags, unsigned long long* ctr)
-{
-	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0, distinct = 0;
-	constexpr uint64_t kElemSerial = (1ull << 56) - 1;
-	const uint32_t lane = lane_id();
-	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-	for (uint64_t base = (blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < n;
-	     base += nwaves * 64) {
-		const uint64_t i = base + lane;
-		const bool valid = i < n;
-		const uint64_t ki = valid ? sk[i] : 0;
-		const uint32_t oi = valid ? order[i] : 0;
-		const uint32_t e = (uint32_t)((ki & kElemSerial) >> 24);
-		uint64_t kprev = __shfl_up(ki, 1, 64);
-		if (lane == 0)
-			kprev = base > 0 ? sk[base - 1] : 0;
-		const bool head = valid && (i == 0 || (uint32_t)((kprev & kElemSerial) >> 24) != e);
-		bool present = false;
-		int m0 = -1000;  // absent: below every prio (signal.go:93-95)
-		if (head) {
-			uint64_t v = 0;
-			present = tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v);
-			m0 = present ? (int)slot_prio(v) : -1000;
-			distinct++;
-		}
-		int m = m0;
-		uint32_t last_new = 0xFFFFFFFFu;
-		auto take = [&](uint64_t kj, uint32_t oj) {
-			const uint32_t k = (uint32_t)kj & kSerialMask;
-			const int p = lm.val[(kj >> 56) & 3];
-			if (p > m || k == last_new) {
-				flags[oj] = 1;
-				m = max(m, p);
-				last_new = k;
-			}
-		};
-		bool walking = head, beyond = false;
-		for (uint32_t t = 0; __ballot(walking); t++) {
-			const uint32_t src = (lane + t) & 63;
-			const uint64_t kj = __shfl(ki, src, 64);
-			const uint32_t oj = __shfl(oi, src, 64);
-			const int vj = __shfl((int)valid, src, 64);
-			if (walking) {
-				if (lane + t >= 64) {  // the run goes on past this wave's positions
-					walking = false;
-					beyond = true;
-				} else if (!vj || (uint32_t)((kj & kElemSerial) >> 24) != e) {
-					walking = false;
-				} else {
-					take(kj, oj);
-				}
-			}
-		}
-		if (beyond) {
-			for (uint64_t j = base + 64; j < n; j++) {
-				const uint64_t kj = sk[j];
-				if ((uint32_t)((kj & kElemSerial) >> 24) != e)
-					break;
-				take(kj, order[j]);
-			}
-		}
-		if (head && m > m0) {  // maxSignal.Merge / newSignal.Merge of the element's final prio
-			changed++;
-			inserted += !present;
-			ovf += tbl_merge(ms, ms_bmask, e, (int8_t)m) < 0;
-			const int r = tbl_merge(ns, ns_bmask, e, (int8_t)m);
-			ns_ins += r == 1;
-			ovf += r < 0;
-		}
-	}
-	block_count(&ctr[kCntInserted], inserted);
-	block_count(&ctr[kCntChanged], changed);
-	block_count(&ctr[kCntAux], ns_ins);
-	block_count(&ctr[kCntOverflow], ovf);
-	block_count(&ctr[kCntDistinct], distinct);
-}
-
-__global__ void k_recs_heads(const uint64_t* __restrict__ sk, uint64_t n, unsigned long long* heads)
+// The sorted positions where an element's run starts, compacted (in no
+// particular order) into heads[0, *cnt).
+__global__ __launch_bounds__(1024) void k_recs_heads(const uint64_t* __restrict__ sk, uint64_t n,
+                                                     unsigned long long* cnt, uint32_t* heads)
 {
 	constexpr uint64_t kElem = ((1ull << 56) - 1) & ~(uint64_t)kSerialMask;
-	uint64_t h = 0;
-	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-		h += i == 0 || ((sk[i] ^ sk[i - 1]) & kElem) != 0;
-	block_count(heads, h);
+	__shared__ uint32_t wbase[16];
+	__shared__ uint32_t s_base;
+	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), nw = blockDim.x >> 6;
+	for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x; b0 < n; b0 += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t i = b0 + threadIdx.x;
+		const bool h = i < n && (i == 0 || ((sk[i] ^ sk[i - 1]) & kElem) != 0);
+		const uint64_t m = __ballot(h);
+		if (lane == 0)
+			wbase[w] = (uint32_t)__popcll(m);
+		__syncthreads();
+		if (threadIdx.x == 0) {
+			uint32_t t = 0;
+			for (uint32_t k = 0; k < nw; k++) {
+				const uint32_t c = wbase[k];
+				wbase[k] = t;
+				t += c;
+			}
+			s_base = t ? (uint32_t)atomicAdd(cnt, (unsigned long long)t) : 0u;
+		}
+		__syncthreads();
+		if (h)
+			heads[s_base + wbase[w] + lane_rank(m)] = (uint32_t)i;
+		__syncthreads();  // wbase / s_base are rewritten by the next step
+	}
 }
 
 static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t n,
@@ -869,11 +873,12 @@ static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** n
 {
 	const hipStream_t s = ctx->stream;
 	void *dk, *dtmp;
-	SYZ_TRY(ws_get(ctx, 48, n * 24 + 256, &dk));
+	SYZ_TRY(ws_get(ctx, 48, n * 28 + 256, &dk));
 	uint64_t* keys = (uint64_t*)dk;
 	uint64_t* keys2 = keys + n;
 	uint32_t* vals = (uint32_t*)(keys2 + n);
 	uint32_t* order = vals + n;
+	uint32_t* heads = order + n;
 	size_t tmp_bytes = 0;
 	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
 	SYZ_TRY(ws_get(ctx, 49, tmp_bytes + 64, &dtmp));
@@ -881,7 +886,7 @@ static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** n
 	k_recs_keys<<<grid_for(n, 256, 8192), 256, 0, s>>>(recs, n, lm.n, keys, vals, &ctx->d_cnt[kCntError]);
 	SYZ_HIP(hipGetLastError());
 	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
-	k_recs_heads<<<grid_for(n, 256, 4096), 256, 0, s>>>(keys2, n, &ctx->d_cnt[kCntDistinct]);
+	k_recs_heads<<<grid_for(n, 1024, 1024), 1024, 0, s>>>(keys2, n, &ctx->d_cnt[kCntDistinct], heads);
 	SYZ_HIP(hipGetLastError());
 	SYZ_TRY(counters_fetch(ctx));
 	if (ctx->h_cnt[kCntError])
@@ -897,10 +902,17 @@ static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** n
 	SYZ_TRY(counters_reset(ctx));
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
-	// (one thread per record position measured slower: 1.09 vs 0.44 ms for 7.3M records)
-	auto walk = (ctx->agg_dbg & SYZSIG_DEBUG_RECS_WAVE) ? k_recs_walk_wave : k_recs_walk;
-	walk<<<grid_for(n, 256, 8192), 256, 0, s>>>(keys2, order, n, lm, ms->slots, ms->nbuckets - 1, nsp->slots,
-	                                            nsp->nbuckets - 1, new_flags, ctx->d_cnt);
+	// (one thread per record position, each walking one record: 1.09 ms for the
+	// owner's 7.3M records; the scan walk 0.44 ms)
+	if (D == 0 || D > n)
+		return fail(SYZSIG_EIO, "triage_records: run head count out of range (internal error)");
+	if (ctx->agg_dbg & SYZSIG_DEBUG_RECS_SCAN)
+		k_recs_walk_scan<<<grid_for(n, 256, 8192), 256, 0, s>>>(keys2, order, n, lm, ms->slots, ms->nbuckets - 1,
+		                                                        nsp->slots, nsp->nbuckets - 1, new_flags, ctx->d_cnt);
+	else
+		k_recs_walk<<<grid_for(D, 256, 8192), 256, 0, s>>>(
+		    heads, D, RecsWalk{keys2, order, n, lm, ms->slots, ms->nbuckets - 1, nsp->slots, nsp->nbuckets - 1, new_flags},
+		    ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[3], s));

@@ -1,5 +1,5 @@
 """CPU: the records-mode algorithm of the owner side (csrc/triage.hip
-k_recs_keys / radix sort / k_recs_walk), restated with numpy, against the
+k_recs_keys / radix sort / k_recs_heads / k_recs_walk), restated with numpy, against the
 oracle's sequential checkNewSignal (oracle/oracle.c orc_triage_batch over the
 calls in serial order; syz-fuzzer/fuzzer.go:494-511, pkg/signal/signal.go:90-131).
 
@@ -15,24 +15,30 @@ import pytest
 from oracle import oracle as O
 
 
-def sorted_walk(rec, m0):
+def sorted_walk(rec, m0, rng=None):
     """rec: u64 records (e << 32 | level << 24 | serial), level = prio here.
-    Returns (flags per record, {e: final prio} of the changed elements)."""
+    Returns (flags per record, {e: final prio} of the changed elements).
+    The runs are walked from their compacted heads (k_recs_heads), in a random
+    order when rng is given: k_recs_heads compacts them in no particular
+    order, and no run's replay depends on another's."""
     e = (rec >> np.uint64(32)).astype(np.uint64)
     serial = rec & np.uint64(0xFFFFFF)
     key = (e << np.uint64(24)) | serial
     order = np.argsort(key, kind="stable")
+    es = e[order]
+    heads = np.flatnonzero(np.r_[True, es[1:] != es[:-1]]) if rec.size else np.zeros(0, np.int64)
+    if rng is not None:
+        heads = rng.permutation(heads)
     flags = np.zeros(rec.size, np.uint8)
     changed = {}
-    i = 0
     n = rec.size
-    while i < n:
-        el = int(e[order[i]])
+    for i in heads.tolist():
+        el = int(es[i])
         m0v = m0.get(el, -1000)
         m = m0v
         last_new = -1
         j = i
-        while j < n and int(e[order[j]]) == el:
+        while j < n and int(es[j]) == el:
             r = int(rec[order[j]])
             p = (r >> 24) & 0xFF
             k = r & 0xFFFFFF
@@ -43,7 +49,6 @@ def sorted_walk(rec, m0):
             j += 1
         if m > m0v:
             changed[el] = m
-        i = j
     return flags, changed
 
 
@@ -64,7 +69,7 @@ def test_sorted_walk_equals_sequential_checknewsignal(seed):
     serial = np.repeat(np.arange(ncall, dtype=np.uint64), clen)
     rec = (sigs.astype(np.uint64) << np.uint64(32)) | (np.repeat(lvl, clen).astype(np.uint64) << np.uint64(24)) | serial
     perm = rng.permutation(nrec)  # the owner receives the records in no particular order
-    flags, changed = sorted_walk(rec[perm], dict(zip(m0e.tolist(), m0p.tolist())))
+    flags, changed = sorted_walk(rec[perm], dict(zip(m0e.tolist(), m0p.tolist())), rng if seed else None)
     oms, ons, obits, _ = O.triage_batch(m0e, m0p, sigs, cs, clen, lvl)
     onew = np.unpackbits(obits.view(np.uint8), bitorder="little")[:nrec].astype(np.uint8)
     np.testing.assert_array_equal(flags, onew[perm])
