@@ -837,7 +837,10 @@ __global__ void k_recs_walk_scan(const uint64_t* __restrict__ sk, const uint32_t
 }
 
 // The sorted positions where an element's run starts, compacted (in no
-// particular order) into heads[0, *cnt).
+// particular order) into heads[0, *cnt).  Each step a block takes
+// kHeadsPer x 1024 positions (all loads issued together), then one block scan
+// and one atomic place its heads.
+constexpr uint32_t kHeadsPer = 8;
 __global__ __launch_bounds__(1024) void k_recs_heads(const uint64_t* __restrict__ sk, uint64_t n,
                                                      unsigned long long* cnt, uint32_t* heads)
 {
@@ -845,12 +848,24 @@ __global__ __launch_bounds__(1024) void k_recs_heads(const uint64_t* __restrict_
 	__shared__ uint32_t wbase[16];
 	__shared__ uint32_t s_base;
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), nw = blockDim.x >> 6;
-	for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x; b0 < n; b0 += (uint64_t)gridDim.x * blockDim.x) {
-		const uint64_t i = b0 + threadIdx.x;
-		const bool h = i < n && (i == 0 || ((sk[i] ^ sk[i - 1]) & kElem) != 0);
-		const uint64_t m = __ballot(h);
+	const uint64_t span = (uint64_t)blockDim.x * kHeadsPer;
+	for (uint64_t b0 = blockIdx.x * span; b0 < n; b0 += (uint64_t)gridDim.x * span) {
+		uint64_t cur[kHeadsPer], prev[kHeadsPer], m[kHeadsPer];
+#pragma unroll
+		for (uint32_t u = 0; u < kHeadsPer; u++) {
+			const uint64_t i = b0 + u * blockDim.x + threadIdx.x;
+			cur[u] = i < n ? sk[i] : 0;
+			prev[u] = i > 0 && i < n ? sk[i - 1] : 0;
+		}
+		uint32_t tot = 0;
+#pragma unroll
+		for (uint32_t u = 0; u < kHeadsPer; u++) {
+			const uint64_t i = b0 + u * blockDim.x + threadIdx.x;
+			m[u] = __ballot(i < n && (i == 0 || ((cur[u] ^ prev[u]) & kElem) != 0));
+			tot += (uint32_t)__popcll(m[u]);
+		}
 		if (lane == 0)
-			wbase[w] = (uint32_t)__popcll(m);
+			wbase[w] = tot;
 		__syncthreads();
 		if (threadIdx.x == 0) {
 			uint32_t t = 0;
@@ -862,8 +877,13 @@ __global__ __launch_bounds__(1024) void k_recs_heads(const uint64_t* __restrict_
 			s_base = t ? (uint32_t)atomicAdd(cnt, (unsigned long long)t) : 0u;
 		}
 		__syncthreads();
-		if (h)
-			heads[s_base + wbase[w] + lane_rank(m)] = (uint32_t)i;
+		uint32_t off = s_base + wbase[w];
+#pragma unroll
+		for (uint32_t u = 0; u < kHeadsPer; u++) {
+			if ((m[u] >> lane) & 1)
+				heads[off + lane_rank(m[u])] = (uint32_t)(b0 + u * blockDim.x + threadIdx.x);
+			off += (uint32_t)__popcll(m[u]);
+		}
 		__syncthreads();  // wbase / s_base are rewritten by the next step
 	}
 }
@@ -886,7 +906,8 @@ static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** n
 	k_recs_keys<<<grid_for(n, 256, 8192), 256, 0, s>>>(recs, n, lm.n, keys, vals, &ctx->d_cnt[kCntError]);
 	SYZ_HIP(hipGetLastError());
 	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
-	k_recs_heads<<<grid_for(n, 1024, 1024), 1024, 0, s>>>(keys2, n, &ctx->d_cnt[kCntDistinct], heads);
+	k_recs_heads<<<grid_for((n + kHeadsPer - 1) / kHeadsPer, 1024, 1024), 1024, 0, s>>>(keys2, n,
+	                                                                                  &ctx->d_cnt[kCntDistinct], heads);
 	SYZ_HIP(hipGetLastError());
 	SYZ_TRY(counters_fetch(ctx));
 	if (ctx->h_cnt[kCntError])
