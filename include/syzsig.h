@@ -79,12 +79,17 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
  * overflow them and take the redo with counted cells;
  * SYZSIG_DEBUG_RECS_SCAN = records mode's sorted walk runs one thread per
  * sorted position (the run heads among them walk their runs) instead of one
- * thread per compacted run head. */
+ * thread per compacted run head;
+ * SYZSIG_DEBUG_RECS_SEL = records mode sorts by the element bits only and its
+ * walk selects each run's records in serial order (a run of more than 64
+ * records falls back to the full-key sort), instead of the full (element,
+ * serial) key sort and in-order runs. */
 #define SYZSIG_DEBUG_FIN_DEFER 32u
 #define SYZSIG_DEBUG_MIN_ATOMIC 64u
 #define SYZSIG_DEBUG_EXACT_CELLS 128u
 #define SYZSIG_DEBUG_CAP_SPILL 256u
 #define SYZSIG_DEBUG_RECS_SCAN 512u
+#define SYZSIG_DEBUG_RECS_SEL 1024u
 int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
 
 /* ---- pkg/signal/signal.go ---- */

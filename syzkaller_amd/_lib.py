@@ -21,6 +21,7 @@ SYZSIG_DEBUG_MIN_ATOMIC = 64
 SYZSIG_DEBUG_EXACT_CELLS = 128
 SYZSIG_DEBUG_CAP_SPILL = 256
 SYZSIG_DEBUG_RECS_SCAN = 512
+SYZSIG_DEBUG_RECS_SEL = 1024
 
 
 class SyzsigError(RuntimeError):

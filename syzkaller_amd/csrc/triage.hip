@@ -729,6 +729,7 @@ __global__ void k_recs_keys(const uint64_t* __restrict__ recs, uint64_t n, uint3
 // The replay of one element run from its head i: checkNewSignal's rule over
 // the run's records in serial order, from M0[e]; then the element's final prio
 // merged into the shard and newSignal.
+constexpr uint32_t kRunMax = 64;  // longest run the element-only sort's walk takes (else: the full-key sort)
 struct RecsWalk {
 	const uint64_t* __restrict__ sk;
 	const uint32_t* __restrict__ order;
@@ -769,6 +770,49 @@ struct RecsWalk {
 			ovf += r < 0;
 		}
 	}
+	// The same replay for a run left in arrival order (records sorted by the
+	// element bits only, stably): the records are taken in (serial, arrival)
+	// order -- the order of the full-key sort -- by selecting the next one in
+	// each of r steps; r <= kRunMax.
+	__device__ void run_sel(uint64_t i)
+	{
+		const uint32_t e = (uint32_t)((sk[i] & kElemSerial) >> 24);
+		distinct++;
+		uint64_t v = 0;
+		const bool present = tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v);
+		const int m0 = present ? (int)slot_prio(v) : -1000;  // absent: below every prio (signal.go:93-95)
+		uint32_t r = 1;
+		while (r < kRunMax && i + r < n && (uint32_t)((sk[i + r] & kElemSerial) >> 24) == e)
+			r++;
+		int m = m0;
+		uint32_t last_new = 0xFFFFFFFFu;
+		uint64_t cur = 0;  // the last taken record's (serial << 8 | position) + 1
+		for (uint32_t step = 0; step < r; step++) {
+			uint64_t best = ~0ull;
+			for (uint32_t t = 0; t < r; t++) {
+				const uint64_t o = ((sk[i + t] & kSerialMask) << 8) | t;
+				best = o >= cur && o < best ? o : best;
+			}
+			cur = best + 1;
+			const uint32_t t = (uint32_t)best & 0xFF;
+			const uint64_t kj = sk[i + t];
+			const uint32_t k = (uint32_t)kj & kSerialMask;
+			const int p = lm.val[(kj >> 56) & 3];
+			if (p > m || k == last_new) {
+				flags[order[i + t]] = 1;
+				m = max(m, p);
+				last_new = k;
+			}
+		}
+		if (m > m0) {
+			changed++;
+			inserted += !present;
+			ovf += tbl_merge(ms, ms_bmask, e, (int8_t)m) < 0;
+			const int rr = tbl_merge(ns, ns_bmask, e, (int8_t)m);
+			ns_ins += rr == 1;
+			ovf += rr < 0;
+		}
+	}
 	__device__ void count(unsigned long long* ctr)
 	{
 		block_count(&ctr[kCntInserted], inserted);
@@ -782,10 +826,15 @@ struct RecsWalk {
 // One thread per element run, over the heads k_recs_heads compacted: every
 // lane of a wave holds a run, so 64 shard probes and merges are in flight per
 // wave.
+template <bool kSel>
 __global__ void k_recs_walk(const uint32_t* __restrict__ heads, uint64_t nh, RecsWalk rw, unsigned long long* ctr)
 {
-	for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nh; t += (uint64_t)gridDim.x * blockDim.x)
-		rw.run(heads[t]);
+	for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nh; t += (uint64_t)gridDim.x * blockDim.x) {
+		if (kSel)
+			rw.run_sel(heads[t]);
+		else
+			rw.run(heads[t]);
+	}
 	rw.count(ctr);
 }
 
@@ -842,7 +891,8 @@ __global__ void k_recs_walk_scan(const uint64_t* __restrict__ sk, const uint32_t
 // and one atomic place its heads.
 constexpr uint32_t kHeadsPer = 8;
 __global__ __launch_bounds__(1024) void k_recs_heads(const uint64_t* __restrict__ sk, uint64_t n,
-                                                     unsigned long long* cnt, uint32_t* heads)
+                                                     unsigned long long* cnt, uint32_t* heads,
+                                                     unsigned long long* nlong)
 {
 	constexpr uint64_t kElem = ((1ull << 56) - 1) & ~(uint64_t)kSerialMask;
 	__shared__ uint32_t wbase[16];
@@ -878,12 +928,18 @@ __global__ __launch_bounds__(1024) void k_recs_heads(const uint64_t* __restrict_
 		}
 		__syncthreads();
 		uint32_t off = s_base + wbase[w];
+		uint32_t lng = 0;
 #pragma unroll
 		for (uint32_t u = 0; u < kHeadsPer; u++) {
-			if ((m[u] >> lane) & 1)
-				heads[off + lane_rank(m[u])] = (uint32_t)(b0 + u * blockDim.x + threadIdx.x);
+			const uint64_t i = b0 + u * blockDim.x + threadIdx.x;
+			if ((m[u] >> lane) & 1) {
+				heads[off + lane_rank(m[u])] = (uint32_t)i;
+				lng += i + kRunMax < n && ((sk[i + kRunMax] ^ cur[u]) & kElem) == 0;  // a run of > kRunMax
+			}
 			off += (uint32_t)__popcll(m[u]);
 		}
+		if (__ballot(lng != 0) && lane == 0)
+			atomicAdd(nlong, 1ull);
 		__syncthreads();  // wbase / s_base are rewritten by the next step
 	}
 }
@@ -899,19 +955,35 @@ static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** n
 	uint32_t* vals = (uint32_t*)(keys2 + n);
 	uint32_t* order = vals + n;
 	uint32_t* heads = order + n;
-	size_t tmp_bytes = 0;
+	// The full (element, serial) key: 7 onesweep passes.  SYZSIG_DEBUG_RECS_SEL:
+	// a stable sort by the element bits alone (4 passes), the walk taking each
+	// run's records in serial order by selection (a run longer than kRunMax
+	// sends the input back to the full-key sort) -- 3 passes saved (0.22 ms at
+	// C4's owner side), the selection walk 0.34 ms dearer: not the default.
+	size_t tmp_bytes = 0, tmp_el = 0;
 	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
+	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_el, keys, keys2, vals, order, (int)n, 24, 56, s));
+	tmp_bytes = std::max(tmp_bytes, tmp_el);
 	SYZ_TRY(ws_get(ctx, 49, tmp_bytes + 64, &dtmp));
 	SYZ_TRY(counters_reset(ctx));
 	k_recs_keys<<<grid_for(n, 256, 8192), 256, 0, s>>>(recs, n, lm.n, keys, vals, &ctx->d_cnt[kCntError]);
 	SYZ_HIP(hipGetLastError());
-	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
-	k_recs_heads<<<grid_for((n + kHeadsPer - 1) / kHeadsPer, 1024, 1024), 1024, 0, s>>>(keys2, n,
-	                                                                                  &ctx->d_cnt[kCntDistinct], heads);
+	bool sel = (ctx->agg_dbg & SYZSIG_DEBUG_RECS_SEL) && !(ctx->agg_dbg & SYZSIG_DEBUG_RECS_SCAN);
+	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, keys, keys2, vals, order, (int)n, sel ? 24 : 0, 56, s));
+	const int hgrid = grid_for((n + kHeadsPer - 1) / kHeadsPer, 1024, 1024);
+	k_recs_heads<<<hgrid, 1024, 0, s>>>(keys2, n, &ctx->d_cnt[kCntDistinct], heads, &ctx->d_cnt[kCntAux2]);
 	SYZ_HIP(hipGetLastError());
 	SYZ_TRY(counters_fetch(ctx));
 	if (ctx->h_cnt[kCntError])
 		return fail(SYZSIG_EINVAL, "triage_records: a record's prio level is out of range");
+	if (sel && ctx->h_cnt[kCntAux2]) {  // a run too long for the selection walk: the full-key sort
+		sel = false;
+		SYZ_TRY(counters_reset(ctx));
+		SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
+		k_recs_heads<<<hgrid, 1024, 0, s>>>(keys2, n, &ctx->d_cnt[kCntDistinct], heads, &ctx->d_cnt[kCntAux2]);
+		SYZ_HIP(hipGetLastError());
+		SYZ_TRY(counters_fetch(ctx));
+	}
 	// room for every distinct element changing
 	const uint64_t D = ctx->h_cnt[kCntDistinct];
 	SYZ_TRY(set_reserve(ms, D));
@@ -931,7 +1003,7 @@ static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** n
 		k_recs_walk_scan<<<grid_for(n, 256, 8192), 256, 0, s>>>(keys2, order, n, lm, ms->slots, ms->nbuckets - 1,
 		                                                        nsp->slots, nsp->nbuckets - 1, new_flags, ctx->d_cnt);
 	else
-		k_recs_walk<<<grid_for(D, 256, 8192), 256, 0, s>>>(
+		(sel ? k_recs_walk<true> : k_recs_walk<false>)<<<grid_for(D, 256, 8192), 256, 0, s>>>(
 		    heads, D, RecsWalk{keys2, order, n, lm, ms->slots, ms->nbuckets - 1, nsp->slots, nsp->nbuckets - 1, new_flags},
 		    ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());

@@ -408,17 +408,19 @@ def test_triage_c2_properties(gpu):
     assert int(cnew3.sum()) == 0 and int(bits3.count_nonzero()) == 0 and ns3.is_nil() and ms.Len() == n_before
 
 
-@pytest.mark.parametrize("agg,npool", [(1, 2_500_000), (0, 2_500_000), ("scan", 2_500_000), (1, 20_000),
-                                       ("scan", 20_000)])
+@pytest.mark.parametrize("agg,npool", [(1, 2_500_000), (0, 2_500_000), ("scan", 2_500_000), ("sel", 2_500_000),
+                                       (1, 200_000), ("sel", 200_000), ("sel", 20_000), ("scan", 20_000)])
 def test_records_mode_vs_oracle(gpu, agg, npool):
     """Records mode (the owner side of a sharded step, triage.hip
     triage_records_impl): ~1.2M records (e, level, serial) in a shuffled order,
     each serial one call of up to 6 distinct elements at one level, against a
     shard holding part of the pool.  agg=1 takes the sorted path (records
-    sorted by (element, serial), one thread per compacted run head; "scan":
-    the same with SYZSIG_DEBUG_RECS_SCAN, one thread per sorted position),
-    agg=0 the per-record probe path.  npool=20k gives ~60 records per element
-    (long runs).  All must flag exactly the
+    by (element, serial), one thread per compacted run head; "sel":
+    SYZSIG_DEBUG_RECS_SEL, sorted by the element bits only, each head selecting
+    its run's records in serial order; "scan": SYZSIG_DEBUG_RECS_SCAN, one
+    thread per sorted position), agg=0 the per-record probe path.  npool=200k
+    gives ~6 records per element; npool=20k ~60, with runs past the selection
+    walk's 64 (its redo with the full-key sort).  All must flag exactly the
     records the oracle's sequential checkNewSignal over the calls in serial
     order marks new, and leave the same shard and newSignal."""
     from syzkaller_amd import signal as S
@@ -446,10 +448,10 @@ def test_records_mode_vs_oracle(gpu, agg, npool):
     ns = S.Signal(None, gpu.eng)
     drec = torch.from_numpy(rec[perm].view(np.int64)).to(gpu.dev)
     flags = torch.zeros(nrec, dtype=torch.uint8, device=gpu.dev)
-    from syzkaller_amd._lib import SYZSIG_DEBUG_RECS_SCAN
+    from syzkaller_amd._lib import SYZSIG_DEBUG_RECS_SCAN, SYZSIG_DEBUG_RECS_SEL
 
     gpu.eng.set_agg(0 if agg == 0 else 1, 0)
-    gpu.eng.set_debug(SYZSIG_DEBUG_RECS_SCAN if agg == "scan" else 0)
+    gpu.eng.set_debug({"scan": SYZSIG_DEBUG_RECS_SCAN, "sel": SYZSIG_DEBUG_RECS_SEL}.get(agg, 0))
     try:
         st = gpu.triage_records(ms, ns, drec, [0, 1, 2, 3], flags)
     finally:
