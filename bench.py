@@ -44,8 +44,9 @@ MIN_KERNELS = ("k_min_calls+k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg"
                "+k_min_from_dist+k_count_u8")
 MIN_BYTES_PER_ENTRY, MIN_BYTES_PER_DISTINCT = 5.0, 4.0  # Minimize: (elem, prio) entry + covered[e]
 # N > 1: the source's aggregation, then the owner's records-mode triage of the staircases
-K3_DIST_KERNELS = ("k_prio_presence+k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg+k_stair_count+k_stair_scatter"
-                   "+k_recs_keys+k_recs_heads+k_recs_walk")
+K3_DIST_KERNELS = ("k_fast_prep+k_cell_plan_fast+k_agg_scatter_blk+k_agg+k_stair_bucket+k_stair_heads"
+                   "+k_step_heads+k_rp_count+k_rp_colsum+k_rp_scan+k_rp_coloffs+k_rp_scatter+k_rp_triage+k_step_status"
+                   "+k_step_back")
 
 
 def parse():
@@ -75,6 +76,7 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming line")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 per-rank line")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 line")
+    ap.add_argument("--no-gw", action="store_true", help="skip the C2 global-walk line")
     return ap.parse_args()
 
 
@@ -82,15 +84,17 @@ TRIAGE_KEYS = ("programs_per_gpu", "calls", "pcs_per_call", "m0_per_gpu", "skew"
 MIN_KEYS = ("workload", "contexts", "entries", "mean_len")
 
 
-def pmc_traffic(kernel_prefixes, cfg, keys=TRIAGE_KEYS):
-    """HBM bytes per launch of the dominant kernel from the newest committed
-    rocprofv3 PMC summary (profiles/*/summary.json, written by
+def pmc_traffic(kernel_prefixes, cfg, keys=TRIAGE_KEYS, expect_ms=None, tol=0.15):
+    """HBM bytes per launch of the dominant kernel chain from the newest
+    committed rocprofv3 PMC summary (profiles/*/summary.json, written by
     scripts/summarize_prof.py from separate FETCH_SIZE / WRITE_SIZE passes of
-    this same workload: scripts/profile.sh) whose workload matches; None if
-    there is none."""
+    this same workload: scripts/profile.sh) whose workload matches.  expect_ms:
+    the line's own chain time; a summary whose matched kernels' summed average
+    duration differs from it by more than `tol` profiled other code and is not
+    used.  Returns (bytes or None, source path or None, reason or None)."""
     import glob
 
-    best = None
+    best, rejected = None, []
     for f in glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")):
         try:
             d = json.load(open(f))
@@ -99,15 +103,25 @@ def pmc_traffic(kernel_prefixes, cfg, keys=TRIAGE_KEYS):
         bc = d.get("bench_config") or {}
         if any(bc.get(k) != cfg.get(k) for k in keys):
             continue
-        tot, hit = 0.0, False
+        tot, ms, hit = 0.0, 0.0, False
         for name, e in d.get("kernels", {}).items():
             if any(name == k or name.startswith(k + "<") for k in kernel_prefixes) and "traffic_bytes" in e:
                 tot += e["traffic_bytes"]
+                ms += e.get("avg_ms", 0.0)
                 hit = True
+        if not hit:
+            continue
+        rel = os.path.relpath(f, ROOT)
+        if expect_ms and abs(ms / expect_ms - 1.0) > tol:
+            rejected.append(f"{rel}: profiled chain {ms:.3f} ms vs this line's {expect_ms:.3f} ms")
+            continue
         t = (d.get("created", 0), f)  # the newest summary (created stamp), then name
-        if hit and (best is None or t > best[0]):
-            best = (t, tot, os.path.relpath(f, ROOT))
-    return (best[1], best[2]) if best else (None, None)
+        if best is None or t > best[0]:
+            best = (t, tot, rel)
+    if best:
+        return best[1], best[2], None
+    return None, None, ("no PMC summary of this workload and code: " + "; ".join(rejected)) if rejected else \
+        "no PMC summary of this workload"
 
 
 def cpu_model():
@@ -198,7 +212,7 @@ def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
     byts = MIN_BYTES_PER_ENTRY * N + MIN_BYTES_PER_DISTINCT * distinct
     cfg = {"workload": f"BASELINE config 3: Minimize over a {n}-program synthetic corpus, 1 GPU",
            "contexts": n, "entries": N, "distinct": distinct, "mean_len": mean, "survivors": cnt}
-    traffic, src = pmc_traffic(["syz::" + k for k in MIN_KERNELS.split("+")], cfg, MIN_KEYS)
+    traffic, src, note = pmc_traffic(["syz::" + k for k in MIN_KERNELS.split("+")], cfg, MIN_KEYS, expect_ms=t)
     achieved = byts / (t * 1e-3) / 1e9
     return {"metric": "signal.Minimize corpus entries/sec", "value": N / (t * 1e-3), "unit": "entries/s",
             "higher_is_better": True, "ms": t, "dtype": "u32",
@@ -206,6 +220,7 @@ def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
             "roofline": {"bound": "hbm", "kernel": MIN_KERNELS,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+                         "traffic_note": note,
                          "bytes_per_unit": f"{MIN_BYTES_PER_ENTRY} B/entry + {MIN_BYTES_PER_DISTINCT} B/distinct",
                          "avg_launch_ms": t}}
 
@@ -267,7 +282,8 @@ def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m
     achieved = PROBE_BYTES_PER_REC * total / (chain * 1e-3) / 1e9
     wl = (f"BASELINE config 5 at one rank's share of 8 GPUs: {nbatches} consecutive batches of {programs} programs "
           f"x {calls} calls x {pcs} PCs, skew=1, each against the state the previous one left (M0 {m0})")
-    traffic, src = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], {"workload": wl}, ("workload",))
+    traffic, src, note = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], {"workload": wl}, ("workload",),
+                                     expect_ms=chain / nbatches)
     return {"metric": "signal elems triaged/sec (Diff+Merge), streaming skewed batches",
             "value": total / wall, "unit": "elems/s", "higher_is_better": True,
             "ms_per_batch": wall * 1e3 / nbatches, "dtype": "u32",
@@ -277,23 +293,78 @@ def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m
                        "new_per_batch": [x["changed"] for x in sts], "distinct": [x["distinct"] for x in sts]},
             "roofline": {"bound": "hbm", "kernel": K3_KERNELS, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+                         "traffic_note": note,
                          "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": total // nbatches,
                          "avg_launch_ms": chain / nbatches}}
 
 
-def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_000, reps=3):
-    """BASELINE config 4 seen from one rank of an 8-GPU node, on one GPU:
-    (1) the source side of a sharded step -- this rank's C2 batch aggregated per
-    element, each element's staircase records routed to its owner
-    (shard_agg_partition); (2) the owner side -- owner 0's records-mode triage
-    of the staircase records all 8 sources send it (the 8 sources' batches are
-    synthesized here one after another, program ranges r*P..), against owner
-    0's shard of a 1B-element maxSignal (125M elements).  The all-to-all
-    between them is not on one GPU: its bytes are reported.  value = this
-    rank's records / (source + owner device time)."""
+def c2_global_walk_line(dev, pairs, P, C, L, reps=5, m0=10_000_000):
+    """BASELINE config 2 on SURVEY 8(d)'s own input distribution: every call a
+    walk b <- (4b + 1 + r%4) mod B over all B = 2^20 blocks from a uniform
+    block (csrc/common.h synth_trace, global_walk=1), so almost every PC emits
+    a signal (~1.07e9 records per batch) -- against a 10M-element M0 that holds
+    the whole 5.2M-edge universe (prio uniform 0..3) plus random elements.
+    Same step as the headline: maxSignal back to M0, then the whole batch
+    (syz-fuzzer/fuzzer.go:494-511 per call, batched)."""
     from syzkaller_amd import signal as S
     from syzkaller_amd import synth
-    from syzkaller_amd.dist import SIGNAL_PRIO_LEVELS, owner_of_torch
+
+    cfg = synth.synth_default(global_walk=1)
+    sigs, cs, cnt, prio, nrec, npc = synth_batch(dev, cfg, 0, P, C, L)
+    m0e, m0p = dev.synth_m0(cfg, 1, m0)
+    pristine = dev.deserialize(m0e, m0p)
+    del m0e, m0p
+    b, _, _ = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
+    ms = pristine.clone()
+    ns = S.Signal.make(4_000_000, dev.eng)
+    walls, chains, st = [], [], None
+    for r in range(reps + 1):
+        if ms.capacity() != pristine.capacity():
+            ms = pristine.clone()
+        else:
+            ms.copy_from(pristine)
+        ns.clear()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        st = dev.triage_b(ms, ns, b)
+        torch.cuda.synchronize()
+        if r:
+            walls.append(time.perf_counter() - t)
+            chains.append(chain_ms(st))
+    wall, chain = float(np.median(walls)), float(np.median(chains))
+    achieved = PROBE_BYTES_PER_REC * nrec / (chain * 1e-3) / 1e9
+    wl = (f"BASELINE config 2 on SURVEY 8(d)'s global walk: {P} programs x {C} calls x {L} PCs over all 2^20 blocks "
+          f"vs a {m0}-element maxSignal holding the edge universe")
+    traffic, src, note = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], {"workload": wl}, ("workload",),
+                                     expect_ms=chain)
+    del sigs, cs, cnt, prio, b
+    return {"metric": "signal elems triaged/sec (Diff+Merge), SURVEY 8(d) global-walk traces",
+            "value": nrec / wall, "unit": "elems/s", "higher_is_better": True, "ms": wall * 1e3, "dtype": "u32",
+            "config": {"workload": wl, "records": nrec, "pcs": npc, "distinct": st["distinct"],
+                       "changed": st["changed"], "retries": st["retries"], "runs": st["runs"],
+                       "parts": st["parts"], "overflow_parts": st["overflow_parts"]},
+            "roofline": {"bound": "hbm", "kernel": K3_KERNELS, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+                         "traffic_note": note, "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": nrec,
+                         "avg_launch_ms": chain}}
+
+
+def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_000, reps=3):
+    """BASELINE config 4 seen from one rank of an 8-GPU node, on one GPU, with
+    the stream-ordered step's own calls (syzsig_step_*): (1) the source side --
+    this rank's C2 batch aggregated per element, each element's staircase into
+    one fixed bucket per owner (syzsig_step_send_dev); (2) the owner side --
+    owner 0's LDS-partitioned replay of the buckets all 8 sources send it
+    (syzsig_step_own_dev; the 8 sources' batches are synthesized here one
+    after another, program ranges r*P..) against owner 0's shard of a
+    1B-element maxSignal (125M elements, built with synth_m0_shard); (3) the
+    flags back at this rank's source (syzsig_step_back_dev).  The two
+    equal-split all-to-alls between them are not on one GPU: their bytes are
+    reported.  value = this rank's records / (source + owner + back device time)."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+    from syzkaller_amd._lib import STEP_HDR_COUNT
+    from syzkaller_amd.dist import SIGNAL_PRIO_LEVELS
 
     cfg = synth.synth_default()
     levels = list(SIGNAL_PRIO_LEVELS)
@@ -308,64 +379,88 @@ def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_
         torch.cuda.synchronize()
         return out, a.elapsed_time(b)
 
-    # owner 0's received records: every source's staircase records for shard 0
-    recv_parts, src_ms, sent = [], [], None
+    # every source's bucket for owner 0 (a generous cap first; the step's cap is
+    # then what all sources needed, as ShardedTriage agrees on it)
+    cap_big = nrec0 // world + 4096
+    send_big = torch.empty(world * (cap_big + 1), dtype=torch.int64, device=dev.dev)
+    parts, max_out, sent_per_owner, b0 = [], 0, None, None
     for r in range(world):
         if r == 0:
             s_sigs, s_cs, s_cnt, s_prio = sigs, cs, cnt, prio
         else:
             s_sigs, s_cs, s_cnt, s_prio, _, _ = synth_batch(dev, cfg, r * P, P, C, L)
         b, _, _ = dev.batch(s_sigs, s_cs, s_cnt, s_prio, want_bits=False)
-        send = torch.empty(max(int(s_sigs.numel()), 1), dtype=torch.int64, device=dev.dev)
-        for rep in range(reps + 1 if r == 0 else 1):
-            (counts, st), ms_ = ev_time(lambda: dev.shard_agg_partition(b, r * P * C, levels, world, send))
-            if r == 0 and rep:
-                src_ms.append(ms_)
+        dev.step_send(b, r * P * C, levels, world, cap_big, send_big)
+        st = dev.step_finish()
+        if st["global_void"] or st["src_void"] or st["max_out"] > cap_big:
+            raise RuntimeError(f"c4_rank: source {r} bucket pass failed: {st}")
+        max_out = max(max_out, st["max_out"])
+        hdr = send_big.view(world, cap_big + 1)[:, 0].cpu().numpy().view(np.uint64) & np.uint64(STEP_HDR_COUNT)
         if r == 0:
-            sent = counts
-            src_st = st
-        recv_parts.append(send[: counts[0]].clone())
-        del send, b
+            sent_per_owner, src_st, b0 = [int(x) for x in hdr], st, (b, s_sigs, s_cs, s_cnt, s_prio)
+        parts.append(send_big[1: 1 + int(hdr[0])].clone())
         if r:
-            del s_sigs, s_cs, s_cnt, s_prio
-    recv = torch.cat(recv_parts)
-    del recv_parts
+            del s_sigs, s_cs, s_cnt, s_prio, b
+    del send_big
+    cap = int(max_out * 1.25) + 4096
+    n = world * (cap + 1)
+    recv = torch.zeros(n, dtype=torch.int64, device=dev.dev)
+    rv = recv.view(world, cap + 1)
+    for r, x in enumerate(parts):
+        rv[r, 0] = x.numel()
+        rv[r, 1: 1 + x.numel()] = x
+    received = sum(x.numel() for x in parts)
+    del parts
     # owner 0's shard of the 1B-element M0
-    ge, gp = dev.synth_m0(cfg, 2048, m0_total)
-    own = owner_of_torch(ge, world) == 0
-    se, sp = ge[own].contiguous(), gp[own].contiguous()
-    del ge, gp, own
+    se, sp = dev.synth_m0_shard(cfg, 2048, m0_total, world, 0)
     pristine = dev.deserialize(se, sp)
     shard_len = int(se.numel())
     del se, sp
-    flags = torch.empty(recv.numel(), dtype=torch.uint8, device=dev.dev)
-    own_ms, ost = [], None
+    b, s_sigs, s_cs, s_cnt, s_prio = b0
+    send = torch.empty(n, dtype=torch.int64, device=dev.dev)
+    flags = torch.empty(n, dtype=torch.uint8, device=dev.dev)
+    back = torch.zeros(n, dtype=torch.uint8, device=dev.dev)
+    src_ms, own_ms, back_ms, ost = [], [], [], None
     for rep in range(reps + 1):
+        _, t_src = ev_time(lambda: dev.step_send(b, 0, levels, world, cap, send))
+        dev.step_finish()
         shard = pristine.clone()
         ns = S.Signal.make(4_000_000, dev.eng)
-        ost, ms_ = ev_time(lambda: dev.triage_records(shard, ns, recv, levels, flags))
+        _, t_own = ev_time(lambda: dev.step_own(shard, ns, recv, world, cap, levels, flags))
+        ost = dev.step_finish()
+        # this source's flags back: owner 0's from the replay, the other owners' none
+        back.view(world, cap + 1)[0].copy_(flags.view(world, cap + 1)[0])
+        _, t_back = ev_time(lambda: dev.step_back(b, 0, send, world, cap, back))
+        dev.step_finish()
         if rep:
-            own_ms.append(ms_)
-        del shard
-    s_ms, o_ms = float(np.median(src_ms)), float(np.median(own_ms))
-    step = s_ms + o_ms
+            src_ms.append(t_src)
+            own_ms.append(t_own)
+            back_ms.append(t_back)
+        del shard, ns
+    if ost["global_void"] or ost["owners_void"] or ost["received"] != received:
+        raise RuntimeError(f"c4_rank: the owner pass failed: {ost}")
+    s_ms, o_ms, k_ms = float(np.median(src_ms)), float(np.median(own_ms)), float(np.median(back_ms))
+    step = s_ms + o_ms + k_ms
     achieved = PROBE_BYTES_PER_REC * nrec0 / (step * 1e-3) / 1e9
-    xbytes = 8 * (sum(sent) - sent[0])
-    wl = (f"BASELINE config 4, one rank of {world}: this rank's {P} x {C} x {L} batch (source aggregation + staircase "
-          f"routing), then owner 0's records-mode triage of what all {world} sources send it against its "
-          f"{shard_len}-element shard of a {m0_total}-element maxSignal")
-    traffic, src = pmc_traffic(["syz::" + k for k in K3_DIST_KERNELS.split("+")], {"workload": wl}, ("workload",))
+    xbytes = 8 * (world - 1) * (cap + 1) + (world - 1) * (cap + 1)  # records out + flags back per rank
+    wl = (f"BASELINE config 4, one rank of {world}: this rank's {P} x {C} x {L} batch (source aggregation into "
+          f"staircase buckets), owner 0's LDS-partitioned replay of what all {world} sources send it against its "
+          f"{shard_len}-element shard of a {m0_total}-element maxSignal, the flags back")
+    traffic, src, note = pmc_traffic(["syz::" + k for k in K3_DIST_KERNELS.split("+")], {"workload": wl},
+                                     ("workload",), expect_ms=step)
     return {"metric": "signal elems triaged/sec (Diff+Merge) per rank of a 1B-element maxSignal over 8 GPUs",
             "value": nrec0 / (step * 1e-3), "unit": "elems/s", "higher_is_better": True, "dtype": "u32",
-            "ms": step, "source_ms": s_ms, "owner_ms": o_ms,
+            "ms": step, "source_ms": s_ms, "owner_ms": o_ms, "back_ms": k_ms,
             "config": {"workload": wl,
-                       "records": nrec0, "staircase_sent": sum(sent), "sent_per_owner": sent,
-                       "owner_received": int(recv.numel()), "shard_elems": shard_len,
+                       "records": nrec0, "staircase_sent": src_st["sent"], "sent_per_owner": sent_per_owner,
+                       "bucket_cap": cap, "owner_received": received, "shard_elems": shard_len,
+                       "owner_parts": ost["own_parts"], "owner_distinct": ost["own_distinct"],
                        "xgmi_bytes_out": xbytes,
                        "xgmi_ms_at_7x153GBps": xbytes / (7 * 153e9) * 1e3,
-                       "source_distinct": src_st.get("distinct"), "owner_changed": ost.get("changed")},
+                       "source_distinct": src_st["distinct"], "owner_changed": ost["changed"]},
             "roofline": {"bound": "hbm", "kernel": K3_DIST_KERNELS, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+                         "traffic_note": note,
                          "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": nrec0, "avg_launch_ms": step}}
 
 
@@ -470,6 +565,14 @@ def ingest_stage(dev, sigs, cs, cnt, prio, comp, P, C, reps=5):
     return float(np.median(ms)), ok
 
 
+def progress(rank, msg):
+    """One line per setup phase on stderr (a silent multi-minute setup looks hung)."""
+    print(f"[bench rank {rank}] {msg} (t={time.perf_counter() - T0:.1f}s)", file=sys.stderr, flush=True)
+
+
+T0 = time.perf_counter()
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -494,11 +597,13 @@ def main():
     from syzkaller_amd import synth
     from syzkaller_amd.device import Device
 
+    progress(rank, f"device {local}, world {world}")
     dev = Device(local)
     dev.L.syzsig_ctx_set_timing(dev.eng.h, 1)
     cfg = synth.synth_default(skew=a.skew)
     P, C, L = a.programs, a.calls, a.pcs
     # ---- setup: traces -> K1+K2 (timed as a stage, not part of `value`)
+    progress(rank, f"traces {P} x {C} x {L}")
     cl = torch.full((P * C,), L, dtype=torch.int32)
     pcs, cs, cl, prio = dev.synth_traces(cfg, rank * P, P, C, cl)
     pidx = torch.arange(P + 1, dtype=torch.int32, device=dev.dev) * C
@@ -518,15 +623,15 @@ def main():
     nrec = int(cnt.to(torch.int64).sum().item())
     # ---- M0 (maxSignal before the batch): 10M elements per GPU
     if distributed:
-        from syzkaller_amd.dist import SIGNAL_PRIO_LEVELS, GpuShardOps, ShardedTriage, owner_of_torch
+        from syzkaller_amd.dist import SIGNAL_PRIO_LEVELS, GpuShardOps, ShardedTriage
 
-        # BASELINE config 4: one maxSignal of m0_total elements, hash-sharded
-        ge, gp = dev.synth_m0(cfg, 2048, a.m0_total)
-        own = owner_of_torch(ge, world) == rank
-        m0e, m0p = ge[own].contiguous(), gp[own].contiguous()
-        del ge, gp
+        # BASELINE config 4: one maxSignal of m0_total elements, hash-sharded;
+        # each rank generates only its own shard (in index order)
+        progress(rank, f"M0 shard of {a.m0_total} elements")
+        m0e, m0p = dev.synth_m0_shard(cfg, 2048, a.m0_total, world, rank)
     else:
         m0e, m0p = dev.synth_m0(cfg, 2048, a.m0)
+    progress(rank, f"maxSignal of {m0e.numel()} elements")
     ms = dev.deserialize(m0e, m0p)
     if a.table_hint:
         sized = S.Signal.make(a.table_hint, dev.eng)
@@ -543,11 +648,9 @@ def main():
     b, bits, cnew = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
     if distributed:
         ops = GpuShardOps(dev)
-        # the prio levels are agreed once for the workload (signalPrio gives 0..3,
-        # fuzzer.go:513-521), not with a collective every step
-        sharded = ShardedTriage(ops, ms, ns)
-        lv = sharded.levels(prio)
-        sharded.fixed_levels = sorted(set(lv) | set(SIGNAL_PRIO_LEVELS)) if len(set(lv) | set(SIGNAL_PRIO_LEVELS)) <= 4 else lv
+        # the prio levels are fixed for the workload (signalPrio gives 0..3,
+        # fuzzer.go:513-521), not agreed with a collective every step
+        sharded = ShardedTriage(ops, ms, ns, levels=SIGNAL_PRIO_LEVELS)
 
     def reset():
         # back to M0: a copy of the whole table, or -- when that moves more bytes,
@@ -569,17 +672,20 @@ def main():
         ns.clear()
         if distributed:
             st = dict(sharded.step((b, bits, cnew), prio, rank * P * C)[2])
-            src = ops.last_source_stats
-            # source-side aggregation, then the owner's records-mode triage
-            st["decide_ms"] = st["probe_ms"] + st["decide_ms"]
-            for k in ("part_ms", "probe_ms", "distinct", "parts", "overflow_parts"):
-                st[k] = src[k]
-            st["records"] = src["records"]
+            # source aggregation + staircase buckets, the owner's replay, the flags back
+            st["part_ms"], st["probe_ms"], st["decide_ms"] = st["src_ms"], st["own_ms"], st["back_ms"]
             return st
         return dev.triage_b(ms, ns, b)
 
+    progress(rank, f"warmup {a.warmup}")
     for _ in range(a.warmup):
         step()
+        if distributed and ms.capacity() != pristine.capacity():
+            # the owner reserved its shard for a step's worst case (bucket cap x
+            # ranks): the snapshot gets the same room, so that the state reset
+            # stays a restore of the changed slots
+            pristine.reserve(world * sharded.cap)
+    progress(rank, f"timed {a.steps}")
     stats = []
     if distributed:
         dist.barrier()
@@ -658,13 +764,15 @@ def main():
                            "checked equal to M0 after the timed steps",
         }
     if rank == 0:
-        traffic, src = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], out["config"])
+        traffic, src, note = pmc_traffic(["syz::" + k for k in (K3_KERNELS if not distributed else K3_DIST_KERNELS)
+                                          .split("+")], out["config"], expect_ms=k3_ms)
         out["roofline"]["traffic"] = traffic
         out["roofline"]["traffic_source"] = src
+        out["roofline"]["traffic_note"] = note
         # K1+K2 (executor write_coverage_signal on device) as its own line
         e_ms = float(np.median(edge_dev_ms))
         e_ach = EDGE_BYTES_PER_PC * npc / (e_ms * 1e-3) / 1e9
-        e_traffic, e_src = pmc_traffic(["syz::k_edge_dedup"], out["config"])
+        e_traffic, e_src, e_note = pmc_traffic(["syz::k_edge_dedup"], out["config"], expect_ms=e_ms)
         out["lines"] = {"edge": {
             "metric": "KCOV PCs -> edge signals/sec (write_coverage_signal K1 + dedup K2)", "value": npc / (e_ms * 1e-3),
             "unit": "PCs/s", "higher_is_better": True, "ms": e_ms, "dtype": "u64->u32",
@@ -672,11 +780,14 @@ def main():
                        "signals": nrec},
             "roofline": {"bound": "hbm", "kernel": "k_edge_dedup", "achieved": e_ach, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": e_ach / HBM_PEAK_GBS, "traffic": e_traffic, "traffic_source": e_src,
+                         "traffic_note": e_note,
                          "bytes_per_unit": EDGE_BYTES_PER_PC, "units_per_launch": npc, "avg_launch_ms": e_ms}}}
     if rank == 0 and world == 1 and not a.no_min:
         out["lines"]["minimize"] = minimize_line(dev, a.min_contexts)
     if rank == 0 and world == 1 and not a.no_c5:
         out["lines"]["c5"] = c5_line(dev, pairs)
+    if rank == 0 and world == 1 and not a.no_gw:
+        out["lines"]["c2_global_walk"] = c2_global_walk_line(dev, pairs, P, C, L)
     if rank == 0 and world == 1 and not a.no_c1:
         out["lines"]["c1"] = c1_line(dev)
     if rank == 0 and world == 1 and not a.no_c4:

@@ -42,7 +42,7 @@ extern "C" {
 #define SYZSIG_ERANGE (-34)    /* a size limit of this ABI exceeded */
 #define SYZSIG_ECORRUPT (-74)  /* panic("corrupted Serial"), pkg/signal/signal.go:60-62 */
 
-#define SYZSIG_ABI_VERSION 3
+#define SYZSIG_ABI_VERSION 4
 
 typedef struct syzsig_ctx syzsig_ctx;
 typedef struct syzsig_set syzsig_set;
@@ -76,20 +76,11 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
  * SYZSIG_DEBUG_EXACT_CELLS = large triage runs partition records into counted
  * cells (count pass + scan) instead of capped cells;
  * SYZSIG_DEBUG_CAP_SPILL = capped cells of 64 records, so that dense runs
- * overflow them and take the redo with counted cells;
- * SYZSIG_DEBUG_RECS_SCAN = records mode's sorted walk runs one thread per
- * sorted position (the run heads among them walk their runs) instead of one
- * thread per compacted run head;
- * SYZSIG_DEBUG_RECS_SEL = records mode sorts by the element bits only and its
- * walk selects each run's records in serial order (a run of more than 64
- * records falls back to the full-key sort), instead of the full (element,
- * serial) key sort and in-order runs. */
+ * overflow them and take the redo with counted cells. */
 #define SYZSIG_DEBUG_FIN_DEFER 32u
 #define SYZSIG_DEBUG_MIN_ATOMIC 64u
 #define SYZSIG_DEBUG_EXACT_CELLS 128u
 #define SYZSIG_DEBUG_CAP_SPILL 256u
-#define SYZSIG_DEBUG_RECS_SCAN 512u
-#define SYZSIG_DEBUG_RECS_SEL 1024u
 int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
 
 /* ---- pkg/signal/signal.go ---- */
@@ -110,6 +101,11 @@ int syzsig_set_copy_from(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src
  * are copied back, so the cost follows the changes, not the table.  Same
  * capacity required (SYZSIG_EINVAL if dst grew).  Stream-ordered. */
 int syzsig_set_restore_keys(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src, const syzsig_set* keys);
+/* Grow s (if needed) so that `extra` more elements fit under the default load
+ * policy -- what a triage call reserves for its worst case; a caller that
+ * keeps a snapshot of a set reserves the snapshot alike to keep capacities
+ * equal (syzsig_set_restore_keys). */
+int syzsig_set_reserve(syzsig_ctx* ctx, syzsig_set* s, uint64_t extra);
 /* *equal = 1 iff a and b have the same capacity, length and slot words. */
 int syzsig_set_equal(syzsig_ctx* ctx, const syzsig_set* a, const syzsig_set* b, int* equal);
 /* Len / Empty, signal.go:23-29. */
@@ -165,7 +161,11 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, const uint32
  * new_max[g] = fuzzer g's newMaxSignal (NULL = nil): a polling fuzzer's set is
  * freed (nil) and may be replaced by a new one.  replies[i] = poll i's
  * r.MaxSignal as a set (NULL = empty Serial) for the caller to Serialize and
- * free.  Host arrays (the RPC payloads). */
+ * free.  Host arrays (the RPC payloads).
+ * Limits of one call (SYZSIG_ERANGE, nothing touched): npolls + nfuzzers <
+ * 2^24 - 1, npolls * nfuzzers <= 2^28, total entries * nfuzzers <= 2^31.  A
+ * caller splits a larger batch into consecutive calls (the loop is sequential,
+ * so that is the same result: signal.py manager_poll does). */
 int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_max, uint32_t nfuzzers,
                               const uint32_t* poll_fuzzer, const uint64_t* poll_off, const uint32_t* elems,
                               const int8_t* prios, uint32_t npolls, syzsig_set** replies);
@@ -392,6 +392,78 @@ int syzsig_shard_agg_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uin
                                      const uint64_t* d_send, uint64_t n_send, const uint8_t* d_back_flags,
                                      syzsig_batch_stats* stats);
 
+/* ---- the stream-ordered sharded step (one process per GPU) ----
+ * The three calls below only enqueue work on the context's stream and return;
+ * syzsig_step_finish is the step's one host synchronisation.  The exchange
+ * uses fixed-size buckets, so no split sizes have to reach the host first:
+ * each source writes, for every owner g, a bucket of cap + 1 words at
+ * d_send[g * (cap + 1)]:
+ *   word 0      header: records for g (the true count, even past cap)
+ *               | SYZSIG_STEP_HDR_VOID (the source's run is void)
+ *               | SYZSIG_STEP_HDR_OVF  (more than cap records for g)
+ *   words 1..   the staircase records (elem << 32 | level << 24 | serial), as
+ *               syzsig_shard_agg_partition_dev packs them.
+ * An equal-split all-to-all of the buckets gives each owner every source's
+ * bucket for it (d_recv, same layout, bucket s from source s); the owner's
+ * flags go back the same way, one byte per word (d_flags / d_back, nshards *
+ * (cap + 1) bytes; byte 0 of a bucket is the owner's status).  Every owner sees
+ * every header, so all ranks agree without another collective that a step is
+ * void (nothing committed anywhere; redo it, with exact = 1 on a void source
+ * and a larger cap after an overflow) or which owners skipped their records
+ * (their records redone with syzsig_step_own_dev(exact = 1) and one more flags
+ * exchange, which syzsig_step_back_dev adds to the first).
+ * Reference semantics: syz-fuzzer/fuzzer.go:494-511 over the batch in global
+ * serial order; the result is the unsharded checkNewSignal's. */
+#define SYZSIG_STEP_HDR_VOID (1ull << 63)
+#define SYZSIG_STEP_HDR_OVF (1ull << 62)
+#define SYZSIG_STEP_HDR_COUNT ((1ull << 40) - 1)
+typedef struct {
+	uint64_t src_void;     /* this source's run was void: 1 = a cell spilled or a partition overflowed the LDS
+	                          table (redo with exact = 1), 2 = a call's prio is not among `levels` */
+	uint64_t global_void;  /* some bucket was void or over cap: nothing was committed on any rank */
+	uint64_t owners_void;  /* bit g: owner g skipped its records (redo them exactly); 0 when global_void */
+	uint64_t records;      /* this source's records */
+	uint64_t distinct;     /* this source's distinct elements */
+	uint64_t sent;         /* this source's staircase records (all owners) */
+	uint64_t max_out;      /* the most records this source had for one owner (the cap it needs) */
+	uint64_t received;     /* records this owner received */
+	uint64_t max_in;       /* the most records one source had for this owner */
+	uint64_t own_distinct; /* distinct elements among them */
+	uint64_t inserted;     /* elements new to this owner's shard */
+	uint64_t changed;      /* elements whose prio rose in this owner's shard */
+	uint64_t new_pairs;    /* this source's DiffRaw entries (call << 32 | elem), see syzsig_batch */
+	uint64_t own_parts;    /* LDS partitions of the owner's records (0 = exact path) */
+	double src_ms, own_ms, back_ms; /* device time of each side (0 unless timing is on) */
+} syzsig_step_status;
+/* Source side: aggregate b (zeroing call_new) and write its staircase buckets.
+ * cap >= 1; d_send has nshards * (cap + 1) words.  exact = 0: one run on
+ * capped cells that voids itself on a spill, an LDS partition overflow or a prio
+ * outside `levels` (no host round trip); exact = 1: the counted path with its
+ * HBM fallback (host round trips; a prio outside `levels` is SYZSIG_EINVAL). */
+int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base, const int8_t* levels,
+                         uint32_t nlevels, uint32_t nshards, uint64_t cap, uint64_t* d_send, int exact);
+/* Owner side: the buckets every source sent this owner (d_recv, nshards *
+ * (cap + 1) words) triaged against its shard and newSignal shard (both
+ * non-NULL); d_flags gets one byte per word.  exact = 0: records partitioned by
+ * element hash through LDS (one workgroup per partition sorts its records by
+ * element and serial and replays checkNewSignal per element); a partition
+ * over the LDS capacity makes this owner skip its records (owners_void).
+ * exact = 1: the per-record path (host round trips), for that redo.  Until
+ * syzsig_step_finish, `shard` and `new_signal` take no other call. */
+int syzsig_step_own_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set* new_signal, const uint64_t* d_recv,
+                        uint32_t nshards, uint64_t cap, const int8_t* levels, uint32_t nlevels, uint8_t* d_flags,
+                        int exact);
+/* Source side again: the owners' flags (d_back, from the flags exchange) for
+ * this source's buckets -> b->call_new, b->new_pairs (new_pairs_cap entries at
+ * most; the total in the status); b->new_bits (if set; costs one host
+ * synchronisation).  Adds to what an earlier call of the step set. */
+int syzsig_step_back_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base, const uint64_t* d_send,
+                         uint32_t nshards, uint64_t cap, const uint8_t* d_back);
+/* The step's one host synchronisation: waits for the context's stream (which
+ * the collectives' streams joined), commits the owner's table lengths and
+ * returns the status of the calls since the last finish. */
+int syzsig_step_finish(syzsig_ctx* ctx, syzsig_step_status* status);
+
 /* ---- synthetic workload (deterministic; host and device give identical data) ---- */
 typedef struct {
 	uint64_t seed;
@@ -417,6 +489,13 @@ int syzsig_synth_m0_host(const syzsig_synth_cfg* cfg, uint64_t known_sys, uint64
                          int8_t* prios);
 int syzsig_synth_m0_dev(syzsig_ctx* ctx, const syzsig_synth_cfg* cfg, uint64_t known_sys, uint64_t n,
                         uint32_t* d_elems, int8_t* d_prios);
+/* The elements i < n of that M0 which shard `shard` of `nshards` owns
+ * (owner_of), in index order, packed into d_elems/d_prios (capacity `cap`);
+ * *n_out = how many.  A rank builds its shard of a 1B-element M0 without
+ * materialising the whole. */
+int syzsig_synth_m0_shard_dev(syzsig_ctx* ctx, const syzsig_synth_cfg* cfg, uint64_t known_sys, uint64_t n,
+                              uint32_t nshards, uint32_t shard, uint32_t* d_elems, int8_t* d_prios, uint64_t cap,
+                              uint64_t* n_out);
 
 #ifdef __cplusplus
 }

@@ -20,8 +20,6 @@ SYZSIG_DEBUG_FIN_DEFER = 32
 SYZSIG_DEBUG_MIN_ATOMIC = 64
 SYZSIG_DEBUG_EXACT_CELLS = 128
 SYZSIG_DEBUG_CAP_SPILL = 256
-SYZSIG_DEBUG_RECS_SCAN = 512
-SYZSIG_DEBUG_RECS_SEL = 1024
 
 
 class SyzsigError(RuntimeError):
@@ -58,6 +56,22 @@ class BatchStats(ctypes.Structure):
         return {f[0]: (float if f[1] is ctypes.c_double else int)(getattr(self, f[0])) for f in self._fields_}
 
 
+class StepStatus(ctypes.Structure):
+    """syzsig_step_status: what syzsig_step_finish reports for one sharded step."""
+    _fields_ = [("src_void", c_uint64), ("global_void", c_uint64), ("owners_void", c_uint64), ("records", c_uint64),
+                ("distinct", c_uint64), ("sent", c_uint64), ("max_out", c_uint64), ("received", c_uint64),
+                ("max_in", c_uint64), ("own_distinct", c_uint64), ("inserted", c_uint64), ("changed", c_uint64),
+                ("new_pairs", c_uint64), ("own_parts", c_uint64), ("src_ms", ctypes.c_double),
+                ("own_ms", ctypes.c_double), ("back_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {f[0]: (float if f[1] is ctypes.c_double else int)(getattr(self, f[0])) for f in self._fields_}
+
+
+STEP_HDR_VOID = 1 << 63
+STEP_HDR_OVF = 1 << 62
+STEP_HDR_COUNT = (1 << 40) - 1
+
 _P = c_void_p
 _PP = POINTER(c_void_p)
 
@@ -80,6 +94,7 @@ SIGNATURES = {
     "syzsig_set_copy_from": (c_int, [_P, _P, _P]),
     "syzsig_set_restore_keys": (c_int, [_P, _P, _P, _P]),
     "syzsig_set_equal": (c_int, [_P, _P, _P, ctypes.POINTER(c_int)]),
+    "syzsig_set_reserve": (c_int, [_P, _P, c_uint64]),
     "syzsig_len": (c_uint64, [_P]),
     "syzsig_empty": (c_int, [_P]),
     "syzsig_capacity": (c_uint64, [_P]),
@@ -116,11 +131,17 @@ SIGNATURES = {
                                                _P, POINTER(BatchStats)]),
     "syzsig_shard_agg_unpartition_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint64, _P,
                                                  POINTER(BatchStats)]),
+    "syzsig_step_send_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint32, c_uint32, c_uint64, _P, c_int]),
+    "syzsig_step_own_dev": (c_int, [_P, _P, _P, _P, c_uint32, c_uint64, _P, c_uint32, _P, c_int]),
+    "syzsig_step_back_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint32, c_uint64, _P]),
+    "syzsig_step_finish": (c_int, [_P, POINTER(StepStatus)]),
     "syzsig_synth_default": (None, [POINTER(SynthCfg)]),
     "syzsig_synth_traces_host": (c_int, [POINTER(SynthCfg), c_uint64, c_uint64, c_uint32, _P, _P, _P, _P]),
     "syzsig_synth_traces_dev": (c_int, [_P, POINTER(SynthCfg), c_uint64, c_uint64, c_uint32, _P, _P, _P, _P]),
     "syzsig_synth_m0_host": (c_int, [POINTER(SynthCfg), c_uint64, c_uint64, _P, _P]),
     "syzsig_synth_m0_dev": (c_int, [_P, POINTER(SynthCfg), c_uint64, c_uint64, _P, _P]),
+    "syzsig_synth_m0_shard_dev": (c_int, [_P, POINTER(SynthCfg), c_uint64, c_uint64, c_uint32, c_uint32, _P, _P,
+                                          c_uint64, POINTER(c_uint64)]),
 }
 
 _lib = None

@@ -62,6 +62,7 @@ constexpr uint32_t kAggBuckets = kAggSlots / kAggBW;
 constexpr uint32_t kAggNoSlot = 0xFFFFFFFFu;
 static_assert(kAggRegion == kAggSlots, "distinct-list region per partition (internal.h)");
 constexpr uint32_t kAggLimit = kAggSlots * 4 / 5;  // distinct elements before a partition overflows
+static_assert(kAggLimit == kAggLimitRecs, "internal.h mirror");
 constexpr double kAggTargetLoad = 0.4;             // partitions are sized for this LDS load
 constexpr uint32_t kAggEmpty = 0xFFFFFFFFu;        // empty key (LDS keys are residuals < 2^29)
 constexpr uint32_t kAggNone = 0xFFFFFFFFu;         // no record at this level
@@ -81,20 +82,6 @@ constexpr uint32_t kAggGroup = SYZ_AGG_GROUP;  // cells per wave work item of k_
 #define SYZ_AGG_D 2
 #endif
 constexpr uint32_t kAggU = SYZ_AGG_U, kAggD = SYZ_AGG_D;
-
-static_assert(0x85ebca6bu * 0xa5cb9243u == 1u, "fmix32_inv multiplier");
-static_assert(0xc2b2ae35u * 0x7ed1b41du == 1u, "fmix32_inv multiplier");
-
-// murmur3 fmix32 (common.h) inverted: the records keep bits of h = fmix32(e)
-__host__ __device__ __forceinline__ uint32_t fmix32_inv(uint32_t h)
-{
-	h ^= h >> 16;
-	h *= 0x7ed1b41du;
-	h ^= (h >> 13) ^ (h >> 26);
-	h *= 0xa5cb9243u;
-	h ^= h >> 16;
-	return h;
-}
 
 // Partition geometry of one run (see the header).
 struct AggGeom {
@@ -826,13 +813,14 @@ __global__ __launch_bounds__(1024) void k_cell_plan(const uint64_t* __restrict__
 
 // The one-sync triage run's first pass, one block per chunk of calls: the
 // chunk's records (for k_cell_plan_fast), call ranges checked, whether a
-// prio outside 0..3 occurs, and call_new zeroed.  part[2 ch] = records,
+// prio outside the run's levels (0..3 for a triage run) occurs, and call_new
+// zeroed.  part[2 ch] = records,
 // part[2 ch + 1] = bad ranges | other prio << 63.
 __global__ __launch_bounds__(256) void k_fast_prep(const uint64_t* __restrict__ call_start,
                                                    const uint32_t* __restrict__ call_len,
                                                    const uint8_t* __restrict__ call_prio, uint64_t c0, uint64_t c1,
                                                    uint32_t ibits, uint64_t nrec_space, uint64_t* sizes,
-                                                   uint64_t* part, uint8_t* call_new)
+                                                   uint64_t* part, uint8_t* call_new, LevelMap lm)
 {
 	const uint64_t ch = blockIdx.x, cbeg = c0 + (ch << ibits), cend = min<uint64_t>(c1, cbeg + (1ull << ibits));
 	uint64_t tot = 0, bad = 0, other = 0;
@@ -841,7 +829,7 @@ __global__ __launch_bounds__(256) void k_fast_prep(const uint64_t* __restrict__ 
 		const uint32_t ln = call_len[c];
 		tot += ln;
 		bad += st > nrec_space || ln > nrec_space - st || ln > kSerialMask;
-		other |= call_prio[c] > 3;
+		other |= lm.lvl[call_prio[c]] == 0xff;
 		call_new[c] = 0;
 	}
 	tot = wave_sum_u64(tot);
@@ -2224,6 +2212,46 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	return SYZSIG_OK;
 }
 
+// Distinct elements per partition (top pbits of fmix32) over regions [r0, r1).
+__global__ __launch_bounds__(256) void k_part_hist(const uint32_t* __restrict__ dist_e,
+                                                   const uint32_t* __restrict__ cnt, uint32_t r0, uint32_t r1,
+                                                   uint32_t pbits, uint32_t* hist)
+{
+	for (uint32_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
+		const uint32_t n = cnt[r] == kAggOverflow ? 0 : cnt[r];
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+			atomicAdd(&hist[fmix32(dist_e[(uint64_t)r * kAggRegion + i]) >> (32 - pbits)], 1u);
+	}
+}
+
+// The finalize probes a partition's elements from its own slice of a table
+// (home buckets = the top bits of the same h).  The HBM fallback's partitions
+// hold more than kAggLimit distinct elements, possibly many more when the
+// elements are not spread by the hash: their slice must take them at most 3/4
+// full, or their probe sequences pile up past the probe limit.  Grows s so
+// that every such partition's slice does.  Synchronises.
+static int reserve_slices(syzsig_ctx* ctx, syzsig_set* s, const uint32_t* dist_e, const uint32_t* d_cnt, uint32_t r0,
+                          uint32_t r1, uint32_t pbits)
+{
+	if (!s || r1 <= r0)
+		return SYZSIG_OK;
+	const uint32_t P = 1u << pbits;
+	void* wh;
+	SYZ_TRY(ws_get(ctx, 53, (uint64_t)P * 4 + 64, &wh));
+	const hipStream_t st = ctx->stream;
+	SYZ_HIP(hipMemsetAsync(wh, 0, (uint64_t)P * 4, st));
+	k_part_hist<<<std::min<uint32_t>(r1 - r0, 2048), 256, 0, st>>>(dist_e, d_cnt, r0, r1, pbits, (uint32_t*)wh);
+	SYZ_HIP(hipGetLastError());
+	std::vector<uint32_t> h(P);
+	SYZ_HIP(hipMemcpyAsync(h.data(), wh, (uint64_t)P * 4, hipMemcpyDeviceToHost, st));
+	SYZ_HIP(hipStreamSynchronize(st));
+	const uint64_t mx = *std::max_element(h.begin(), h.end());
+	const uint64_t need = pow2_at_least((uint64_t)((double)P * (double)mx / (kBucketSlots * kMaxLoad)) + 1);
+	if (need > s->nbuckets)
+		SYZ_TRY(set_rehash(s, need, false));
+	return SYZSIG_OK;
+}
+
 // One triage run with one host synchronisation at the end ("the
 // one-sync triage run"): scatter into capped cells, k_agg, the slice-exclusive
 // finalize and the deferred lists.  maxSignal and newSignal are reserved for
@@ -2305,7 +2333,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		SYZ_TRY(ws_get(ctx, 54, nchunks * 16 + 64, &dpart));
 		ovf = (uint32_t*)&ctx->d_cnt[kCntSpill];
 		k_fast_prep<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_start, b->call_len, b->call_prio, c0, c1, g.ibits, b->nrec,
-		                                              sizes, (uint64_t*)dpart, b->call_new);
+		                                              sizes, (uint64_t*)dpart, b->call_new, lm);
 		k_cell_plan_fast<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap, (const uint64_t*)dpart, run_recs,
 		                                    *npairs_io, ctx->d_cnt);
 	} else {
@@ -2409,12 +2437,13 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		return SYZSIG_OK;
 	}
 	if (ctx->h_cnt[kCntOverflow])
-		return fail(SYZSIG_EIO, "triage: table overflow after reserve (internal error)");
+		return fail(SYZSIG_EIO, "triage: table overflow after reserve (internal error; one-sync run)");
 	uint64_t D = ctx->h_cnt[kCntDistinct];
 	uint64_t inserted = ctx->h_cnt[kCntInserted], changed = ctx->h_cnt[kCntChanged], ns_ins = ctx->h_cnt[kCntAux];
+	uint64_t inserted_done = 0;  // already added to maxSignal's length
 	uint64_t npairs = ctx->h_cnt[kCntAux2];
 	const uint64_t novf = ctx->h_cnt[kCntAggOvf];
-	if (ctx->agg_variant != 7 && novf > gate) {
+	if (novf > gate) {
 		// too few partitions (the distinct-ratio guess was low): nothing was
 		// committed; the next attempt sizes them for at least what was seen
 		// (an overflowed partition held more than kAggLimit)
@@ -2433,7 +2462,12 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	if (novf) {
 		// partitions past the LDS table: aggregated in HBM from their cells,
 		// then finalized with the atomic code (their elements are disjoint from
-		// every committed partition's)
+		// every committed partition's).  The committed partitions' inserts count
+		// first: the reservations below start from the tables' true lengths.
+		ms->len += inserted;
+		nsp->len += ns_ins;
+		inserted_done += inserted;
+		inserted = ns_ins = 0;
 		std::vector<uint32_t> hc(P);
 		SYZ_HIP(hipMemcpy(hc.data(), dc, P * 4, hipMemcpyDeviceToHost));
 		std::vector<uint32_t> ovl;
@@ -2477,10 +2511,25 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 			// distinct each); these elements come on top
 			SYZ_TRY(set_reserve(ms, gcnt));
 			SYZ_TRY(set_reserve_load(nsp, gcnt, kHardLoad));
-			SYZ_TRY(ws_grow_keep(ctx, 15, (npairs + 4 * gcnt) * 8 + 64, npairs * 8, &pr));
-			*pairs_out = (uint64_t*)pr;
 			SYZ_TRY(ws_get(ctx, 35, rc.size() * 4 + 64, &dc2));
 			SYZ_HIP(hipMemcpyAsync(dc2, rc.data(), rc.size() * 4, hipMemcpyHostToDevice, s));
+			SYZ_TRY(reserve_slices(ctx, ms, (const uint32_t*)de2, (const uint32_t*)dc2, 0, (uint32_t)rc.size(), pb));
+			SYZ_TRY(reserve_slices(ctx, nsp, (const uint32_t*)de2, (const uint32_t*)dc2, 0, (uint32_t)rc.size(), pb));
+			if (pr == b->new_pairs) {
+				// the run wrote its pairs straight into the caller's buffer: keep
+				// appending there while it has room, else move them to workspace
+				// 15 first (ws_grow_keep keeps only what that workspace held)
+				if (b->new_pairs_cap < npairs + 4 * gcnt) {
+					void* w;
+					SYZ_TRY(ws_get(ctx, 15, (npairs + 4 * gcnt) * 8 + 64, &w));
+					if (npairs)
+						SYZ_HIP(hipMemcpyAsync(w, pr, npairs * 8, hipMemcpyDeviceToDevice, s));
+					pr = w;
+				}
+			} else {
+				SYZ_TRY(ws_grow_keep(ctx, 15, (npairs + 4 * gcnt) * 8 + 64, npairs * 8, &pr));
+			}
+			*pairs_out = (uint64_t*)pr;
 			SYZ_TRY(counters_reset(ctx));
 			memcpy(ctx->h_pin + kPinPairs, &npairs, 8);
 			SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], ctx->h_pin + kPinPairs, 8, hipMemcpyHostToDevice, s));
@@ -2491,7 +2540,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 			SYZ_HIP(hipGetLastError());
 			SYZ_TRY(counters_fetch(ctx));  // (synchronizes: rc is consumed)
 			if (ctx->h_cnt[kCntOverflow])
-				return fail(SYZSIG_EIO, "triage: table overflow after reserve (internal error)");
+				return fail(SYZSIG_EIO, "triage: table overflow after reserve (internal error; one-sync run, HBM partitions)");
 			inserted += ctx->h_cnt[kCntInserted];
 			changed += ctx->h_cnt[kCntChanged];
 			ns_ins += ctx->h_cnt[kCntAux];
@@ -2507,6 +2556,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	ms->len += inserted;
 	if (nsp)
 		nsp->len += ns_ins;
+	inserted += inserted_done;
 	st->distinct += D;
 	st->parts = P;
 	st->survivors += D;
@@ -2557,6 +2607,11 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 	// probe chains stay short in the finalize (0.34 -> 0.28 ms at C2)
 	if (D)
 		SYZ_TRY(set_reserve_load(*ns, D, kTargetLoad));
+	if (a.nregions > a.parts) {  // the HBM fallback's partitions: room in their slices
+		const uint32_t pb = 31 - __builtin_clz(a.parts);
+		SYZ_TRY(reserve_slices(ctx, ms, a.dist_e, a.cnt, a.parts, a.nregions, pb));
+		SYZ_TRY(reserve_slices(ctx, *ns, a.dist_e, a.cnt, a.parts, a.nregions, pb));
+	}
 	const uint64_t need_pairs = *npairs_io + 4 * D;
 	SYZ_TRY(ws_grow_keep(ctx, 15, need_pairs * 8 + 64, *npairs_io * 8, &pr));
 	*pairs_out = (uint64_t*)pr;
@@ -2579,9 +2634,7 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 		SYZ_TRY(ws_get(ctx, 33, D * 8 + 64, &dn));
 		uint32_t* def_e = (uint32_t*)dd;
 		uint4* def_f = (uint4*)((char*)dd + ((D * 4 + 15) & ~15ull));
-		auto fin = ctx->agg_variant == 4 ? k_agg_finalize_x<4> : ctx->agg_variant == 5 ? k_agg_finalize_x<1>
-		                                                                                : k_agg_finalize_x<2>;
-		fin<<<a.nregions, kFxThreads, 0, s>>>(
+		k_agg_finalize_x<2><<<a.nregions, kFxThreads, 0, s>>>(
 		    a.dist_e, a.dist_f, a.cnt, a.nregions, lm, c0, ms->slots, ms->nbuckets - 1, ms_shift, nsp->slots,
 		    nsp->nbuckets - 1, ns_shift, b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2], ctx->d_cnt, def_e, def_f,
 		    &ctx->d_cnt[kCntDefer], (uint64_t*)dn, &ctx->d_cnt[kCntDeferNs], ctx->agg_dbg, nullptr, nullptr, 0);
@@ -2605,7 +2658,7 @@ int agg_triage_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const syzsi
 		st->decide_ms += t;
 	}
 	if (ctx->h_cnt[kCntOverflow])
-		return fail(SYZSIG_EIO, "triage: table overflow after reserve (internal error)");
+		return fail(SYZSIG_EIO, "triage: table overflow after reserve (internal error; planned run)");
 	if (fresh_ns && ctx->h_cnt[kCntChanged] == 0) {
 		syzsig_set_free(*ns);
 		*ns = nullptr;
@@ -2819,11 +2872,274 @@ __global__ __launch_bounds__(256) void k_stair_back(const uint64_t* __restrict__
 	}
 }
 
+// ---- the stream-ordered step's source side (syzsig_step_send_dev / _back_dev)
+// Staircase records into fixed buckets: owner g's at send[g * (cap + 1) + 1 ...],
+// cursor[g] = its true count (records past cap are counted, not written).
+// Nothing is written when the run is void (gate: its spill flag or an LDS
+// partition overflow).
+__global__ __launch_bounds__(256) void k_stair_bucket(const uint32_t* __restrict__ dist_e,
+                                                      const uint4* __restrict__ dist_f,
+                                                      const uint32_t* __restrict__ cnt, uint32_t nregions,
+                                                      uint32_t nlev, uint32_t nshards, uint64_t serial_base,
+                                                      uint64_t cap, unsigned long long* cursor, uint64_t* send,
+                                                      const unsigned long long* gate)
+{
+	__shared__ uint32_t h[kMaxShardsAgg];
+	__shared__ unsigned long long base[kMaxShardsAgg];
+	if (gate[kCntSpill] || gate[kCntAggOvf])
+		return;
+	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
+		if (threadIdx.x < kMaxShardsAgg)
+			h[threadIdx.x] = 0;
+		__syncthreads();
+		const uint32_t n = cnt[r] == kAggOverflow ? 0 : cnt[r];
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+			const uint64_t o = (uint64_t)r * kAggRegion + i;
+			const uint32_t m = stair_levels(dist_f[o], nlev);
+			if (m)
+				atomicAdd(&h[owner_of(dist_e[o], nshards)], (uint32_t)__popc(m));
+		}
+		__syncthreads();
+		if (threadIdx.x < nshards) {
+			base[threadIdx.x] = h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)h[threadIdx.x]) : 0;
+			h[threadIdx.x] = 0;
+		}
+		__syncthreads();
+		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+			const uint64_t o = (uint64_t)r * kAggRegion + i;
+			const uint4 f4 = dist_f[o];
+			const uint32_t m = stair_levels(f4, nlev);
+			if (!m)
+				continue;
+			const uint32_t e = dist_e[o], g = owner_of(e, nshards);
+			const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
+			uint64_t pos = base[g] + atomicAdd(&h[g], (uint32_t)__popc(m));
+			uint64_t* bk = send + (uint64_t)g * (cap + 1) + 1;
+#pragma unroll
+			for (uint32_t l = 0; l < 4; l++)
+				if ((m >> l) & 1) {
+					if (pos < cap)
+						bk[pos] = ((uint64_t)e << 32) | ((uint64_t)l << 24) | ((serial_base + f[l]) & kSerialMask);
+					pos++;
+				}
+		}
+		__syncthreads();
+	}
+}
+
+// bucket headers; the source's sent records and its largest bucket
+__global__ void k_stair_heads(const unsigned long long* __restrict__ cursor, uint32_t nshards, uint64_t cap,
+                              uint64_t* send, unsigned long long* sc)
+{
+	if (threadIdx.x != 0)
+		return;
+	const bool vd = sc[kCntSpill] != 0 || sc[kCntAggOvf] != 0;
+	uint64_t tot = 0, mx = 0;
+	for (uint32_t g = 0; g < nshards; g++) {
+		const uint64_t c = vd ? 0 : cursor[g];
+		tot += c;
+		mx = max(mx, c);
+	}
+	// an overflow toward any owner is flagged to every owner, so that all of
+	// them skip the step alike
+	for (uint32_t g = 0; g < nshards; g++) {
+		const uint64_t c = vd ? 0 : cursor[g];
+		send[(uint64_t)g * (cap + 1)] = (c & SYZSIG_STEP_HDR_COUNT) | (vd ? SYZSIG_STEP_HDR_VOID : 0) |
+		                                (mx > cap ? SYZSIG_STEP_HDR_OVF : 0);
+	}
+	sc[kCntCandidates] = tot;
+	sc[kCntTouched] = mx;
+}
+
+// The owners' flags back at the source (blockIdx.y = owner g): the owner's
+// status byte (1: the step is void, 2: the owner skipped) and, when 0, every
+// flagged record of bucket g as the pair (call = serial - serial_base, e).
+__global__ __launch_bounds__(256) void k_step_back(const uint64_t* __restrict__ send, const uint8_t* __restrict__ back,
+                                                   uint64_t cap, uint64_t serial_base, uint8_t* call_new,
+                                                   uint64_t* pairs, uint64_t pairs_cap, unsigned long long* bc)
+{
+	const uint32_t g = blockIdx.y, lane = lane_id();
+	const uint64_t s0 = (uint64_t)g * (cap + 1);
+	const uint8_t st = back[s0];
+	if (st) {
+		if (blockIdx.x == 0 && threadIdx.x == 0) {
+			if (st == 1)
+				atomicOr(&bc[kCntError], 1ull);
+			else
+				atomicOr(&bc[kCntAux], 1ull << g);
+		}
+		return;
+	}
+	const uint64_t n = min<uint64_t>(send[s0] & SYZSIG_STEP_HDR_COUNT, cap);
+	for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += (uint64_t)gridDim.x * blockDim.x) {
+		const uint64_t i = i0 + threadIdx.x;
+		const bool on = i < n && back[s0 + 1 + i];
+		uint64_t v = 0;
+		if (on) {
+			const uint64_t r = send[s0 + 1 + i];
+			const uint64_t c = (r & kSerialMask) - serial_base;
+			call_new[c] = 1;
+			v = (c << 32) | (r >> 32);
+		}
+		const uint64_t m = __ballot(on);
+		unsigned long long wb = 0;
+		if (lane == 0 && m)
+			wb = atomicAdd(&bc[kCntAux2], (unsigned long long)__popcll(m));
+		wb = __shfl(wb, 0, 64);
+		if (on && pairs && wb + lane_rank(m) < pairs_cap)
+			pairs[wb + lane_rank(m)] = v;
+	}
+}
+
 }  // namespace syz
 
 using namespace syz;
 
 extern "C" {
+
+int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base, const int8_t* levels,
+                         uint32_t nlevels, uint32_t nshards, uint64_t cap, uint64_t* d_send, int exact)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !b || !d_send || (b->nrec && !b->sigs) ||
+	    (b->ncalls && (!b->call_start || !b->call_len || !b->call_prio || !b->call_new)))
+		return fail(SYZSIG_EINVAL, "step_send: NULL argument");
+	if (nshards == 0 || nshards > kMaxShardsAgg || cap == 0 || cap > SYZSIG_STEP_HDR_COUNT)
+		return fail(SYZSIG_EINVAL, "step_send: need 1 <= nshards <= 64 and 1 <= cap < 2^40");
+	if (b->nrec >= (1ull << 32))
+		return fail(SYZSIG_ERANGE, "step_send: >= 2^32 records per GPU");
+	if (serial_base + b->ncalls > kSerialMask + 1ull)
+		return fail(SYZSIG_ERANGE, "step_send: batch serial order exceeds 2^24 calls");
+	LevelMap lm;
+	SYZ_TRY(level_map_from_levels(levels, nlevels, &lm));
+	const hipStream_t s = ctx->stream;
+	unsigned long long* sc = ctx->d_step + kStepSrc;
+	void* wcur;
+	SYZ_TRY(ws_get(ctx, 63, kMaxShardsAgg * 8 + 64, &wcur));
+	unsigned long long* cursor = (unsigned long long*)wcur;
+	ctx->step_src_timed = ctx->timing;
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev_step[0], s));
+	// the flags-back counters start the step; the source counters are zeroed
+	// below (or by k_cell_plan_fast)
+	SYZ_HIP(hipMemsetAsync(ctx->d_step + kStepBack, 0, kNumCounters * 8, s));
+	SYZ_HIP(hipMemsetAsync(cursor, 0, kMaxShardsAgg * 8, s));
+	if (b->new_bits)
+		SYZ_HIP(hipMemsetAsync(b->new_bits, 0, ((b->nrec + 31) / 32) * 4, s));
+	const bool fast = !exact && ctx->cap_sd > 0 && !ctx->agg_counted_once && b->ncalls && b->nrec &&
+	                  !(ctx->agg_dbg & (SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL));
+	if (fast) {
+		// one capped-cell run with its assumptions checked on device (as the
+		// one-sync triage run): prios among `levels`, valid ranges, <= nrec records
+		AggGeom g = agg_geom_for(ctx, b->nrec, 0);
+		g.ibits = g.cbits();
+		const uint32_t S = 1u << g.pbits, P = S;
+		const uint64_t nchunks = (b->ncalls + (1ull << g.ibits) - 1) >> g.ibits;
+		const float sd = ctx->cap_sd;
+		ctx->step_src_parts = P;
+		const uint64_t bound = b->nrec + b->nrec / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
+		void *recs, *cm, *dc, *de, *df, *dpart;
+		SYZ_TRY(ws_get(ctx, 16, (bound + kDummyLines * kBlk) * 4, &recs));
+		SYZ_TRY(ws_get(ctx, 17, nchunks * 20 + (uint64_t)S * nchunks * 4 + 256, &cm));
+		SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
+		SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
+		SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
+		SYZ_TRY(ws_get(ctx, 54, nchunks * 16 + 64, &dpart));
+		uint64_t* sizes = (uint64_t*)cm;
+		uint64_t* cbase = sizes + nchunks;
+		uint32_t* ccap = (uint32_t*)(cbase + nchunks);
+		uint32_t* ccnt = ccap + nchunks;
+		uint32_t* ovf = (uint32_t*)&sc[kCntSpill];
+		k_fast_prep<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_start, b->call_len, b->call_prio, 0, b->ncalls, g.ibits,
+		                                              b->nrec, sizes, (uint64_t*)dpart, b->call_new, lm);
+		k_cell_plan_fast<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap, (const uint64_t*)dpart, b->nrec, 0, sc);
+		const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
+		k_agg_scatter_blk<false><<<(int)std::min<uint64_t>(nchunks, 2048), kAggThreads, 0, s>>>(
+		    b->sigs, b->call_start, b->call_len, b->call_prio, lm, 0, b->ncalls, g, AggSrc{nullptr, 1, 0, 0}, cc,
+		    (uint32_t*)recs, ctx->agg_dbg >> 10);
+		const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),
+		                  ovf, sc};
+		k_agg<kAggU, kAggD, true><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+		k_stair_bucket<<<(int)std::min<uint32_t>(P, 2048), 256, 0, s>>>(
+		    (const uint32_t*)de, (const uint4*)df, (const uint32_t*)dc, P, lm.n, nshards, serial_base, cap, cursor,
+		    d_send, sc);
+		SYZ_HIP(hipGetLastError());
+	} else {
+		// the exact path: validated, counted cells, the HBM fallback (host round trips)
+		unsigned long long* hs = ctx->h_step + kStepSrc;
+		memset(hs, 0, kNumCounters * 8);
+		if (b->ncalls)
+			SYZ_HIP(hipMemsetAsync(b->call_new, 0, b->ncalls, s));
+		if (b->ncalls && b->nrec) {
+			uint64_t total = 0;
+			uint32_t mask[8];
+			SYZ_TRY(batch_total_records(ctx, b, &total, mask));
+			for (int p = 0; p < 256; p++)
+				if (((mask[p >> 5] >> (p & 31)) & 1) && lm.lvl[p] == 0xff)
+					return fail(SYZSIG_EINVAL, "step_send: a call's prio is not among `levels`");
+			hs[kCntRecords] = total;
+			if (total) {
+				syzsig_batch_stats st;
+				memset(&st, 0, sizeof(st));
+				AggOut a;
+				SYZ_TRY(agg_aggregate(ctx, b, 0, b->ncalls, lm, total, &st, &a));
+				hs[kCntDistinct] = a.D;
+				SYZ_HIP(hipMemcpyAsync(sc, hs, kNumCounters * 8, hipMemcpyHostToDevice, s));
+				k_stair_bucket<<<(int)std::min<uint32_t>(a.nregions, 2048), 256, 0, s>>>(
+				    a.dist_e, a.dist_f, a.cnt, a.nregions, lm.n, nshards, serial_base, cap, cursor, d_send, sc);
+				SYZ_HIP(hipGetLastError());
+			}
+		}
+		SYZ_HIP(hipMemcpyAsync(sc, hs, kNumCounters * 8, hipMemcpyHostToDevice, s));
+		SYZ_HIP(hipStreamSynchronize(s));  // hs is consumed
+	}
+	k_stair_heads<<<1, 64, 0, s>>>(cursor, nshards, cap, d_send, sc);
+	SYZ_HIP(hipGetLastError());
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev_step[1], s));
+	return SYZSIG_OK;
+}
+
+int syzsig_step_back_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base, const uint64_t* d_send,
+                         uint32_t nshards, uint64_t cap, const uint8_t* d_back)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !b || !d_send || !d_back || (b->ncalls && !b->call_new) || (b->new_pairs_cap && !b->new_pairs))
+		return fail(SYZSIG_EINVAL, "step_back: NULL argument");
+	if (nshards == 0 || nshards > kMaxShardsAgg || cap == 0 || cap > SYZSIG_STEP_HDR_COUNT)
+		return fail(SYZSIG_EINVAL, "step_back: need 1 <= nshards <= 64 and 1 <= cap < 2^40");
+	const hipStream_t s = ctx->stream;
+	unsigned long long* bc = ctx->d_step + kStepBack;
+	ctx->step_back_timed = ctx->timing;
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev_step[4], s));
+	const dim3 grid(grid_for(cap, 256, std::max(1, 2048 / (int)nshards)), nshards);
+	if (!b->new_bits) {
+		k_step_back<<<grid, 256, 0, s>>>(d_send, d_back, cap, serial_base, b->call_new, b->new_pairs,
+		                                 b->new_pairs ? b->new_pairs_cap : 0, bc);
+		SYZ_HIP(hipGetLastError());
+	} else {
+		// per-record bits need the pairs' count on the host: this call synchronises
+		unsigned long long* hb = ctx->h_step + kStepBack;
+		SYZ_HIP(hipMemcpyAsync(hb, bc, kNumCounters * 8, hipMemcpyDeviceToHost, s));
+		SYZ_HIP(hipStreamSynchronize(s));
+		const uint64_t np0 = hb[kCntAux2], bound = np0 + (uint64_t)nshards * cap;
+		void* wp;
+		SYZ_TRY(ws_grow_keep(ctx, 55, bound * 8 + 64, np0 * 8, &wp));
+		k_step_back<<<grid, 256, 0, s>>>(d_send, d_back, cap, serial_base, b->call_new, (uint64_t*)wp, bound, bc);
+		SYZ_HIP(hipGetLastError());
+		SYZ_HIP(hipMemcpyAsync(hb, bc, kNumCounters * 8, hipMemcpyDeviceToHost, s));
+		SYZ_HIP(hipStreamSynchronize(s));
+		const uint64_t np1 = hb[kCntAux2];
+		SYZ_TRY(agg_mark_bits(ctx, b, 0, b->ncalls, (const uint64_t*)wp, np0, np1));
+		if (b->new_pairs && np1 > np0 && np0 < b->new_pairs_cap)
+			SYZ_HIP(hipMemcpyAsync(b->new_pairs + np0, (const uint64_t*)wp + np0,
+			                       (std::min(np1, b->new_pairs_cap) - np0) * 8, hipMemcpyDeviceToDevice, s));
+	}
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev_step[5], s));
+	return SYZSIG_OK;
+}
 
 int syzsig_shard_agg_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
                                    const int8_t* levels, uint32_t nlevels, uint32_t nshards, uint64_t* d_send,

@@ -60,6 +60,20 @@ SYZ_HD uint32_t fmix32(uint32_t h)
 	return h;
 }
 
+// fmix32 inverted (a bijection of u32): records that keep bits of h = fmix32(e)
+// recover e from them (agg.hip, recs.hip).
+SYZ_HD uint32_t fmix32_inv(uint32_t h)
+{
+	h ^= h >> 16;
+	h *= 0x7ed1b41du;  // 0xc2b2ae35^-1 mod 2^32
+	h ^= (h >> 13) ^ (h >> 26);
+	h *= 0xa5cb9243u;  // 0x85ebca6b^-1 mod 2^32
+	h ^= h >> 16;
+	return h;
+}
+static_assert(0x85ebca6bu * 0xa5cb9243u == 1u, "fmix32_inv multiplier");
+static_assert(0xc2b2ae35u * 0x7ed1b41du == 1u, "fmix32_inv multiplier");
+
 // Owner shard of an element in an N-way hash-partitioned maxSignal.  Independent
 // of fmix32 (different multiplier/offset), so slots stay uniform inside a shard.
 SYZ_HD uint32_t owner_of(uint32_t e, uint32_t nshards)

@@ -61,6 +61,8 @@ enum Counter : int {
 	kCntRecords,        // one-sync triage run: the batch's records
 	kNumCounters = 16,
 };
+// the sharded step's counter blocks in syzsig_ctx::d_step
+constexpr int kStepSrc = 0, kStepOwn = 16, kStepBack = 32, kStepCounters = 48;
 
 struct Workspace {
 	void* ptr = nullptr;
@@ -69,8 +71,7 @@ struct Workspace {
 
 // the debug flags that change only the path taken, never a result
 constexpr uint32_t kDebugResultPreserving =
-    SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL |
-    SYZSIG_DEBUG_RECS_SCAN | SYZSIG_DEBUG_RECS_SEL;
+    SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL;
 
 // capped cells of the aggregation path (agg.hip): default slack, in standard deviations
 constexpr float kCapSdDefault = 6.0f;
@@ -97,9 +98,10 @@ struct syzsig_ctx {
 	char* h_pin = nullptr;
 	// grow-only scratch buffers by role (35: the one-sync run's fallback): 0-2 set ops, 3-6 triage candidates and
 	// small state, 7-10 host uploads of minimize, 11-14 triage partitions and
-	// minimize internals and triage pairs (13-15), 16-23 + 30-31 triage aggregation,
+	// minimize internals and triage pairs (13-15), 16-23 + 30-31 triage aggregation, 55-63 the sharded step and
+	// the LDS records path,
 	// 24-29 check_new_signal uploads, 32-33 the finalize's deferred lists, 40-47 manager poll
-	syz::Workspace ws[56];
+	syz::Workspace ws[64];
 	bool timing = false;                  // HIP events around triage kernels
 	// tuning knobs (defaults; SYZSIG_* environment overrides read at ctx creation)
 	int part_mode = 1;                    // 0 = never use the aggregation path (agg.hip)
@@ -109,10 +111,19 @@ struct syzsig_ctx {
 	float cap_sd_entry = syz::kCapSdDefault;  // the same for Minimize's runs
 	bool agg_counted_once = false;        // the next agg_aggregate takes counted cells (a one-sync run spilled)
 	uint32_t edge_waves = 4;              // waves per program of k_edge_dedup (4 or 8; SYZSIG_EDGE_WAVES)
-	uint32_t agg_variant = 0;             // k_agg pipeline variant (SYZSIG_AGG_VARIANT; tuning)
 	uint32_t agg_dbg = 0;                 // SYZSIG_DEBUG_* path flags; timing-only bits need -DSYZ_EXPERIMENTS
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	double last_ms = 0;                   // device time of the last timed entry point's kernels
+	// the stream-ordered sharded step (syzsig_step_*): its counters, read once by
+	// syzsig_step_finish -- [0,16) source, [16,32) owner, [32,48) flags back
+	unsigned long long* d_step = nullptr;
+	unsigned long long* h_step = nullptr;  // pinned mirror
+	syzsig_set* step_ms = nullptr;         // the owner's shard and newSignal until finish
+	syzsig_set* step_ns = nullptr;
+	uint64_t step_parts = 0;
+	uint64_t step_src_parts = 1;           // the source run's aggregation partitions
+	bool step_own_timed = false, step_src_timed = false, step_back_timed = false;
+	hipEvent_t ev_step[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 struct syzsig_set {
@@ -124,6 +135,7 @@ struct syzsig_set {
 	uint32_t* firsts = nullptr;  // 4 per slot: epoch_rev << 24 | serial, per prio level
 	uint32_t* touched = nullptr; // 1 bit per slot
 	uint32_t epoch = 0;          // current epoch_rev (counts down 254..1)
+	bool step_busy = false;      // an owner step is in flight on it (len not final until syzsig_step_finish)
 	uint64_t nslots() const { return nbuckets * syz::kBucketSlots; }
 };
 
@@ -173,6 +185,7 @@ int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm);
 
 // aggregation path (agg.hip)
 constexpr uint32_t kAggRegion = 7424;  // distinct-list region per partition (= LDS slots of k_agg)
+constexpr uint32_t kAggLimitRecs = kAggRegion * 4 / 5;  // distinct elements an LDS partition holds (agg.hip kAggLimit)
 struct AggOut {
 	const uint32_t* dist_e;  // distinct elements; region r at [r * kAggRegion, + cnt[r])
 	const uint4* dist_f;     // their first serial per level (0xFFFFFFFF = none)
@@ -206,6 +219,18 @@ int agg_triage_optimistic(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, cons
                           syzsig_batch_stats* st, uint64_t** pairs, uint64_t* npairs, bool* done);
 int agg_mark_bits(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t c1, const uint64_t* pairs,
                   uint64_t p0, uint64_t p1);
+// records mode (triage.hip: the per-record path, and the entry; recs.hip: the LDS path)
+int triage_records_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t nrec,
+                        const int8_t* levels, uint32_t nlevels, uint8_t* new_flags, syzsig_batch_stats* st,
+                        bool allow_lds = true);
+// *done = false: the LDS path voided itself (nothing committed), take the per-record path
+int rp_triage_records(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t nrec,
+                      const LevelMap& lm, uint8_t* new_flags, syzsig_batch_stats* st, bool* done);
+// a set an owner step holds until syzsig_step_finish takes no other call
+inline int set_check_idle(const syzsig_set* s)
+{
+	return s && s->step_busy ? fail(SYZSIG_EINVAL, "set is held by a sharded step until syzsig_step_finish") : 0;
+}
 int pairs_from_bits(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* bits, uint64_t c0, uint64_t c1,
                     uint64_t bound, uint64_t** pairs, uint64_t* npairs);
 

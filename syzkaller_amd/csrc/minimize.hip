@@ -260,6 +260,77 @@ __global__ __launch_bounds__(256) void k_min_split_scatter(const uint32_t* __res
 	}
 }
 
+// The split's atomic fallback (more than 4 distinct prios in the part, or a
+// context of >= 2^24 entries): one wave per rank r of the part, every entry's
+// record atomicMax'ed into a table keyed by element -- the slot word is the
+// winner record min_winner builds, argmax (prio, -rank)
+__global__ __launch_bounds__(256) void k_min_cover_ranks(uint64_t* slots, uint64_t bmask,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ elems,
+                                                         const int8_t* __restrict__ prios,
+                                                         const uint32_t* __restrict__ order, uint64_t r_lo,
+                                                         uint64_t n, unsigned long long* cnt)
+{
+	const uint32_t lane = lane_id();
+	const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+	const uint64_t maxp = max_probe_for(bmask);
+	uint64_t ovf = 0;
+	for (uint64_t i = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nwaves) {
+		const uint32_t c = order[r_lo + i];
+		const uint32_t low_rank = 0xFFFFFFu - (uint32_t)(r_lo + i);
+		for (uint64_t j = off[c] + lane; j < off[c + 1]; j += 64) {
+			const uint32_t e = elems[j];
+			const uint64_t v = ((uint64_t)e << 32) | ((uint64_t)prio_biased(prios[j]) << 24) | low_rank;
+			uint64_t old;
+			const int64_t s = tbl_find_or_insert(slots, bmask, e, v, old, maxp);
+			if (s < 0)
+				ovf++;
+			else if (old != 0 && old < v)
+				atomicMax(reinterpret_cast<unsigned long long*>(slots + s), (unsigned long long)v);
+		}
+	}
+	block_count(&cnt[kCntOverflow], ovf);
+}
+
+// the fallback table's records per owner, then -> send[] grouped by owner
+__global__ __launch_bounds__(256) void k_min_split_tbl(const uint64_t* __restrict__ slots, uint64_t nslots,
+                                                       uint32_t nshards, unsigned long long* counts,
+                                                       unsigned long long* cursor, uint64_t* send)
+{
+	__shared__ uint32_t h[kMinMaxShards];
+	__shared__ unsigned long long base[kMinMaxShards];
+	const uint64_t per = (nslots + gridDim.x - 1) / gridDim.x;
+	const uint64_t s0 = blockIdx.x * per, s1 = min<uint64_t>(nslots, s0 + per);
+	if (threadIdx.x < kMinMaxShards)
+		h[threadIdx.x] = 0;
+	__syncthreads();
+	for (uint64_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
+		const uint64_t v = slots[i];
+		if (v != kSlotEmpty)
+			atomicAdd(&h[owner_of((uint32_t)(v >> 32), nshards)], 1u);
+	}
+	__syncthreads();
+	if (threadIdx.x < nshards) {
+		if (!send) {
+			if (h[threadIdx.x])
+				atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+		} else {
+			base[threadIdx.x] = h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)h[threadIdx.x]) : 0;
+		}
+		h[threadIdx.x] = 0;
+	}
+	__syncthreads();
+	if (!send)
+		return;
+	for (uint64_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
+		const uint64_t v = slots[i];
+		if (v == kSlotEmpty)
+			continue;
+		const uint32_t g = owner_of((uint32_t)(v >> 32), nshards);
+		send[base[g] + atomicAdd(&h[g], 1u)] = v;
+	}
+}
+
 // owner side: the max winner record per element (the slot word IS the record:
 // key e in the top 32 bits, never 0 because rank < 2^24 - 1)
 __global__ void k_min_resolve(uint64_t* slots, uint64_t bmask, const uint64_t* __restrict__ recs, uint64_t n,
@@ -470,17 +541,63 @@ int syzsig_minimize_split_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint
 	uint32_t* hmask = (uint32_t*)(ctx->h_pin + kPinMask);
 	SYZ_HIP(hipMemcpyAsync(hmask, dmask, 32, hipMemcpyDeviceToHost, st));
 	SYZ_TRY(counters_fetch(ctx));
-	if (ctx->h_cnt[kCntAux])
-		return fail(SYZSIG_ERANGE, "minimize_split: a context of >= 2^24 entries");
 	int8_t levels[4];
 	uint32_t nl = 0;
-	for (int v = -128; v <= 127; v++) {
+	bool atomic_path = ctx->h_cnt[kCntAux] != 0 || (ctx->agg_dbg & SYZSIG_DEBUG_MIN_ATOMIC);
+	for (int v = -128; v <= 127 && !atomic_path; v++) {
 		const uint8_t u = (uint8_t)(int8_t)v;
 		if ((hmask[u >> 5] >> (u & 31)) & 1) {
 			if (nl == 4)
-				return fail(SYZSIG_ERANGE, "minimize_split: more than 4 distinct prios in a part");
-			levels[nl++] = (int8_t)v;
+				atomic_path = true;  // the records carry 2 level bits
+			else
+				levels[nl++] = (int8_t)v;
 		}
+	}
+	if (atomic_path) {
+		// a context of >= 2^24 entries or more than 4 prios: any int8 prio is a
+		// valid DiffRaw/Minimize prio (signal.go:138-166), so the part's winners
+		// come from the per-entry atomicMax table instead of failing
+		syzsig_set* t = nullptr;
+		SYZ_TRY(set_alloc(ctx, buckets_for(local), &t));
+		void* dcur;
+		int rc = ws_get(ctx, 36, 2 * kMinMaxShards * 8, &dcur);
+		unsigned long long* counts = (unsigned long long*)dcur;
+		unsigned long long* cursor = counts + kMinMaxShards;
+		unsigned long long h[kMinMaxShards] = {};
+		const int tg = (int)std::min<uint64_t>(std::max<uint64_t>(t->nslots() / 4096, 1), 4096);
+		if (rc == SYZSIG_OK)
+			rc = counters_reset(ctx);
+		if (rc == SYZSIG_OK) {
+			(void)hipMemsetAsync(counts, 0, kMinMaxShards * 8, st);
+			k_min_cover_ranks<<<grid_for(n * 64, 256, 8192), 256, 0, st>>>(t->slots, t->nbuckets - 1, d_off, d_elems,
+			                                                               d_prios, order, r_lo, n, ctx->d_cnt);
+			k_min_split_tbl<<<tg, 256, 0, st>>>(t->slots, t->nslots(), nshards, counts, nullptr, nullptr);
+			hipError_t e = hipGetLastError();
+			if (e == hipSuccess)
+				e = hipMemcpyAsync(h, counts, nshards * 8, hipMemcpyDeviceToHost, st);
+			rc = e == hipSuccess ? counters_fetch(ctx) : hip_fail(e, "k_min_cover_ranks", __FILE__, __LINE__);
+		}
+		if (rc == SYZSIG_OK && ctx->h_cnt[kCntOverflow])
+			rc = fail(SYZSIG_EIO, "minimize_split: table overflow (internal error)");
+		if (rc == SYZSIG_OK) {
+			unsigned long long offs[kMinMaxShards], run = 0;
+			for (uint32_t g = 0; g < nshards; g++) {
+				offs[g] = run;
+				run += h[g];
+				send_counts[g] = h[g];
+			}
+			hipError_t e = hipMemcpyAsync(cursor, offs, nshards * 8, hipMemcpyHostToDevice, st);
+			if (e == hipSuccess) {
+				k_min_split_tbl<<<tg, 256, 0, st>>>(t->slots, t->nslots(), nshards, counts, cursor, d_send);
+				e = hipGetLastError();
+			}
+			if (e == hipSuccess)
+				e = hipStreamSynchronize(st);
+			if (e != hipSuccess)
+				rc = hip_fail(e, "k_min_split_tbl", __FILE__, __LINE__);
+		}
+		syzsig_set_free(t);
+		return rc;
 	}
 	LevelMap lm;
 	SYZ_TRY(level_map_from_levels(levels, nl, &lm));

@@ -111,6 +111,12 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 		e = hipHostMalloc(&c->h_cnt, sizeof(unsigned long long) * syz::kNumCounters, hipHostMallocDefault);
 	if (e == hipSuccess)
 		e = hipHostMalloc(&c->h_pin, syz::kPinBytes, hipHostMallocDefault);
+	if (e == hipSuccess)
+		e = hipMalloc(&c->d_step, sizeof(unsigned long long) * syz::kStepCounters);
+	if (e == hipSuccess)
+		e = hipMemset(c->d_step, 0, sizeof(unsigned long long) * syz::kStepCounters);
+	if (e == hipSuccess)
+		e = hipHostMalloc(&c->h_step, sizeof(unsigned long long) * syz::kStepCounters, hipHostMallocDefault);
 	if (e != hipSuccess) {
 		syzsig_ctx_destroy(c);
 		return syz::hip_fail(e, "ctx_create", __FILE__, __LINE__);
@@ -118,8 +124,6 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 	c->stream = c->own_stream;
 	if (const char* v = getenv("SYZSIG_PART_MODE"))
 		c->part_mode = atoi(v);
-	if (const char* v = getenv("SYZSIG_AGG_VARIANT"))
-		c->agg_variant = (uint32_t)atoi(v);
 	if (const char* v = getenv("SYZSIG_AGG_DBG")) {
 		c->agg_dbg = (uint32_t)atoi(v);
 #ifndef SYZ_EXPERIMENTS
@@ -156,7 +160,14 @@ void syzsig_ctx_destroy(syzsig_ctx* c)
 		(void)hipHostFree(c->h_cnt);
 	if (c->h_pin)
 		(void)hipHostFree(c->h_pin);
+	if (c->d_step)
+		(void)hipFree(c->d_step);
+	if (c->h_step)
+		(void)hipHostFree(c->h_step);
 	for (auto& e : c->ev)
+		if (e)
+			(void)hipEventDestroy(e);
+	for (auto& e : c->ev_step)
 		if (e)
 			(void)hipEventDestroy(e);
 	if (c->own_stream)
@@ -212,9 +223,12 @@ int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable)
 	SYZ_LOCK(ctx);
 	if (!ctx)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_timing: ctx is NULL");
-	if (enable && !ctx->ev[0])
+	if (enable && !ctx->ev[0]) {
 		for (auto& e : ctx->ev)
 			SYZ_HIP(hipEventCreate(&e));
+		for (auto& e : ctx->ev_step)
+			SYZ_HIP(hipEventCreate(&e));
+	}
 	ctx->timing = enable != 0;
 	return SYZSIG_OK;
 }

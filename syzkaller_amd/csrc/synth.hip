@@ -46,6 +46,103 @@ __global__ void k_synth_m0(SynthCfg cfg, uint64_t n_known, uint64_t n, uint32_t*
 		synth_m0_elem(cfg, i, n_known, &elems[i], &prios[i]);
 }
 
+// One rank's shard of M0 (syzsig_synth_m0_shard_dev), in index order: per tile
+// of kM0Tile indices the owned count, a scan over the tiles, then each tile
+// writes its owned elements at its offset, ordered by index (wave ballots and
+// a running offset in LDS).
+constexpr uint32_t kM0Tile = 4096, kM0Threads = 256;
+
+__global__ __launch_bounds__(kM0Threads) void k_m0_shard_count(SynthCfg cfg, uint64_t n_known, uint64_t n,
+                                                               uint32_t nshards, uint32_t shard, uint64_t* tcnt)
+{
+	const uint64_t t0 = (uint64_t)blockIdx.x * kM0Tile;
+	uint64_t c = 0;
+	for (uint32_t u = threadIdx.x; u < kM0Tile; u += kM0Threads) {
+		const uint64_t i = t0 + u;
+		if (i < n) {
+			uint32_t e;
+			int8_t p;
+			synth_m0_elem(cfg, i, n_known, &e, &p);
+			c += owner_of(e, nshards) == shard;
+		}
+	}
+	__shared__ unsigned long long s;
+	if (threadIdx.x == 0)
+		s = 0;
+	__syncthreads();
+	c = wave_sum_u64(c);
+	if (lane_id() == 0)
+		atomicAdd(&s, (unsigned long long)c);
+	__syncthreads();
+	if (threadIdx.x == 0)
+		tcnt[blockIdx.x] = s;
+}
+
+// exclusive scan of ntiles counts (one block), total -> *total
+__global__ __launch_bounds__(1024) void k_m0_shard_scan(uint64_t* tcnt, uint64_t ntiles, uint64_t* total)
+{
+	__shared__ uint64_t part[1024];
+	const uint64_t per = (ntiles + 1023) / 1024, a = threadIdx.x * per, z = min<uint64_t>(ntiles, a + per);
+	uint64_t s = 0;
+	for (uint64_t i = a; i < z; i++)
+		s += tcnt[i];
+	part[threadIdx.x] = s;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		uint64_t run = 0;
+		for (int k = 0; k < 1024; k++) {
+			const uint64_t v = part[k];
+			part[k] = run;
+			run += v;
+		}
+		*total = run;
+	}
+	__syncthreads();
+	uint64_t run = part[threadIdx.x];
+	for (uint64_t i = a; i < z; i++) {
+		const uint64_t v = tcnt[i];
+		tcnt[i] = run;
+		run += v;
+	}
+}
+
+__global__ __launch_bounds__(kM0Threads) void k_m0_shard_write(SynthCfg cfg, uint64_t n_known, uint64_t n,
+                                                               uint32_t nshards, uint32_t shard,
+                                                               const uint64_t* __restrict__ toff, uint32_t* elems,
+                                                               int8_t* prios, uint64_t cap)
+{
+	__shared__ uint32_t wc[kM0Threads / 64];
+	const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+	const uint64_t t0 = (uint64_t)blockIdx.x * kM0Tile;
+	uint64_t run = toff[blockIdx.x];
+	for (uint32_t u = 0; u < kM0Tile; u += kM0Threads) {
+		const uint64_t i = t0 + u + threadIdx.x;
+		uint32_t e = 0;
+		int8_t p = 0;
+		bool own = false;
+		if (i < n) {
+			synth_m0_elem(cfg, i, n_known, &e, &p);
+			own = owner_of(e, nshards) == shard;
+		}
+		const uint64_t m = __ballot(own);
+		if (lane == 0)
+			wc[w] = (uint32_t)__popcll(m);
+		__syncthreads();
+		uint32_t before = 0, tot = 0;
+		for (uint32_t k = 0; k < kM0Threads / 64; k++) {
+			before += k < w ? wc[k] : 0;
+			tot += wc[k];
+		}
+		const uint64_t o = run + before + lane_rank(m);
+		if (own && o < cap) {
+			elems[o] = e;
+			prios[o] = p;
+		}
+		run += tot;
+		__syncthreads();  // wc is rewritten by the next step
+	}
+}
+
 }  // namespace syz
 
 using namespace syz;
@@ -123,6 +220,38 @@ int syzsig_synth_m0_dev(syzsig_ctx* ctx, const syzsig_synth_cfg* cfg, uint64_t k
 	                                                             d_prios);
 	SYZ_HIP(hipGetLastError());
 	SYZ_HIP(hipStreamSynchronize(ctx->stream));
+	return SYZSIG_OK;
+}
+
+int syzsig_synth_m0_shard_dev(syzsig_ctx* ctx, const syzsig_synth_cfg* cfg, uint64_t known_sys, uint64_t n,
+                              uint32_t nshards, uint32_t shard, uint32_t* d_elems, int8_t* d_prios, uint64_t cap,
+                              uint64_t* n_out)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !cfg_ok(cfg) || !n_out || nshards == 0 || shard >= nshards || (cap && (!d_elems || !d_prios)))
+		return fail(SYZSIG_EINVAL, "synth_m0_shard: bad argument");
+	*n_out = 0;
+	if (!n)
+		return SYZSIG_OK;
+	SynthCfg s = to_cfg(cfg);
+	const uint64_t nk = synth_n_known(s, known_sys), ntiles = (n + kM0Tile - 1) / kM0Tile;
+	if (ntiles > 0x7FFFFFFFull)
+		return fail(SYZSIG_ERANGE, "synth_m0_shard: n too large");
+	void* w;
+	SYZ_TRY(ws_get(ctx, 9, (ntiles + 1) * 8 + 64, &w));
+	uint64_t* tcnt = (uint64_t*)w;
+	uint64_t* tot = tcnt + ntiles;
+	const hipStream_t st = ctx->stream;
+	k_m0_shard_count<<<(uint32_t)ntiles, kM0Threads, 0, st>>>(s, nk, n, nshards, shard, tcnt);
+	k_m0_shard_scan<<<1, 1024, 0, st>>>(tcnt, ntiles, tot);
+	k_m0_shard_write<<<(uint32_t)ntiles, kM0Threads, 0, st>>>(s, nk, n, nshards, shard, tcnt, d_elems, d_prios, cap);
+	SYZ_HIP(hipGetLastError());
+	uint64_t* h = (uint64_t*)(ctx->h_pin + kPinPairs);
+	SYZ_HIP(hipMemcpyAsync(h, tot, 8, hipMemcpyDeviceToHost, st));
+	SYZ_HIP(hipStreamSynchronize(st));
+	*n_out = *h;
+	if (*h > cap)
+		return fail(SYZSIG_ERANGE, "synth_m0_shard: cap smaller than the shard");
 	return SYZSIG_OK;
 }
 

@@ -447,6 +447,14 @@ void syzsig_set_free(syzsig_set* s)
 	SYZ_LOCK(s ? s->ctx : nullptr);
 	if (!s)
 		return;
+	if (s->step_busy && s->ctx) {  // freed under an owner step: the step forgets its sets
+		syzsig_ctx* c = s->ctx;
+		if (c->step_ms)
+			c->step_ms->step_busy = false;
+		if (c->step_ns)
+			c->step_ns->step_busy = false;
+		c->step_ms = c->step_ns = nullptr;
+	}
 	set_release_storage(s);
 	delete s;
 }
@@ -456,6 +464,7 @@ int syzsig_set_clone(syzsig_ctx* ctx, const syzsig_set* s, syzsig_set** out)
 	SYZ_LOCK(ctx);
 	if (!ctx || !out)
 		return fail(SYZSIG_EINVAL, "set_clone: NULL argument");
+	SYZ_TRY(set_check_idle(s));
 	*out = nullptr;
 	if (!s)
 		return SYZSIG_OK;
@@ -473,6 +482,7 @@ int syzsig_set_clear(syzsig_ctx* ctx, syzsig_set* s)
 	SYZ_LOCK(ctx);
 	if (!ctx || !s)
 		return fail(SYZSIG_EINVAL, "set_clear: NULL argument");
+	SYZ_TRY(set_check_idle(s));
 	SYZ_HIP(hipMemsetAsync(s->slots, 0, s->nslots() * sizeof(uint64_t), ctx->stream));
 	s->len = 0;
 	return SYZSIG_OK;
@@ -483,6 +493,8 @@ int syzsig_set_copy_from(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src
 	SYZ_LOCK(ctx);
 	if (!ctx || !dst || !src)
 		return fail(SYZSIG_EINVAL, "set_copy_from: NULL argument");
+	SYZ_TRY(set_check_idle(dst));
+	SYZ_TRY(set_check_idle(src));
 	if (dst->nbuckets != src->nbuckets)
 		return fail(SYZSIG_EINVAL, "set_copy_from: capacity mismatch");
 	SYZ_HIP(hipMemcpyAsync(dst->slots, src->slots, src->nslots() * sizeof(uint64_t), hipMemcpyDeviceToDevice,
@@ -496,6 +508,9 @@ int syzsig_set_restore_keys(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* 
 	SYZ_LOCK(ctx);
 	if (!ctx || !dst || !src)
 		return fail(SYZSIG_EINVAL, "set_restore_keys: NULL argument");
+	SYZ_TRY(set_check_idle(dst));
+	SYZ_TRY(set_check_idle(src));
+	SYZ_TRY(set_check_idle(keys));
 	if (dst->nbuckets != src->nbuckets)
 		return fail(SYZSIG_EINVAL, "set_restore_keys: capacity mismatch (dst grew since the snapshot)");
 	if (keys && keys->len) {
@@ -511,11 +526,22 @@ int syzsig_set_restore_keys(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* 
 	return SYZSIG_OK;
 }
 
+int syzsig_set_reserve(syzsig_ctx* ctx, syzsig_set* s, uint64_t extra)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !s)
+		return fail(SYZSIG_EINVAL, "set_reserve: NULL argument");
+	SYZ_TRY(set_check_idle(s));
+	return set_reserve(s, extra);
+}
+
 int syzsig_set_equal(syzsig_ctx* ctx, const syzsig_set* a, const syzsig_set* b, int* equal)
 {
 	SYZ_LOCK(ctx);
 	if (!ctx || !a || !b || !equal)
 		return fail(SYZSIG_EINVAL, "set_equal: NULL argument");
+	SYZ_TRY(set_check_idle(a));
+	SYZ_TRY(set_check_idle(b));
 	*equal = 0;
 	if (a->nbuckets != b->nbuckets || a->len != b->len)
 		return SYZSIG_OK;
@@ -564,6 +590,7 @@ int syzsig_serialize(syzsig_ctx* ctx, const syzsig_set* s, uint32_t* elems, int8
 	SYZ_LOCK(ctx);
 	if (!ctx || !n_out || (cap && (!elems || !prios)))
 		return fail(SYZSIG_EINVAL, "serialize: NULL argument");
+	SYZ_TRY(set_check_idle(s));
 	*n_out = 0;
 	if (!s || s->len == 0)
 		return SYZSIG_OK;  // signal.go:43-45
@@ -631,6 +658,8 @@ int syzsig_diff(syzsig_ctx* ctx, const syzsig_set* s, const syzsig_set* s1, syzs
 	SYZ_LOCK(ctx);
 	if (!ctx || !out)
 		return fail(SYZSIG_EINVAL, "diff: NULL argument");
+	SYZ_TRY(set_check_idle(s));
+	SYZ_TRY(set_check_idle(s1));
 	*out = nullptr;
 	if (syzsig_empty(s1))
 		return SYZSIG_OK;  // signal.go:74-76
@@ -648,6 +677,7 @@ int syzsig_diff_raw(syzsig_ctx* ctx, const syzsig_set* s, const uint32_t* raw, u
 	SYZ_LOCK(ctx);
 	if (!ctx || !out || (n && !raw))
 		return fail(SYZSIG_EINVAL, "diff_raw: NULL argument");
+	SYZ_TRY(set_check_idle(s));
 	*out = nullptr;
 	if (n == 0)
 		return SYZSIG_OK;
@@ -666,6 +696,8 @@ int syzsig_intersection(syzsig_ctx* ctx, const syzsig_set* s, const syzsig_set* 
 	SYZ_LOCK(ctx);
 	if (!ctx || !out)
 		return fail(SYZSIG_EINVAL, "intersection: NULL argument");
+	SYZ_TRY(set_check_idle(s));
+	SYZ_TRY(set_check_idle(s1));
 	*out = nullptr;
 	if (syzsig_empty(s1))
 		return SYZSIG_OK;  // signal.go:105-107
@@ -721,6 +753,8 @@ int syzsig_merge(syzsig_ctx* ctx, syzsig_set** sp, const syzsig_set* s1)
 	SYZ_LOCK(ctx);
 	if (!ctx || !sp)
 		return fail(SYZSIG_EINVAL, "merge: NULL argument");
+	SYZ_TRY(set_check_idle(*sp));
+	SYZ_TRY(set_check_idle(s1));
 	if (syzsig_empty(s1))
 		return SYZSIG_OK;  // signal.go:118-120
 	if (!*sp)

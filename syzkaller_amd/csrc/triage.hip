@@ -26,7 +26,6 @@
 #include <algorithm>
 #include <vector>
 
-#include <hipcub/hipcub.hpp>
 
 #include "internal.h"
 
@@ -703,338 +702,9 @@ int level_map_from_levels(const int8_t* levels, uint32_t nlevels, LevelMap* lm)
 	return SYZSIG_OK;
 }
 
-// ---- records mode by sorting (the owner side of a sharded step, large
-// inputs): the records sorted by (element, serial) -- one radix sort, the
-// record's index carried -- so each element's records are a contiguous run in
-// serial order, and one thread per run replays checkNewSignal for it: the
-// running maximum starts at M0[e] (one shard probe per distinct element, not
-// per record), a record is new iff its prio exceeds it (and so is a duplicate
-// of a new record in the same call, as DiffRaw collapses duplicates); the
-// run's final maximum, when raised, is merged into the shard and newSignal.
-// Sort key: e << 24 | serial (bits 0..55, the sorted ones) | level << 56.
-__global__ void k_recs_keys(const uint64_t* __restrict__ recs, uint64_t n, uint32_t nlev, uint64_t* keys,
-                            uint32_t* vals, unsigned long long* bad)
-{
-	uint64_t nbad = 0;
-	for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-		const uint64_t x = recs[r];
-		const uint64_t l = (x >> 24) & 0xff;
-		nbad += l >= nlev;
-		keys[r] = ((x >> 32) << 24) | (x & kSerialMask) | (l << 56);
-		vals[r] = (uint32_t)r;
-	}
-	block_count(bad, nbad);
-}
-
-// The replay of one element run from its head i: checkNewSignal's rule over
-// the run's records in serial order, from M0[e]; then the element's final prio
-// merged into the shard and newSignal.
-constexpr uint32_t kRunMax = 64;  // longest run the element-only sort's walk takes (else: the full-key sort)
-struct RecsWalk {
-	const uint64_t* __restrict__ sk;
-	const uint32_t* __restrict__ order;
-	uint64_t n;
-	LevelMap lm;
-	uint64_t *ms, ms_bmask, *ns, ns_bmask;
-	uint8_t* flags;
-	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0, distinct = 0;
-	static constexpr uint64_t kElemSerial = (1ull << 56) - 1;
-
-	__device__ void run(uint64_t i)
-	{
-		const uint32_t e = (uint32_t)((sk[i] & kElemSerial) >> 24);
-		distinct++;
-		uint64_t v = 0;
-		const bool present = tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v);
-		const int m0 = present ? (int)slot_prio(v) : -1000;  // absent: below every prio (signal.go:93-95)
-		int m = m0;
-		uint32_t last_new = 0xFFFFFFFFu;
-		for (uint64_t j = i; j < n; j++) {
-			const uint64_t kj = sk[j];
-			if ((uint32_t)((kj & kElemSerial) >> 24) != e)
-				break;
-			const uint32_t k = (uint32_t)kj & kSerialMask;
-			const int p = lm.val[(kj >> 56) & 3];
-			if (p > m || k == last_new) {
-				flags[order[j]] = 1;
-				m = max(m, p);
-				last_new = k;
-			}
-		}
-		if (m > m0) {  // maxSignal.Merge / newSignal.Merge of the element's final prio
-			changed++;
-			inserted += !present;
-			ovf += tbl_merge(ms, ms_bmask, e, (int8_t)m) < 0;
-			const int r = tbl_merge(ns, ns_bmask, e, (int8_t)m);
-			ns_ins += r == 1;
-			ovf += r < 0;
-		}
-	}
-	// The same replay for a run left in arrival order (records sorted by the
-	// element bits only, stably): the records are taken in (serial, arrival)
-	// order -- the order of the full-key sort -- by selecting the next one in
-	// each of r steps; r <= kRunMax.
-	__device__ void run_sel(uint64_t i)
-	{
-		const uint32_t e = (uint32_t)((sk[i] & kElemSerial) >> 24);
-		distinct++;
-		uint64_t v = 0;
-		const bool present = tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v);
-		const int m0 = present ? (int)slot_prio(v) : -1000;  // absent: below every prio (signal.go:93-95)
-		uint32_t r = 1;
-		while (r < kRunMax && i + r < n && (uint32_t)((sk[i + r] & kElemSerial) >> 24) == e)
-			r++;
-		int m = m0;
-		uint32_t last_new = 0xFFFFFFFFu;
-		uint64_t cur = 0;  // the last taken record's (serial << 8 | position) + 1
-		for (uint32_t step = 0; step < r; step++) {
-			uint64_t best = ~0ull;
-			for (uint32_t t = 0; t < r; t++) {
-				const uint64_t o = ((sk[i + t] & kSerialMask) << 8) | t;
-				best = o >= cur && o < best ? o : best;
-			}
-			cur = best + 1;
-			const uint32_t t = (uint32_t)best & 0xFF;
-			const uint64_t kj = sk[i + t];
-			const uint32_t k = (uint32_t)kj & kSerialMask;
-			const int p = lm.val[(kj >> 56) & 3];
-			if (p > m || k == last_new) {
-				flags[order[i + t]] = 1;
-				m = max(m, p);
-				last_new = k;
-			}
-		}
-		if (m > m0) {
-			changed++;
-			inserted += !present;
-			ovf += tbl_merge(ms, ms_bmask, e, (int8_t)m) < 0;
-			const int rr = tbl_merge(ns, ns_bmask, e, (int8_t)m);
-			ns_ins += rr == 1;
-			ovf += rr < 0;
-		}
-	}
-	__device__ void count(unsigned long long* ctr)
-	{
-		block_count(&ctr[kCntInserted], inserted);
-		block_count(&ctr[kCntChanged], changed);
-		block_count(&ctr[kCntAux], ns_ins);
-		block_count(&ctr[kCntOverflow], ovf);
-		block_count(&ctr[kCntDistinct], distinct);
-	}
-};
-
-// One thread per element run, over the heads k_recs_heads compacted: every
-// lane of a wave holds a run, so 64 shard probes and merges are in flight per
-// wave.
-template <bool kSel>
-__global__ void k_recs_walk(const uint32_t* __restrict__ heads, uint64_t nh, RecsWalk rw, unsigned long long* ctr)
-{
-	for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nh; t += (uint64_t)gridDim.x * blockDim.x) {
-		if (kSel)
-			rw.run_sel(heads[t]);
-		else
-			rw.run(heads[t]);
-	}
-	rw.count(ctr);
-}
-
-// SYZSIG_DEBUG_RECS_SCAN: one thread per sorted position, the heads among them
-// walking their runs (a wave waits for its slowest head each step).
-__global__ void k_recs_walk_scan(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ order, uint64_t n,
-                                 LevelMap lm, uint64_t* ms, uint64_t ms_bmask, uint64_t* ns, uint64_t ns_bmask,
-                                 uint8_t* flags, unsigned long long* ctr)
-{
-	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0, distinct = 0;
-	constexpr uint64_t kElemSerial = (1ull << 56) - 1;
-	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-		const uint64_t ki = sk[i];
-		const uint32_t e = (uint32_t)((ki & kElemSerial) >> 24);
-		if (i > 0 && (uint32_t)((sk[i - 1] & kElemSerial) >> 24) == e)
-			continue;  // not the head of e's run
-		distinct++;
-		uint64_t v = 0;
-		const bool present = tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v);
-		const int m0 = present ? (int)slot_prio(v) : -1000;  // absent: below every prio (signal.go:93-95)
-		int m = m0;
-		uint32_t last_new = 0xFFFFFFFFu;
-		for (uint64_t j = i; j < n; j++) {
-			const uint64_t kj = sk[j];
-			if ((uint32_t)((kj & kElemSerial) >> 24) != e)
-				break;
-			const uint32_t k = (uint32_t)kj & kSerialMask;
-			const int p = lm.val[(kj >> 56) & 3];
-			if (p > m || k == last_new) {
-				flags[order[j]] = 1;
-				m = max(m, p);
-				last_new = k;
-			}
-		}
-		if (m > m0) {  // maxSignal.Merge / newSignal.Merge of the element's final prio
-			changed++;
-			inserted += !present;
-			ovf += tbl_merge(ms, ms_bmask, e, (int8_t)m) < 0;
-			const int r = tbl_merge(ns, ns_bmask, e, (int8_t)m);
-			ns_ins += r == 1;
-			ovf += r < 0;
-		}
-	}
-	block_count(&ctr[kCntInserted], inserted);
-	block_count(&ctr[kCntChanged], changed);
-	block_count(&ctr[kCntAux], ns_ins);
-	block_count(&ctr[kCntOverflow], ovf);
-	block_count(&ctr[kCntDistinct], distinct);
-}
-
-// The sorted positions where an element's run starts, compacted (in no
-// particular order) into heads[0, *cnt).  Each step a block takes
-// kHeadsPer x 1024 positions (all loads issued together), then one block scan
-// and one atomic place its heads.
-constexpr uint32_t kHeadsPer = 8;
-__global__ __launch_bounds__(1024) void k_recs_heads(const uint64_t* __restrict__ sk, uint64_t n,
-                                                     unsigned long long* cnt, uint32_t* heads,
-                                                     unsigned long long* nlong)
-{
-	constexpr uint64_t kElem = ((1ull << 56) - 1) & ~(uint64_t)kSerialMask;
-	__shared__ uint32_t wbase[16];
-	__shared__ uint32_t s_base;
-	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), nw = blockDim.x >> 6;
-	const uint64_t span = (uint64_t)blockDim.x * kHeadsPer;
-	for (uint64_t b0 = blockIdx.x * span; b0 < n; b0 += (uint64_t)gridDim.x * span) {
-		uint64_t cur[kHeadsPer], prev[kHeadsPer], m[kHeadsPer];
-#pragma unroll
-		for (uint32_t u = 0; u < kHeadsPer; u++) {
-			const uint64_t i = b0 + u * blockDim.x + threadIdx.x;
-			cur[u] = i < n ? sk[i] : 0;
-			prev[u] = i > 0 && i < n ? sk[i - 1] : 0;
-		}
-		uint32_t tot = 0;
-#pragma unroll
-		for (uint32_t u = 0; u < kHeadsPer; u++) {
-			const uint64_t i = b0 + u * blockDim.x + threadIdx.x;
-			m[u] = __ballot(i < n && (i == 0 || ((cur[u] ^ prev[u]) & kElem) != 0));
-			tot += (uint32_t)__popcll(m[u]);
-		}
-		if (lane == 0)
-			wbase[w] = tot;
-		__syncthreads();
-		if (threadIdx.x == 0) {
-			uint32_t t = 0;
-			for (uint32_t k = 0; k < nw; k++) {
-				const uint32_t c = wbase[k];
-				wbase[k] = t;
-				t += c;
-			}
-			s_base = t ? (uint32_t)atomicAdd(cnt, (unsigned long long)t) : 0u;
-		}
-		__syncthreads();
-		uint32_t off = s_base + wbase[w];
-		uint32_t lng = 0;
-#pragma unroll
-		for (uint32_t u = 0; u < kHeadsPer; u++) {
-			const uint64_t i = b0 + u * blockDim.x + threadIdx.x;
-			if ((m[u] >> lane) & 1) {
-				heads[off + lane_rank(m[u])] = (uint32_t)i;
-				lng += i + kRunMax < n && ((sk[i + kRunMax] ^ cur[u]) & kElem) == 0;  // a run of > kRunMax
-			}
-			off += (uint32_t)__popcll(m[u]);
-		}
-		if (__ballot(lng != 0) && lane == 0)
-			atomicAdd(nlong, 1ull);
-		__syncthreads();  // wbase / s_base are rewritten by the next step
-	}
-}
-
-static int triage_records_sorted(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t n,
-                                 const LevelMap& lm, uint8_t* new_flags, syzsig_batch_stats* st)
-{
-	const hipStream_t s = ctx->stream;
-	void *dk, *dtmp;
-	SYZ_TRY(ws_get(ctx, 48, n * 28 + 256, &dk));
-	uint64_t* keys = (uint64_t*)dk;
-	uint64_t* keys2 = keys + n;
-	uint32_t* vals = (uint32_t*)(keys2 + n);
-	uint32_t* order = vals + n;
-	uint32_t* heads = order + n;
-	// The full (element, serial) key: 7 onesweep passes.  SYZSIG_DEBUG_RECS_SEL:
-	// a stable sort by the element bits alone (4 passes), the walk taking each
-	// run's records in serial order by selection (a run longer than kRunMax
-	// sends the input back to the full-key sort) -- 3 passes saved (0.22 ms at
-	// C4's owner side), the selection walk 0.34 ms dearer: not the default.
-	size_t tmp_bytes = 0, tmp_el = 0;
-	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
-	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_el, keys, keys2, vals, order, (int)n, 24, 56, s));
-	tmp_bytes = std::max(tmp_bytes, tmp_el);
-	SYZ_TRY(ws_get(ctx, 49, tmp_bytes + 64, &dtmp));
-	SYZ_TRY(counters_reset(ctx));
-	k_recs_keys<<<grid_for(n, 256, 8192), 256, 0, s>>>(recs, n, lm.n, keys, vals, &ctx->d_cnt[kCntError]);
-	SYZ_HIP(hipGetLastError());
-	bool sel = (ctx->agg_dbg & SYZSIG_DEBUG_RECS_SEL) && !(ctx->agg_dbg & SYZSIG_DEBUG_RECS_SCAN);
-	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, keys, keys2, vals, order, (int)n, sel ? 24 : 0, 56, s));
-	const int hgrid = grid_for((n + kHeadsPer - 1) / kHeadsPer, 1024, 1024);
-	k_recs_heads<<<hgrid, 1024, 0, s>>>(keys2, n, &ctx->d_cnt[kCntDistinct], heads, &ctx->d_cnt[kCntAux2]);
-	SYZ_HIP(hipGetLastError());
-	SYZ_TRY(counters_fetch(ctx));
-	if (ctx->h_cnt[kCntError])
-		return fail(SYZSIG_EINVAL, "triage_records: a record's prio level is out of range");
-	if (sel && ctx->h_cnt[kCntAux2]) {  // a run too long for the selection walk: the full-key sort
-		sel = false;
-		SYZ_TRY(counters_reset(ctx));
-		SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, keys, keys2, vals, order, (int)n, 0, 56, s));
-		k_recs_heads<<<hgrid, 1024, 0, s>>>(keys2, n, &ctx->d_cnt[kCntDistinct], heads, &ctx->d_cnt[kCntAux2]);
-		SYZ_HIP(hipGetLastError());
-		SYZ_TRY(counters_fetch(ctx));
-	}
-	// room for every distinct element changing
-	const uint64_t D = ctx->h_cnt[kCntDistinct];
-	SYZ_TRY(set_reserve(ms, D));
-	const bool fresh_ns = !*ns;
-	if (fresh_ns)
-		SYZ_TRY(syzsig_set_make(ctx, D, ns));  // newSignal.Merge allocates a nil receiver (signal.go:121-125)
-	syzsig_set* nsp = *ns;
-	SYZ_TRY(set_reserve_load(nsp, D, kHardLoad));
-	SYZ_TRY(counters_reset(ctx));
-	if (ctx->timing)
-		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
-	// (one thread per record position, each walking one record: 1.09 ms for the
-	// owner's 7.3M records; the scan walk 0.44 ms)
-	if (D == 0 || D > n)
-		return fail(SYZSIG_EIO, "triage_records: run head count out of range (internal error)");
-	if (ctx->agg_dbg & SYZSIG_DEBUG_RECS_SCAN)
-		k_recs_walk_scan<<<grid_for(n, 256, 8192), 256, 0, s>>>(keys2, order, n, lm, ms->slots, ms->nbuckets - 1,
-		                                                        nsp->slots, nsp->nbuckets - 1, new_flags, ctx->d_cnt);
-	else
-		(sel ? k_recs_walk<true> : k_recs_walk<false>)<<<grid_for(D, 256, 8192), 256, 0, s>>>(
-		    heads, D, RecsWalk{keys2, order, n, lm, ms->slots, ms->nbuckets - 1, nsp->slots, nsp->nbuckets - 1, new_flags},
-		    ctx->d_cnt);
-	SYZ_HIP(hipGetLastError());
-	if (ctx->timing)
-		SYZ_HIP(hipEventRecord(ctx->ev[3], s));
-	SYZ_TRY(counters_fetch(ctx));
-	if (ctx->timing) {
-		float t = 0;
-		SYZ_HIP(hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]));
-		st->decide_ms += t;
-	}
-	if (ctx->h_cnt[kCntOverflow])
-		return fail(SYZSIG_EIO, "triage_records: table overflow after reserve (internal error)");
-	const uint64_t changed = ctx->h_cnt[kCntChanged];
-	ms->len += ctx->h_cnt[kCntInserted];
-	nsp->len += ctx->h_cnt[kCntAux];
-	if (fresh_ns && changed == 0) {
-		syzsig_set_free(nsp);
-		*ns = nullptr;
-	}
-	st->inserted += ctx->h_cnt[kCntInserted];
-	st->changed += changed;
-	st->candidates += changed;
-	st->distinct += ctx->h_cnt[kCntDistinct];
-	st->survivors += ctx->h_cnt[kCntDistinct];
-	st->runs++;
-	return SYZSIG_OK;
-}
-
 int triage_records_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t nrec,
-                        const int8_t* levels, uint32_t nlevels, uint8_t* new_flags, syzsig_batch_stats* st)
+                        const int8_t* levels, uint32_t nlevels, uint8_t* new_flags, syzsig_batch_stats* st,
+                        bool allow_lds)
 {
 	LevelMap lm;
 	SYZ_TRY(level_map_from_levels(levels, nlevels, &lm));
@@ -1042,12 +712,18 @@ int triage_records_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const 
 	if (nrec == 0)
 		return SYZSIG_OK;
 	SYZ_HIP(hipMemsetAsync(new_flags, 0, nrec, ctx->stream));
-	if (nrec >= (1ull << 20) && nrec < (1ull << 31) && ctx->part_mode != 0) {
-		SYZ_TRY(triage_records_sorted(ctx, ms, ns, recs, nrec, lm, new_flags, st));
-		if ((double)ms->len > kMaxLoad * (double)ms->nslots())
-			SYZ_TRY(set_rehash(ms, buckets_for(ms->len), false));
-		st->new_signal_len = syzsig_len(*ns);
-		return SYZSIG_OK;
+	if (nrec >= (1ull << 20) && nrec < (1ull << 31) && ctx->part_mode != 0 && allow_lds) {
+		// partitioned by element through LDS (recs.hip); a partition past the LDS
+		// capacity (a hot element's records in a generic input) voids that run
+		// before anything is committed and the per-record path below runs instead
+		bool done = false;
+		SYZ_TRY(rp_triage_records(ctx, ms, ns, recs, nrec, lm, new_flags, st, &done));
+		if (done) {
+			if ((double)ms->len > kMaxLoad * (double)ms->nslots())
+				SYZ_TRY(set_rehash(ms, buckets_for(ms->len), false));
+			st->new_signal_len = syzsig_len(*ns);
+			return SYZSIG_OK;
+		}
 	}
 	SYZ_TRY(set_ensure_triage_state(ms));
 	const uint64_t nseg = (nrec + kSegRecs - 1) / kSegRecs;
@@ -1089,6 +765,8 @@ int syzsig_triage_batch(syzsig_ctx* ctx, syzsig_set* max_signal, syzsig_set** ne
 		return fail(SYZSIG_EINVAL, "triage_batch: new_pairs_cap without new_pairs");
 	if (b->ncalls && (!b->call_start || !b->call_len || !b->call_prio || !b->call_new))
 		return fail(SYZSIG_EINVAL, "triage_batch: NULL call arrays");
+	SYZ_TRY(set_check_idle(max_signal));
+	SYZ_TRY(set_check_idle(*new_signal));
 	syzsig_batch_stats st;
 	memset(&st, 0, sizeof(st));
 	int rc = triage_batch_impl(ctx, max_signal, new_signal, b, &st);
@@ -1164,9 +842,11 @@ int syzsig_triage_records_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set** n
 		return fail(SYZSIG_EINVAL, "triage_records: NULL argument");
 	if (*new_signal == shard)
 		return fail(SYZSIG_EINVAL, "triage_records: new_signal aliases the shard");
+	SYZ_TRY(set_check_idle(shard));
+	SYZ_TRY(set_check_idle(*new_signal));
 	syzsig_batch_stats st;
 	memset(&st, 0, sizeof(st));
-	int rc = triage_records_impl(ctx, shard, new_signal, d_recs, nrec, levels, nlevels, d_new_flags, &st);
+	int rc = triage_records_impl(ctx, shard, new_signal, d_recs, nrec, levels, nlevels, d_new_flags, &st, true);
 	if (stats)
 		*stats = st;
 	return rc;

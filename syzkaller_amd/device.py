@@ -8,7 +8,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import Batch, BatchStats, check
+from ._lib import Batch, BatchStats, StepStatus, check
 from .signal import Signal, engine
 
 __all__ = ["Device", "call_layout"]
@@ -269,6 +269,43 @@ class Device:
                                                       send.numel(), _p(back_flags), ctypes.byref(st)))
         return st.as_dict()
 
+    # ---------------------------------------------------------------- the stream-ordered sharded step
+    def step_send(self, b, serial_base, levels, nshards, cap, send, exact=False):
+        """Source side (syzsig_step_send_dev): b's staircase records into
+        nshards buckets of cap + 1 words (send, int64).  Enqueues only."""
+        self._check_dev(send)
+        if send.numel() < nshards * (cap + 1):
+            raise ValueError("send needs nshards * (cap + 1) words")
+        lv = (ctypes.c_int8 * len(levels))(*levels)
+        check(self.L.syzsig_step_send_dev(self.eng.h, ctypes.byref(b), int(serial_base), lv, len(levels), int(nshards),
+                                          int(cap), _p(send), int(bool(exact))))
+
+    def step_own(self, shard, new_signal, recv, nshards, cap, levels, flags, exact=False):
+        """Owner side (syzsig_step_own_dev): the received buckets against this
+        owner's shard; flags (uint8, nshards * (cap + 1)).  Enqueues only
+        (exact: the per-record path, synchronous)."""
+        self._check_dev(recv, flags)
+        if recv.numel() < nshards * (cap + 1) or flags.numel() < nshards * (cap + 1):
+            raise ValueError("recv / flags need nshards * (cap + 1) entries")
+        if new_signal.is_nil():
+            raise ValueError("step_own needs a non-nil newSignal shard (make(Signal, hint))")
+        lv = (ctypes.c_int8 * len(levels))(*levels)
+        check(self.L.syzsig_step_own_dev(self.eng.h, shard.handle, new_signal.handle, _p(recv), int(nshards),
+                                         int(cap), lv, len(levels), _p(flags), int(bool(exact))))
+
+    def step_back(self, b, serial_base, send, nshards, cap, back):
+        """Source side again (syzsig_step_back_dev): the owners' flags -> b's
+        call_new / new_pairs (/ new_bits).  Enqueues only unless bits are wanted."""
+        self._check_dev(send, back)
+        check(self.L.syzsig_step_back_dev(self.eng.h, ctypes.byref(b), int(serial_base), _p(send), int(nshards),
+                                          int(cap), _p(back)))
+
+    def step_finish(self):
+        """The step's one host synchronisation -> the status dict."""
+        st = StepStatus()
+        check(self.L.syzsig_step_finish(self.eng.h, ctypes.byref(st)))
+        return st.as_dict()
+
     # ---------------------------------------------------------------- synthetic data
     def synth_traces(self, cfg, prog_base, nprog, calls_per_prog, call_len):
         """-> (pcs int64[sum], call_start int64[n], call_prio uint8[n]) for nprog programs."""
@@ -280,6 +317,23 @@ class Device:
         check(self.L.syzsig_synth_traces_dev(self.eng.h, ctypes.byref(cfg), int(prog_base), int(nprog),
                                              int(calls_per_prog), _p(call_start), _p(call_len), _p(pcs), _p(prio)))
         return pcs, call_start, call_len, prio
+
+    def synth_m0_shard(self, cfg, known_sys, n, nshards, shard):
+        """This shard's elements of synth_m0(cfg, known_sys, n), in index order
+        (owner_of), without materialising the whole M0."""
+        cap = n // nshards + 8 * int(n ** 0.5) + 1024 if nshards > 1 else n
+        for _ in range(2):
+            elems = torch.empty(max(cap, 1), dtype=torch.int32, device=self.dev)
+            prios = torch.empty(max(cap, 1), dtype=torch.int8, device=self.dev)
+            got = ctypes.c_uint64()
+            rc = self.L.syzsig_synth_m0_shard_dev(self.eng.h, ctypes.byref(cfg), int(known_sys), int(n), int(nshards),
+                                                  int(shard), _p(elems), _p(prios), cap, ctypes.byref(got))
+            if rc == _lib.SYZSIG_ERANGE and got.value > cap:
+                cap = got.value
+                continue
+            check(rc)
+            return elems[: got.value], prios[: got.value]
+        raise RuntimeError("synth_m0_shard: size changed between calls")
 
     def synth_m0(self, cfg, known_sys, n):
         elems = torch.empty(n, dtype=torch.int32, device=self.dev)

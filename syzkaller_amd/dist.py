@@ -4,20 +4,26 @@
 A batch is split by program range: rank r triages programs
 [r*P, (r+1)*P), so the global serial order is rank-major (the order a single
 fuzzer would see them).  maxSignal is partitioned by element:
-shard(e) = owner_of(e, world) (csrc/common.h).  One step:
+shard(e) = owner_of(e, world) (csrc/common.h).  One step (ShardedTriage.step),
+stream-ordered with ONE host synchronisation:
 
-  1. levels  = union of every rank's call prios          (all_reduce, 256 ints)
-  2. aggregate the rank's records per element and keep
-     each element's staircase, grouped by owner           (agg.hip; shard.hip
-                                                           routes every record)
-  3. exchange counts, then records                       (all_to_all_single)
-  4. owner triages the records it received               (triage.hip, records mode)
-  5. new-flags travel back to the sources                (all_to_all_single)
-  6. sources turn flags into call flags / pairs / bits   (agg.hip or shard.hip)
+  1. source: aggregate the rank's records per element and write each
+     element's staircase into fixed buckets, one per owner, each with a
+     header word (count, void / overflow flags)       (syzsig_step_send_dev)
+  2. equal-split all_to_all_single of the buckets        (RCCL, no split sizes
+                                                          needed on the host)
+  3. owner: the received buckets, LDS-partitioned by
+     element, replayed against the shard               (syzsig_step_own_dev)
+  4. equal-split all_to_all_single of the flags back (a status byte per bucket)
+  5. source: flags -> call_new / pairs                   (syzsig_step_back_dev)
+  6. syzsig_step_finish: the one synchronisation; reads the step's status.
 
-Only step 3/5 move data between GPUs; each element's whole history in the
-batch lands on one owner, which applies the exact serial semantics via the
-serial index carried in every record (see triage.hip).
+Every owner sees every source's header, so all ranks agree, without another
+collective, whether the step is void (nothing committed anywhere: redone with
+a larger bucket cap or the exact source path) or which owners skipped their
+records (redone by those owners on the exact path, one more flags exchange).
+Each element's whole history in the batch lands on one owner, which applies
+the exact serial semantics via the serial index carried in every record.
 """
 import torch
 import torch.distributed as dist
@@ -45,49 +51,37 @@ def owner_of_torch(elems, nshards):
 
 
 class GpuShardOps:
-    """The device half of a sharded step, on libsyzsig.
+    """The device half of a sharded step, on libsyzsig (syzsig_step_*):
+    stream-ordered, one host synchronisation in finish()."""
 
-    aggregate=True (default): the source aggregates its batch per element and
-    sends only the staircase records (agg.hip, <= 4 per distinct element);
-    False: every record is sent (shard.hip).  Both give the same result."""
-
-    def __init__(self, dev, aggregate=True):
+    def __init__(self, dev):
         self.dev = dev
-        self.aggregate = aggregate
-        self._send = None
-        self._flags = None
-        self.last_source_stats = {}
+        self.device = dev.dev
+        self.last = {}
 
-    def partition(self, batch, serial_base, levels, nshards):
-        b, new_bits, call_new = batch
-        n = b.nrec
-        if self.aggregate:
-            if self._send is None or self._send.numel() < max(n, 1):
-                self._send = torch.empty(max(n, 1), dtype=torch.int64, device=self.dev.dev)
-            counts, st = self.dev.shard_agg_partition(b, serial_base, levels, nshards, self._send)
-            self.last_source_stats = st
-            send = self._send[: sum(counts)]
-            return send, (send, serial_base), counts
-        send = torch.empty(n, dtype=torch.int64, device=self.dev.dev)
-        send_pos = torch.empty(n, dtype=torch.int32, device=self.dev.dev)
-        counts = self.dev.shard_partition(b, serial_base, levels, nshards, send, send_pos)
-        return send, send_pos, counts
+    def alloc(self, n, dtype):
+        return torch.empty(n, dtype=dtype, device=self.device)
 
-    def triage_records(self, shard, new_signal, recs, levels):
-        if self._flags is None or self._flags.numel() < recs.numel():
-            self._flags = torch.empty(max(recs.numel(), 1) * 5 // 4 + 1, dtype=torch.uint8, device=self.dev.dev)
-        flags = self._flags[: recs.numel()]
-        st = self.dev.triage_records(shard, new_signal, recs, levels, flags)
-        return flags, st
+    @staticmethod
+    def records(batch):
+        return int(batch[0].nrec)
 
-    def unpartition(self, batch, token, back):
-        b, new_bits, call_new = batch
-        if self.aggregate:
-            send, serial_base = token
-            self.dev.shard_agg_unpartition(b, serial_base, send, back)
-        else:
-            self.dev.shard_unpartition(b, token, back)
-        return new_bits, call_new
+    def send(self, batch, serial_base, levels, nshards, cap, send, exact=False):
+        self.dev.step_send(batch[0], serial_base, levels, nshards, cap, send, exact)
+
+    def own(self, shard, new_signal, recv, nshards, cap, levels, flags, exact=False):
+        self.dev.step_own(shard, new_signal, recv, nshards, cap, levels, flags, exact)
+
+    def back(self, batch, serial_base, send, nshards, cap, back):
+        self.dev.step_back(batch[0], serial_base, send, nshards, cap, back)
+
+    def finish(self):
+        self.last = self.dev.step_finish()
+        return self.last
+
+    @staticmethod
+    def outputs(batch):
+        return batch[1], batch[2]
 
 
 # The prios signalPrio can produce (syz-fuzzer/fuzzer.go:513-521): a fixed
@@ -98,24 +92,33 @@ SIGNAL_PRIO_LEVELS = (0, 1, 2, 3)
 
 
 class ShardedTriage:
-    """One rank's side of a sharded checkNewSignal step.
+    """One rank's side of a sharded checkNewSignal step (syz-fuzzer/fuzzer.go:494-511
+    over the rank-major batch).
 
-    levels: the prio levels of every rank's calls, ascending as int8 (<= 4);
-    None = agree on them with an all_reduce each step.  Per step the only host
-    synchronisation is the exchange of the per-owner record counts (the split
-    sizes all_to_all_single needs); the receive and flag buffers are reused."""
+    ops: GpuShardOps(dev) or a restatement with the same send / own / back /
+    finish / alloc methods.  levels: the prio levels of every rank's calls,
+    ascending as int8 (<= 4); None = agree on them with an all_reduce each step.
+    The bucket cap (records per source and owner) is agreed by all ranks: on the
+    first step from the batch sizes, then tightened once to what the first step
+    needed; a step that overflows it is redone with a larger one."""
 
-    def __init__(self, ops, shard, new_signal, group=None, device=None, levels=None):
+    CAP_SLACK = 1.25
+
+    def __init__(self, ops, shard, new_signal, group=None, device=None, levels=None, cap=None):
         self.ops = ops
         self.shard = shard            # this rank's maxSignal shard
-        self.new_signal = new_signal  # this rank's newSignal shard
+        self.new_signal = new_signal  # this rank's newSignal shard (non-nil)
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = device
         self.fixed_levels = sorted(levels) if levels is not None else None
-        self._recv = None
-        self._back = None
+        self.cap = cap
+        self._tightened = cap is not None
+        self._exact = False
+        self._bufs = {}
+        self.redos = 0
+        self.fixups = 0
 
     def levels(self, call_prio):
         """Union of the prios of all ranks' calls, ascending as int8."""
@@ -128,37 +131,80 @@ class ShardedTriage:
         vals = [v if v < 128 else v - 256 for v in torch.nonzero(present).flatten().tolist()]
         return sorted(vals)
 
-    @staticmethod
-    def _buffer(buf, n, dtype, dev):
-        if buf is None or buf.numel() < n or buf.device != dev:
-            buf = torch.empty(max(n, 1) + max(n, 1) // 4, dtype=dtype, device=dev)
-        return buf
+    def _agree(self, vals):
+        t = torch.tensor(vals, dtype=torch.int64, device=self.ops.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return [int(x) for x in t.tolist()]
+
+    def _cap_for(self, need):
+        return int(need * self.CAP_SLACK) + 4096
+
+    def _buffers(self, cap):
+        n = self.world * (cap + 1)
+        if self._bufs.get("n", 0) < n:
+            self._bufs = {"n": n, "send": self.ops.alloc(n, torch.int64), "recv": self.ops.alloc(n, torch.int64),
+                          "flags": self.ops.alloc(n, torch.uint8), "back": self.ops.alloc(n, torch.uint8)}
+        return [self._bufs[k][:n] for k in ("send", "recv", "flags", "back")]
 
     def step(self, batch, call_prio, serial_base):
-        """batch = (Batch, new_bits, call_new) for this rank's calls."""
+        """batch: what ops.send takes for this rank's calls (GpuShardOps: the
+        (Batch, new_bits, call_new) triple of Device.batch).  Returns
+        (new_bits, call_new, stats)."""
         levels = self.levels(call_prio)
         if len(levels) > 4:
             raise ValueError("sharded triage supports <= 4 distinct prios per batch (signalPrio gives 0..3)")
         if not levels:
             levels = [0]
-        send, token, counts = self.ops.partition(batch, serial_base, levels, self.world)
-        dev = send.device
-        cnt_out = torch.tensor(counts, dtype=torch.int64, device=dev)
-        cnt_in = torch.empty_like(cnt_out)
-        dist.all_to_all_single(cnt_in, cnt_out, group=self.group)
-        recv_counts = cnt_in.tolist()  # the step's one host sync: split sizes
-        nrecv = sum(recv_counts)
-        self._recv = self._buffer(self._recv, nrecv, torch.int64, dev)
-        recv = self._recv[:nrecv]
-        dist.all_to_all_single(recv, send, recv_counts, counts, group=self.group)
-        flags, st = self.ops.triage_records(self.shard, self.new_signal, recv, levels)
-        self._back = self._buffer(self._back, send.numel(), torch.uint8, dev)
-        back = self._back[: send.numel()]
-        dist.all_to_all_single(back, flags, counts, recv_counts, group=self.group)
-        new_bits, call_new = self.ops.unpartition(batch, token, back)
+        W, g = self.world, self.group
+        if self.cap is None:
+            # first step: a guess every rank agrees on (a step that overflows it
+            # is redone with what the sources counted)
+            self.cap = self._cap_for(self._agree([min(self.ops.records(batch) // (4 * W) + 1, 1 << 21)])[0])
+        for attempt in range(4):
+            cap = self.cap
+            send, recv, flags, back = self._buffers(cap)
+            self.ops.send(batch, serial_base, levels, W, cap, send, self._exact)
+            dist.all_to_all_single(recv, send, group=g)
+            self.ops.own(self.shard, self.new_signal, recv, W, cap, levels, flags)
+            dist.all_to_all_single(back, flags, group=g)
+            self.ops.back(batch, serial_base, send, W, cap, back)
+            st = self.ops.finish()  # the step's one host synchronisation
+            if not st["global_void"]:
+                break
+            # nothing was committed on any rank (every owner saw the same headers):
+            # agree on a cap for what the sources counted, a void source takes its
+            # exact path, and the step runs again
+            self.redos += 1
+            need, bad = self._agree([st["max_out"], 1 if st["src_void"] == 2 else 0])
+            if bad:  # a call's prio outside the agreed levels: an error on every rank alike
+                raise ValueError("sharded step: a call's prio is not among the step's levels")
+            self.cap = max(self.cap, self._cap_for(need)) if need > cap else self.cap
+            self._exact = st["src_void"] != 0
+        else:
+            raise RuntimeError("sharded step: still void after 4 attempts")
+        self._exact = False
+        if st["owners_void"]:
+            # owners whose records overflowed the LDS partitions skipped them:
+            # they redo them on the per-record path, the flags go back once more
+            self.fixups += 1
+            if (st["owners_void"] >> self.rank) & 1:
+                self.ops.own(self.shard, self.new_signal, recv, W, cap, levels, flags, True)
+            else:
+                flags.zero_()
+            dist.all_to_all_single(back, flags, group=g)
+            self.ops.back(batch, serial_base, send, W, cap, back)
+            st2 = self.ops.finish()
+            for k in ("inserted", "changed", "own_distinct"):
+                st[k] += st2[k]
+            st["new_pairs"] = st2["new_pairs"]
+        if not self._tightened:
+            # once: the cap this workload needs (all ranks agree on it)
+            self._tightened = True
+            need = self._agree([st["max_out"]])[0]
+            self.cap = min(self.cap, self._cap_for(need))
         st = dict(st)
-        st["sent"] = int(send.numel())
-        st["received"] = int(nrecv)
+        st["cap"] = cap
+        new_bits, call_new = self.ops.outputs(batch)
         return new_bits, call_new, st
 
 
@@ -187,7 +233,20 @@ def sharded_minimize(ops, ctx_off, elems, prios, group=None, hint_distinct=0):
     methods.  Every rank holds the corpus description (ctx_off); elems/prios
     need only hold its own range.  Returns (keep u8[nctx], survivors)."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    send, counts = ops.split(ctx_off, elems, prios, world, rank, world, hint_distinct)
+    err = None
+    try:
+        send, counts = ops.split(ctx_off, elems, prios, world, rank, world, hint_distinct)
+    except Exception as e:  # noqa: BLE001 -- re-raised on every rank below
+        err = e
+    # every rank agrees on the split's success before entering the exchange: a
+    # rank that raised alone would leave its peers blocked in all_to_all_single
+    dev = ctx_off.device if isinstance(ctx_off, torch.Tensor) else "cpu"
+    bad = torch.tensor([1 if err is not None else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=group)
+    if err is not None:
+        raise err
+    if int(bad.item()):
+        raise RuntimeError("sharded_minimize: the split failed on another rank")
     dev = send.device
     cnt_out = torch.tensor(counts, dtype=torch.int64, device=dev)
     cnt_in = torch.empty_like(cnt_out)

@@ -185,6 +185,10 @@ class Signal:
         newSignal of the batches since, if it was empty at the snapshot)."""
         check(self._e.L.syzsig_set_restore_keys(self._e.h, self.handle, src.handle, keys.handle))
 
+    def reserve(self, extra):
+        """Room for `extra` more elements (syzsig_set_reserve)."""
+        check(self._e.L.syzsig_set_reserve(self._e.h, self.handle, int(extra)))
+
     def equal(self, other):
         """Same capacity, length and slot words (a snapshot check)."""
         eq = ctypes.c_int(0)
@@ -324,6 +328,12 @@ def check_new_signal(max_signal, new_signal, calls, eng=None, want_bits=False):
     return (idx, bits[: (sigs.size + 31) // 32]) if want_bits else idx
 
 
+# limits of one syzsig_manager_poll_batch call (csrc/poll.hip kPollMax*)
+POLL_MAX_TARGETS = (1 << 24) - 2
+POLL_MAX_NEXT = 1 << 28
+POLL_MAX_FANOUT = 1 << 31
+
+
 def manager_poll(max_signal, new_max, polls, eng=None):
     """syz-manager/manager.go:1027-1052 Manager.Poll for a batch of polls, in
     order: polls = [(fuzzer index, Serial a.MaxSignal)], new_max = every
@@ -332,6 +342,22 @@ def manager_poll(max_signal, new_max, polls, eng=None):
     Returns each poll's reply r.MaxSignal as a Serial (empty if none)."""
     eng = eng or max_signal._e
     F, K = len(new_max), len(polls)
+    lens = [np.asarray(s.Elems).size for _, s in polls]
+    # one library call holds at most POLL_MAX_NEXT polls x fuzzers and
+    # POLL_MAX_FANOUT entries x fuzzers (include/syzsig.h): a larger batch is
+    # applied as consecutive sub-batches, which is the same sequential loop
+    cuts, k0, n_acc = [], 0, 0
+    for k in range(K):
+        if k > k0 and ((k + 1 - k0) * F > POLL_MAX_NEXT or (n_acc + lens[k]) * F > POLL_MAX_FANOUT
+                       or (k + 1 - k0) + F > POLL_MAX_TARGETS):
+            cuts.append((k0, k))
+            k0, n_acc = k, 0
+        n_acc += lens[k]
+    if cuts:
+        out = []
+        for a, z in cuts + [(k0, K)]:
+            out += manager_poll(max_signal, new_max, polls[a:z], eng)
+        return out
     pf = np.array([int(f) for f, _ in polls], dtype=np.uint32)
     lens = np.array([np.asarray(s.Elems).size for _, s in polls], dtype=np.uint64)
     for _, s in polls:

@@ -20,115 +20,172 @@ from tests.test_gpu_minimize_shard import _owner
 SER = 0xFFFFFF
 
 
-class NumpyShardOps:
-    def partition(self, batch, serial_base, levels, nshards):
+HDR_VOID, HDR_OVF, HDR_COUNT = 1 << 63, 1 << 62, (1 << 40) - 1
+
+
+class NumpyStepOps:
+    """The stream-ordered sharded step of csrc (syzsig_step_send_dev /
+    _own_dev / _back_dev / _finish) restated over torch CPU tensors: buckets of
+    cap + 1 words per owner with a header (count | VOID | OVF), the owner's
+    records-mode replay in serial order, a status byte per flags bucket.
+    stair=True: each element's staircase is sent (agg.hip), else every record.
+    fail_owner: this rank's first non-exact owner pass skips its records
+    (status 2), as an LDS partition overflow would."""
+
+    device = "cpu"
+
+    def __init__(self, rank, stair=True, fail_owner=False):
+        self.rank, self.stair, self.fail_owner = rank, stair, fail_owner
+        self.pairs = set()
+        self.st = {}
+
+    @staticmethod
+    def alloc(n, dtype):
+        return torch.zeros(n, dtype=dtype)
+
+    @staticmethod
+    def records(batch):
+        return int(batch["sigs"].size)
+
+    def send(self, batch, serial_base, levels, nshards, cap, send, exact=False):
         sigs, cs, cl, prio = batch["sigs"], batch["call_start"], batch["call_len"], batch["call_prio"]
         lvl = {(v & 0xFF): i for i, v in enumerate(levels)}
-        recs, owners, pos_of = [], [], []
-        for c in range(cl.size):
-            for j in range(int(cl[c])):
-                e = int(sigs[int(cs[c]) + j])
-                recs.append((e << 32) | (lvl[int(prio[c])] << 24) | ((serial_base + c) & SER))
-                owners.append(_owner(e, nshards))
-                pos_of.append(int(cs[c]) + j)
-        order = sorted(range(len(recs)), key=lambda i: owners[i])
-        send = np.array([recs[i] for i in order], dtype=np.uint64).view(np.int64)
-        send_pos = np.zeros(sigs.size, np.int64)
-        for k, i in enumerate(order):
-            send_pos[pos_of[i]] = k
-        counts = [owners.count(g) for g in range(nshards)]
-        return torch.from_numpy(send.copy()), send_pos, counts
-
-    def triage_records(self, shard, new_signal, recs, levels):
-        r = recs.numpy().view(np.uint64)
-        flags = np.zeros(r.size, np.uint8)
-        by_k = {}
-        for i, x in enumerate(r):
-            by_k.setdefault(int(x) & SER, []).append(i)
-        for k in sorted(by_k):
-            upd = {}
-            for i in by_k[k]:
-                e, p = int(r[i]) >> 32, levels[(int(r[i]) >> 24) & 0xFF]
-                if e not in shard or p > shard[e]:
-                    flags[i] = 1
-                    upd[e] = max(p, upd.get(e, -999))
-            for e, p in upd.items():
-                shard[e] = p
-                new_signal[e] = max(p, new_signal.get(e, -999))
-        return torch.from_numpy(flags), {"records": int(r.size)}
-
-    def unpartition(self, batch, send_pos, back):
-        b = back.numpy()
-        bits = np.array([b[send_pos[i]] for i in range(send_pos.size)], np.uint8)
-        cs, cl = batch["call_start"], batch["call_len"]
-        cnew = np.array([bits[int(cs[c]): int(cs[c]) + int(cl[c])].any() for c in range(cl.size)], np.uint8)
-        return bits, cnew
-
-
-class NumpyStairOps(NumpyShardOps):
-    """The aggregated routing of agg.hip restated: per element, the first call
-    at each level; only the staircase (a level's first call precedes every
-    higher level's) is sent; flags come back as (call, elem) pairs."""
-
-    def partition(self, batch, serial_base, levels, nshards):
-        sigs, cs, cl, prio = batch["sigs"], batch["call_start"], batch["call_len"], batch["call_prio"]
-        lvl = {(v & 0xFF): i for i, v in enumerate(levels)}
+        groups = [[] for _ in range(nshards)]
         first = {}
         for c in range(cl.size):
             lv = lvl[int(prio[c])]
             for j in range(int(cl[c])):
-                f = first.setdefault(int(sigs[int(cs[c]) + j]), [None] * 4)
-                if f[lv] is None:
-                    f[lv] = c
-        groups = [[] for _ in range(nshards)]
+                e = int(sigs[int(cs[c]) + j])
+                if not self.stair:
+                    groups[_owner(e, nshards)].append((e << 32) | (lv << 24) | ((serial_base + c) & SER))
+                else:
+                    f = first.setdefault(e, [None] * 4)
+                    if f[lv] is None:
+                        f[lv] = c
         for e, f in first.items():
-            mk = None
+            mk, recs = None, []
             for lv in range(3, -1, -1):
                 if f[lv] is not None and (mk is None or f[lv] < mk):
                     mk = f[lv]
-                    groups[_owner(e, nshards)].append((e << 32) | (lv << 24) | ((serial_base + f[lv]) & SER))
-        send = np.array([r for g in groups for r in g], dtype=np.uint64)
-        return torch.from_numpy(send.view(np.int64).copy()), (send, serial_base), [len(g) for g in groups]
+                    recs.append((e << 32) | (lv << 24) | ((serial_base + f[lv]) & SER))
+            groups[_owner(e, nshards)] += recs[::-1]  # serial order, as k_stair_bucket writes them
+        mx = max(len(x) for x in groups)
+        sv = send.numpy().view(np.uint64)
+        for g, recs in enumerate(groups):
+            base = g * (cap + 1)
+            sv[base] = len(recs) | (HDR_OVF if mx > cap else 0)
+            for k, r in enumerate(recs[:cap]):
+                sv[base + 1 + k] = r
+        self.pairs = set()
+        self.st = {"src_void": 0, "global_void": 0, "owners_void": 0, "records": int(sigs.size),
+                   "sent": sum(len(x) for x in groups), "max_out": mx, "inserted": 0, "changed": 0,
+                   "own_distinct": 0, "new_pairs": 0}
 
-    def unpartition(self, batch, token, back):
-        send, serial_base = token
-        pairs = {((int(send[i]) & SER) - serial_base, int(send[i]) >> 32) for i in np.nonzero(back.numpy())[0]}
+    def own(self, shard, new_signal, recv, nshards, cap, levels, flags, exact=False):
+        rv = recv.numpy().view(np.uint64)
+        fl = flags.numpy()
+        fl[:] = 0
+        hdr = [int(rv[g * (cap + 1)]) for g in range(nshards)]
+        status = 0
+        if any(h & (HDR_VOID | HDR_OVF) for h in hdr):
+            status = 1
+        elif self.fail_owner and not exact:
+            self.fail_owner = False
+            status = 2
+        else:
+            by_k = {}
+            for g in range(nshards):
+                for j in range(min(hdr[g] & HDR_COUNT, cap)):
+                    i = g * (cap + 1) + 1 + j
+                    by_k.setdefault(int(rv[i]) & SER, []).append(i)
+            seen, changed, inserted = set(), set(), set()
+            for k in sorted(by_k):
+                upd = {}
+                for i in by_k[k]:
+                    e, p = int(rv[i]) >> 32, levels[(int(rv[i]) >> 24) & 0xFF]
+                    seen.add(e)
+                    if e not in shard or p > shard[e]:
+                        fl[i] = 1
+                        upd[e] = max(p, upd.get(e, -999))
+                for e, p in upd.items():
+                    if e not in shard:
+                        inserted.add(e)
+                    changed.add(e)
+                    shard[e] = p
+                    new_signal[e] = max(p, new_signal.get(e, -999))
+            self.st["own_distinct"] += len(seen)
+            self.st["inserted"] += len(inserted)
+            self.st["changed"] += len(changed)
+        for g in range(nshards):
+            fl[g * (cap + 1)] = status
+
+    def back(self, batch, serial_base, send, nshards, cap, back):
+        sv, bk = send.numpy().view(np.uint64), back.numpy()
+        for g in range(nshards):
+            base = g * (cap + 1)
+            if bk[base] == 1:
+                self.st["global_void"] = 1
+                continue
+            if bk[base] == 2:
+                self.st["owners_void"] |= 1 << g
+                continue
+            for j in range(min(int(sv[base]) & HDR_COUNT, cap)):
+                if bk[base + 1 + j]:
+                    r = int(sv[base + 1 + j])
+                    self.pairs.add(((r & SER) - serial_base, r >> 32))
+
+    def finish(self):
+        st = dict(self.st)
+        st["new_pairs"] = len(self.pairs)
+        self.st["global_void"] = self.st["owners_void"] = 0
+        self.st["inserted"] = self.st["changed"] = self.st["own_distinct"] = 0
+        return st
+
+    def outputs(self, batch):
         sigs, cs, cl = batch["sigs"], batch["call_start"], batch["call_len"]
         bits = np.zeros(sigs.size, np.uint8)
         cnew = np.zeros(cl.size, np.uint8)
         for c in range(cl.size):
             for j in range(int(cl[c])):
-                if (c, int(sigs[int(cs[c]) + j])) in pairs:
+                if (c, int(sigs[int(cs[c]) + j])) in self.pairs:
                     bits[int(cs[c]) + j] = 1
                     cnew[c] = 1
         return bits, cnew
 
 
-def make_rank_batch(rank, ncalls, seed):
+def make_rank_batch(rank, ncalls, seed, universe=300):
     rng = np.random.default_rng(seed + rank)
     cl = rng.integers(0, 40, size=ncalls).astype(np.uint32)
     cs = np.zeros(ncalls, np.uint64)
     cs[1:] = np.cumsum(cl[:-1])
-    sigs = rng.integers(0, 300, size=int(cl.sum())).astype(np.uint32)
+    sigs = rng.integers(0, universe, size=int(cl.sum())).astype(np.uint32)
     prio = rng.choice(np.array([0, 1, 2, 3], np.uint8), size=ncalls)
     return {"sigs": sigs, "call_start": cs, "call_len": cl, "call_prio": prio}
 
 
-def m0_global(seed):
+def m0_global(seed, universe=300):
     rng = np.random.default_rng(seed)
-    e = rng.choice(300, size=150, replace=False)
+    e = rng.choice(universe, size=universe // 2, replace=False)
     return {int(x): int(rng.integers(0, 4)) for x in e}
 
 
-def worker(rank, world, port, outdir, ncalls, seed, stair):
+def rank_calls(rank, ncalls, uneven):
+    """Calls of rank r: uneven loads give later ranks more calls."""
+    return ncalls + (25 * rank if uneven else 0)
+
+
+def worker(rank, world, port, outdir, ncalls, seed, stair, uneven, cap, fail_rank):
     from syzkaller_amd.dist import ShardedTriage
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    batch = make_rank_batch(rank, ncalls, seed)
+    batch = make_rank_batch(rank, rank_calls(rank, ncalls, uneven), seed)
+    base = sum(rank_calls(r, ncalls, uneven) for r in range(rank))
     shard = {e: p for e, p in m0_global(seed).items() if _owner(e, world) == rank}
     news = {}
-    st = ShardedTriage(NumpyStairOps() if stair else NumpyShardOps(), shard, news)
-    bits, cnew, stats = st.step(batch, torch.from_numpy(batch["call_prio"]), rank * ncalls)
+    ops = NumpyStepOps(rank, stair, fail_owner=rank == fail_rank)
+    st = ShardedTriage(ops, shard, news, cap=cap, levels=[0, 1, 2, 3])
+    bits, cnew, stats = st.step(batch, torch.from_numpy(batch["call_prio"]), base)
+    stats.update(redos=st.redos, fixups=st.fixups, cap_after=st.cap)
     json.dump({"bits": bits.tolist(), "cnew": cnew.tolist(), "shard": shard, "new": news, "stats": stats},
               open(os.path.join(outdir, f"r{rank}.json"), "w"))
     dist.destroy_process_group()
@@ -142,19 +199,26 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("stair", [False, True])
-@pytest.mark.parametrize("seed", [1, 2])
-def test_sharded_step_equals_sequential_checknewsignal(seed, stair):
-    """stair: route only each element's staircase (the aggregated routing)."""
+@pytest.mark.parametrize("world,stair,uneven,cap,fail_rank,seed", [
+    (2, False, False, None, -1, 1), (2, True, False, None, -1, 2),
+    (2, True, True, 4, -1, 3),       # a cap of 4 records: every bucket overflows, the step is redone
+    (4, True, True, None, -1, 4),
+    (4, True, True, None, 2, 5),     # owner 2 skips its records (LDS overflow): the fix-up round
+    (4, False, True, 16, 1, 6),      # every record routed, both a redo and a fix-up
+])
+def test_sharded_step_equals_sequential_checknewsignal(world, stair, uneven, cap, fail_rank, seed):
+    """The stream-ordered sharded step (dist.ShardedTriage over gloo, the device
+    half restated in numpy) against sequential checkNewSignal over the whole
+    rank-major batch (syz-fuzzer/fuzzer.go:494-511): bits, call flags, the
+    union of the shards and of the newSignal shards."""
     from oracle import oracle as O
 
-    world, ncalls = 2, 60
+    ncalls = 40
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(worker, args=(world, free_port(), d, ncalls, seed, stair), nprocs=world,
-                           start_method="spawn")
+        mp.start_processes(worker, args=(world, free_port(), d, ncalls, seed, stair, uneven, cap, fail_rank),
+                           nprocs=world, start_method="spawn")
         res = [json.load(open(os.path.join(d, f"r{r}.json"))) for r in range(world)]
-    # sequential reference over the concatenated batch (rank-major serial order)
-    parts = [make_rank_batch(r, ncalls, seed) for r in range(world)]
+    parts = [make_rank_batch(r, rank_calls(r, ncalls, uneven), seed) for r in range(world)]
     sigs = np.concatenate([p["sigs"] for p in parts])
     off, cs = 0, []
     for p in parts:
@@ -178,9 +242,11 @@ def test_sharded_step_equals_sequential_checknewsignal(seed, stair):
     for r in res:
         nm.update({int(k): v for k, v in r["new"].items()})
     assert nm == ns.to_dict()
-    sent = sum(r["stats"]["sent"] for r in res)
-    assert sent == sum(r["stats"]["received"] for r in res)
-    assert sent < sigs.size if stair else sent == sigs.size
+    st = [r["stats"] for r in res]
+    assert all(x["redos"] == (1 if cap is not None else 0) for x in st), st  # a small cap: one redo
+    assert all(x["fixups"] == (1 if fail_rank >= 0 else 0) for x in st), st
+    assert sum(x["changed"] for x in st) == len(ns.to_dict())
+    assert all(x["cap_after"] == st[0]["cap_after"] for x in st)  # every rank agrees on the cap
 
 
 # ---- Minimize sharded by element (dist.sharded_minimize) ----
@@ -298,3 +364,39 @@ def test_minimize_split_restatement_parts_cover_corpus(nparts):
         recv = torch.cat([s[g * 0 + sum(c[:g]): sum(c[: g + 1])] for s, c in sends])
         keep |= ops.resolve(off, recv).numpy()
     assert np.nonzero(keep)[0].tolist() == O.minimize(off, elems, prios)
+
+
+class FailingMinimizeOps(NumpyMinimizeOps):
+    """split raises on rank 1 only (as syzsig_minimize_split_dev can with
+    ERANGE on a send buffer too small for its part)."""
+
+    def split(self, off, elems, prios, nparts, part, nshards, hint_distinct=0):
+        if part == 1:
+            raise ValueError("split failed on part 1")
+        return super().split(off, elems, prios, nparts, part, nshards, hint_distinct)
+
+
+def failing_minimize_worker(rank, world, port, outdir):
+    from syzkaller_amd.dist import sharded_minimize
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    off, elems, prios = _corpus(7)
+    try:
+        sharded_minimize(FailingMinimizeOps(), off, elems, prios)
+        msg = None
+    except Exception as e:  # noqa: BLE001
+        msg = f"{type(e).__name__}: {e}"
+    json.dump({"err": msg}, open(os.path.join(outdir, f"f{rank}.json"), "w"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_sharded_minimize_split_failure_raises_on_every_rank():
+    """A split that fails on one rank makes every rank raise before the
+    all-to-all instead of leaving the others blocked in it."""
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(failing_minimize_worker, args=(world, free_port(), d), nprocs=world, start_method="spawn")
+        res = [json.load(open(os.path.join(d, f"f{r}.json")))["err"] for r in range(world)]
+    assert res[1] == "ValueError: split failed on part 1"
+    assert res[0] and res[2] and "another rank" in res[0] and "another rank" in res[2]

@@ -30,25 +30,25 @@ def _port():
     return p
 
 
-def worker(rank, world, port, outdir):
+def worker(rank, world, port, outdir, want_bits, cap):
     import torch
     import torch.distributed as dist
 
     from syzkaller_amd import signal as S
     from syzkaller_amd import synth
     from syzkaller_amd.device import Device
-    from syzkaller_amd.dist import GpuShardOps, ShardedTriage, owner_of_torch
+    from syzkaller_amd.dist import GpuShardOps, ShardedTriage
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     dev = Device(0)
+    dev.L.syzsig_ctx_set_timing(dev.eng.h, 1)
     cfg = synth.synth_default(skew=1)
-    ge, gp = dev.synth_m0(cfg, KNOWN, NM0)
-    own = owner_of_torch(ge, world) == rank
-    ms = dev.deserialize(ge[own].contiguous(), gp[own].contiguous())
-    ns = S.Signal(None, dev.eng)
+    se, sp = dev.synth_m0_shard(cfg, KNOWN, NM0, world, rank)  # this rank's shard of M0, in index order
+    ms = dev.deserialize(se, sp)
+    ns = S.Signal.make(1 << 16, dev.eng)
     ops = GpuShardOps(dev)
-    sh = ShardedTriage(ops, ms, ns)  # first step: levels agreed by all_reduce
+    sh = ShardedTriage(ops, ms, ns, cap=cap)  # first step: levels agreed by all_reduce
     out = {}
     for step in range(2):
         # batch `step`, rank r's programs: a contiguous range of the global, rank-major order
@@ -57,29 +57,40 @@ def worker(rank, world, port, outdir):
         pcs, cs, cl, prio = dev.synth_traces(cfg, p0, NPROG, CPP, cl)
         pidx = torch.arange(NPROG + 1, dtype=torch.int32, device=dev.dev) * CPP
         sigs, cnt, _ = dev.edge_derive(pcs, cs, cl, pidx)
-        b, bits, cnew = dev.batch(sigs, cs, cnt, prio, want_bits=True)
+        pairs = torch.full((int(cnt.to(torch.int64).sum()) + 1,), -1, dtype=torch.int64, device=dev.dev)
+        b, bits, cnew = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=want_bits)
         bits, cnew, st = sh.step((b, bits, cnew), prio, rank * NPROG * CPP)
         if step == 0:
             sh.fixed_levels = sh.levels(prio)  # later steps: no collective
+        out[f"redos{step}"] = np.array([sh.redos])
         torch.cuda.synchronize()
-        out[f"bits{step}"] = bits.cpu().numpy().view(np.uint32)
+        if want_bits:
+            out[f"bits{step}"] = bits.cpu().numpy().view(np.uint32)
         out[f"cnew{step}"] = cnew.cpu().numpy()
+        out[f"pairs{step}"] = pairs[: st["new_pairs"]].cpu().numpy().view(np.uint64)
         out[f"sent{step}"] = np.array([st["sent"], st["received"]])
     se = ms.Serialize()
     out["ms_e"], out["ms_p"] = se.Elems, se.Prios
     sn = ns.Serialize() if not ns.is_nil() else S.Serial()
     out["ns_e"], out["ns_p"] = sn.Elems, sn.Prios
+    out["redos"] = np.array([sh.redos, sh.fixups])
     np.savez(os.path.join(outdir, f"r{rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gpu_sharded_step_gloo_two_ranks():
+@pytest.mark.parametrize("want_bits,cap", [(True, None), (False, None), (False, 256)])
+def test_gpu_sharded_step_gloo_two_ranks(want_bits, cap):
+    """The stream-ordered step (syzsig_step_*: staircase buckets, equal-split
+    exchanges, the owners' LDS-partitioned replay, flags back) on the real
+    kernels, two ranks on one GPU over gloo, two consecutive batches; cap=256
+    overflows the first step's buckets, which is redone with a larger cap."""
+    from tests.test_gpu_triage import oracle_pairs
     from syzkaller_amd import synth
 
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(worker, args=(world, _port(), d), nprocs=world, start_method="spawn")
+        mp.start_processes(worker, args=(world, _port(), d, want_bits, cap), nprocs=world, start_method="spawn")
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     cfg = synth.synth_default(skew=1)
     m0e, m0p = synth.m0(cfg, KNOWN, NM0)
@@ -93,9 +104,16 @@ def test_gpu_sharded_step_gloo_two_ranks():
             sigs, cnt, _ = O.exec_batch(pcs, cs, cl, pidx)
             ons, obits, ocnew = O.triage_batch_into(oms, sigs, cs, cnt, prio, ons)
             np.testing.assert_array_equal(res[r][f"cnew{step}"], ocnew[: cnt.size])
-            np.testing.assert_array_equal(res[r][f"bits{step}"], obits[: (sigs.size + 31) // 32])
+            if want_bits:
+                np.testing.assert_array_equal(res[r][f"bits{step}"], obits[: (sigs.size + 31) // 32])
+            np.testing.assert_array_equal(np.sort(res[r][f"pairs{step}"]), oracle_pairs(sigs, cs, cnt, obits))
     assert sum(int(x[f"sent{s}"][0]) for x in res for s in range(2)) == \
         sum(int(x[f"sent{s}"][1]) for x in res for s in range(2))
+    # a fresh context's first step may void itself once (its distinct-ratio guess
+    # for the LDS partitions is learned by the exact redo); the second never does,
+    # and a 256-record cap always overflows the first
+    assert all(int(x["redos1"][0]) == int(x["redos0"][0]) for x in res)
+    assert all(int(x["redos0"][0]) >= (1 if cap else 0) for x in res)
     ge = np.concatenate([x["ms_e"] for x in res])
     gpr = np.concatenate([x["ms_p"] for x in res])
     oe, op = oms.Serialize()
@@ -153,3 +171,21 @@ def test_gpu_sharded_minimize_gloo_two_ranks():
     exp = O.minimize(off, e, p)
     for k in keeps:
         assert np.nonzero(k)[0].tolist() == exp
+
+
+@pytest.mark.parametrize("nshards", [1, 3, 8])
+def test_synth_m0_shard_equals_filtered_m0(gpu, nshards):
+    """syzsig_synth_m0_shard_dev (how a rank builds its shard of the 1B-element
+    M0) = synth_m0 filtered by owner_of, in index order."""
+    import torch
+
+    from syzkaller_amd import synth
+    from syzkaller_amd.dist import owner_of_torch
+
+    cfg = synth.synth_default()
+    n = 3_000_017
+    ge, gp = gpu.synth_m0(cfg, 2048, n)
+    own = owner_of_torch(ge, nshards)
+    for g in range(nshards):
+        e, p = gpu.synth_m0_shard(cfg, 2048, n, nshards, g)
+        assert torch.equal(e, ge[own == g]) and torch.equal(p, gp[own == g])

@@ -270,6 +270,30 @@ def test_minimize_data_split_equals_unsharded(gpu, nparts, nshards):
     assert all(sum(c) <= np.unique(e).size for _, c in sends)
 
 
+@pytest.mark.parametrize("case", ["many_prios", "forced_atomic"])
+@pytest.mark.parametrize("nparts,nshards", [(2, 2), (3, 5)])
+def test_minimize_data_split_atomic_fallback(gpu, case, nparts, nshards):
+    """A part with more than 4 distinct prios (any int8 is a valid prio:
+    signal.go:138-166) takes the split's per-entry atomicMax table instead of
+    failing (which would have left its peers blocked in the all-to-all);
+    forced_atomic runs that table on 0..3 prios.  Equal to the oracle."""
+    from syzkaller_amd._lib import SYZSIG_DEBUG_MIN_ATOMIC
+
+    rng = np.random.default_rng(90 + nparts)
+    off, e, p = corpus(rng, 2000, 100, 20000)
+    if case == "many_prios":
+        p = rng.integers(-4, 4, size=e.size).astype(np.int8)
+    t = lambda a, dt: torch.from_numpy(a.view(dt)).to(gpu.dev)  # noqa: E731
+    doff, de, dp = t(off, np.int64), t(e, np.int32), t(p, np.int8)
+    gpu.eng.set_debug(SYZSIG_DEBUG_MIN_ATOMIC if case == "forced_atomic" else 0)
+    try:
+        keep, sends = _split_emulated(gpu, doff, de, dp, nparts, nshards)
+    finally:
+        gpu.eng.set_debug(0)
+    assert np.nonzero(keep.cpu().numpy())[0].tolist() == O.minimize(off, e, p)
+    assert all(sum(c) <= np.unique(e).size for _, c in sends)
+
+
 def test_minimize_data_split_c3_eight_parts(gpu):
     """BASELINE config 3 (200k contexts, ~400M entries) split over 8 parts and
     8 owners on one GPU (the N=8 exchange emulated) against unsharded Minimize

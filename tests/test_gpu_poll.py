@@ -17,11 +17,17 @@ def _serial(rng, n, U, dup=True):
     return e, p
 
 
-@pytest.mark.parametrize("seed,F,K,U,n", [(0, 5, 40, 3000, 400), (1, 1, 8, 500, 100), (2, 16, 200, 50_000, 3000),
-                                          (3, 3, 30, 200, 50)])
-def test_poll_batch_vs_sequential_oracle(gpu, seed, F, K, U, n):
+@pytest.mark.parametrize("seed,F,K,U,n,limits", [(0, 5, 40, 3000, 400, None), (1, 1, 8, 500, 100, None),
+                                                 (2, 16, 200, 50_000, 3000, None), (3, 3, 30, 200, 50, None),
+                                                 (4, 5, 40, 3000, 400, (24, 4000))])
+def test_poll_batch_vs_sequential_oracle(gpu, monkeypatch, seed, F, K, U, n, limits):
+    """limits: (polls x fuzzers, entries x fuzzers) per library call lowered so
+    that signal.manager_poll applies the batch as several consecutive calls."""
     from syzkaller_amd import signal as S
 
+    if limits:
+        monkeypatch.setattr(S, "POLL_MAX_NEXT", limits[0])
+        monkeypatch.setattr(S, "POLL_MAX_FANOUT", limits[1])
     rng = np.random.default_rng(seed)
     m0 = _serial(rng, 4 * n, U, dup=False)
     pre = [None if rng.random() < 0.3 else _serial(rng, int(rng.integers(0, n)), U, dup=False) for _ in range(F)]

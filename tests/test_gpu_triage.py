@@ -292,6 +292,39 @@ def test_triage_agg_lds_overflow_fallback(gpu, over):
     assert st["overflow_parts"] == sum(over), st
 
 
+@pytest.mark.parametrize("big", [AGG_LIMIT + 300, 9 * AGG_LIMIT])
+def test_triage_one_sync_direct_pairs_lds_overflow(gpu, big):
+    """The one-sync run (want_bits=False) writing its pairs straight into the
+    caller's new_pairs (capacity 4 x 8 partitions x kAggLimit, the least that
+    path accepts) while one of its 8 partitions overflows the LDS table and is
+    committed from the HBM table after the sync: the pairs already written must
+    survive.  With 9 x kAggLimit elements in that partition the run's pairs no
+    longer all fit the caller's buffer, so they move to the workspace first."""
+    rng = np.random.default_rng(big)
+    per_part = 2 * big  # records of every partition alike, so that no capped cell spills
+    parts = []
+    for p in range(8):
+        n = big if p == 2 else 400
+        low = rng.choice(1 << 29, size=n, replace=False).astype(np.uint32)
+        e = fmix32_inv_np((np.uint32(p) << np.uint32(29)) | low)
+        parts.append(np.concatenate([e, rng.choice(e, size=per_part - n)]))
+    elems = np.concatenate(parts)
+    ncalls = 500
+    stream = rng.permutation(elems)
+    cuts = np.sort(rng.choice(np.arange(1, stream.size), size=ncalls - 1, replace=False))
+    hcs = np.concatenate([[0], cuts]).astype(np.uint64)
+    hcnt = np.diff(np.concatenate([hcs, [stream.size]])).astype(np.uint32)
+    hprio = rng.integers(0, 4, size=ncalls).astype(np.uint8)
+    hs = stream.astype(np.uint32)
+    m0e = np.unique(rng.choice(np.unique(elems), size=2000, replace=False))
+    m0p = rng.integers(0, 4, size=m0e.size).astype(np.int8)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(gpu.dev)  # noqa: E731
+    db = (t(hs, np.int32), t(hcs, np.int64), t(hcnt, np.int32), t(hprio, np.uint8))
+    st = compare(gpu, (m0e, m0p), (hs, hcs, hcnt, hprio), db, agg=2, parts=8, want_bits=False,
+                 pairs_cap=4 * 8 * AGG_LIMIT)
+    assert st["parts"] == 8 and st["overflow_parts"] == 1 and st["retries"] == 0, st
+
+
 @pytest.mark.parametrize("agg", [0, 2])
 def test_triage_overflow_retry(gpu, agg):
     """maxSignal starts as make(Signal) with 16 slots: the per-call path
@@ -408,21 +441,20 @@ def test_triage_c2_properties(gpu):
     assert int(cnew3.sum()) == 0 and int(bits3.count_nonzero()) == 0 and ns3.is_nil() and ms.Len() == n_before
 
 
-@pytest.mark.parametrize("agg,npool", [(1, 2_500_000), (0, 2_500_000), ("scan", 2_500_000), ("sel", 2_500_000),
-                                       (1, 200_000), ("sel", 200_000), ("sel", 20_000), ("scan", 20_000)])
+@pytest.mark.parametrize("agg,npool", [(1, 2_500_000), (0, 2_500_000), (1, 200_000), (1, 20_000), (1, 200)])
 def test_records_mode_vs_oracle(gpu, agg, npool):
     """Records mode (the owner side of a sharded step, triage.hip
     triage_records_impl): ~1.2M records (e, level, serial) in a shuffled order,
     each serial one call of up to 6 distinct elements at one level, against a
-    shard holding part of the pool.  agg=1 takes the sorted path (records
-    by (element, serial), one thread per compacted run head; "sel":
-    SYZSIG_DEBUG_RECS_SEL, sorted by the element bits only, each head selecting
-    its run's records in serial order; "scan": SYZSIG_DEBUG_RECS_SCAN, one
-    thread per sorted position), agg=0 the per-record probe path.  npool=200k
-    gives ~6 records per element; npool=20k ~60, with runs past the selection
-    walk's 64 (its redo with the full-key sort).  All must flag exactly the
-    records the oracle's sequential checkNewSignal over the calls in serial
-    order marks new, and leave the same shard and newSignal."""
+    shard holding part of the pool.  agg=1 takes the LDS-partitioned path
+    (recs.hip: records grouped by element hash, each partition sorted by
+    (element, serial) in LDS, one thread per element run), agg=0 the per-record
+    probe path.  npool=200k gives ~6 records per element, 20k ~60; npool=200
+    puts ~6000 records on each element, so partitions overflow the LDS
+    capacity and the run falls back to the per-record path before committing.
+    All must flag exactly the records the oracle's sequential checkNewSignal
+    over the calls in serial order marks new, and leave the same shard and
+    newSignal."""
     from syzkaller_amd import signal as S
 
     rng = np.random.default_rng(77)
@@ -448,21 +480,17 @@ def test_records_mode_vs_oracle(gpu, agg, npool):
     ns = S.Signal(None, gpu.eng)
     drec = torch.from_numpy(rec[perm].view(np.int64)).to(gpu.dev)
     flags = torch.zeros(nrec, dtype=torch.uint8, device=gpu.dev)
-    from syzkaller_amd._lib import SYZSIG_DEBUG_RECS_SCAN, SYZSIG_DEBUG_RECS_SEL
-
     gpu.eng.set_agg(0 if agg == 0 else 1, 0)
-    gpu.eng.set_debug({"scan": SYZSIG_DEBUG_RECS_SCAN, "sel": SYZSIG_DEBUG_RECS_SEL}.get(agg, 0))
     try:
         st = gpu.triage_records(ms, ns, drec, [0, 1, 2, 3], flags)
     finally:
         gpu.eng.set_agg(1, 0)
-        gpu.eng.set_debug(0)
     oms, ons, obits, _ = O.triage_batch(m0e, m0p, sigs, cs, clen, lvl)
     onew = np.unpackbits(obits.view(np.uint8), bitorder="little")[:nrec].astype(np.uint8)
     np.testing.assert_array_equal(_u(flags, np.uint8), onew[perm])
     assert ms.to_dict() == oms.to_dict()
     assert ns.to_dict() == ons.to_dict()
-    assert (st["distinct"] > 0) == (agg != 0), st  # the sorted path counts distinct elements
+    assert (st["parts"] > 0) == (agg != 0 and npool > 1000), st  # the LDS path reports its partitions
 
 
 def test_restore_keys_brings_back_the_snapshot(gpu):
