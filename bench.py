@@ -77,6 +77,7 @@ def parse():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 per-rank line")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 line")
     ap.add_argument("--no-gw", action="store_true", help="skip the C2 global-walk line")
+    ap.add_argument("--no-pipe", action="store_true", help="skip the K1+K2 -> K3 pipeline line")
     return ap.parse_args()
 
 
@@ -464,6 +465,56 @@ def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_
                          "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": nrec0, "avg_launch_ms": step}}
 
 
+def pipeline_line(dev, pairs, P, C, L, reps=3, m0=10_000_000):
+    """The per-execution path end to end on one C2 batch: raw KCOV traces in
+    HBM -> K1+K2 (executor write_coverage_signal + dedup, executor.h:492-512)
+    -> K3 (checkNewSignal over the batch, fuzzer.go:494-511; proc.go:230-247
+    calls one after the other), timed as one sequence with HIP events, maxSignal
+    back to M0 and newSignal cleared before each (outside the events)."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd import synth
+
+    cfg = synth.synth_default()
+    cl = torch.full((P * C,), L, dtype=torch.int32)
+    pcs, cs, cl, prio = dev.synth_traces(cfg, 0, P, C, cl)
+    pidx = torch.arange(P + 1, dtype=torch.int32, device=dev.dev) * C
+    sigs = torch.empty(pcs.numel(), dtype=torch.int32, device=dev.dev)
+    cnt = torch.empty(P * C, dtype=torch.int32, device=dev.dev)
+    comp = torch.empty(P, dtype=torch.int32, device=dev.dev)
+    m0e, m0p = dev.synth_m0(cfg, 2048, m0)
+    pristine = dev.deserialize(m0e, m0p)
+    del m0e, m0p
+    ms = pristine.clone()
+    ns = S.Signal.make(4_000_000, dev.eng)
+    b, _, _ = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
+    times, st = [], None
+    for r in range(reps + 1):
+        if ms.capacity() != pristine.capacity():
+            ms = pristine.clone()
+        else:
+            ms.copy_from(pristine)
+        ns.clear()
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        dev.edge_derive(pcs, cs, cl, pidx, sigs, cnt, comp)
+        st = dev.triage_b(ms, ns, b)
+        z.record()
+        torch.cuda.synchronize()
+        if r:
+            times.append(a.elapsed_time(z))
+    t = float(np.median(times))
+    npc = pcs.numel()
+    nrec = int(cnt.to(torch.int64).sum().item())
+    del pcs, sigs
+    return {"metric": "KCOV PCs -> checkNewSignal result per second (K1+K2 then K3 on one batch)",
+            "value": npc / (t * 1e-3), "unit": "PCs/s", "higher_is_better": True, "ms": t, "dtype": "u64->u32",
+            "records_per_s": nrec / (t * 1e-3),
+            "config": {"workload": f"BASELINE config 2 batch: {P} programs x {C} calls x {L} PCs from raw traces, "
+                                   f"vs a {m0}-element maxSignal",
+                       "pcs": npc, "records": nrec, "changed": st["changed"]}}
+
+
 def c1_line(dev, reps=20):
     """BASELINE config 1 (64 programs x 32 calls x 2k PCs): the reference's
     CPU-runnable case, FromRaw/DiffRaw+Merge per call (checkNewSignal,
@@ -786,6 +837,8 @@ def main():
         out["lines"]["minimize"] = minimize_line(dev, a.min_contexts)
     if rank == 0 and world == 1 and not a.no_c5:
         out["lines"]["c5"] = c5_line(dev, pairs)
+    if rank == 0 and world == 1 and not a.no_pipe:
+        out["lines"]["pipeline"] = pipeline_line(dev, pairs, P, C, L)
     if rank == 0 and world == 1 and not a.no_gw:
         out["lines"]["c2_global_walk"] = c2_global_walk_line(dev, pairs, P, C, L)
     if rank == 0 and world == 1 and not a.no_c1:

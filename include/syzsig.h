@@ -362,7 +362,8 @@ int syzsig_shard_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t 
                                uint64_t* d_send, uint32_t* d_send_pos, uint64_t* send_counts);
 /* Owner side: triage received records against the local shard of maxSignal;
  * d_new_flags[i] = 1 iff received record i is new (checkNewSignal's DiffRaw
- * result for its call).  Serial order comes from the records' serial fields. */
+ * result for its call).  Serial order comes from the records' serial fields;
+ * records with one serial are one call's, so they carry one level. */
 int syzsig_triage_records_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set** new_signal,
                               const uint64_t* d_recs, uint64_t nrec, const int8_t* levels,
                               uint32_t nlevels, uint8_t* d_new_flags, syzsig_batch_stats* stats);

@@ -2970,6 +2970,11 @@ __global__ __launch_bounds__(256) void k_step_back(const uint64_t* __restrict__ 
 		}
 		return;
 	}
+	// one device atomic per block and pass (a per-wave atomic on the one
+	// counter serialised the kernel: 176 us at C4)
+	__shared__ uint32_t wcnt[4];
+	__shared__ unsigned long long s_base;
+	const uint32_t w = threadIdx.x >> 6;
 	const uint64_t n = min<uint64_t>(send[s0] & SYZSIG_STEP_HDR_COUNT, cap);
 	for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += (uint64_t)gridDim.x * blockDim.x) {
 		const uint64_t i = i0 + threadIdx.x;
@@ -2982,12 +2987,21 @@ __global__ __launch_bounds__(256) void k_step_back(const uint64_t* __restrict__ 
 			v = (c << 32) | (r >> 32);
 		}
 		const uint64_t m = __ballot(on);
-		unsigned long long wb = 0;
-		if (lane == 0 && m)
-			wb = atomicAdd(&bc[kCntAux2], (unsigned long long)__popcll(m));
-		wb = __shfl(wb, 0, 64);
-		if (on && pairs && wb + lane_rank(m) < pairs_cap)
-			pairs[wb + lane_rank(m)] = v;
+		if (lane == 0)
+			wcnt[w] = (uint32_t)__popcll(m);
+		__syncthreads();
+		uint32_t before = 0, tot = 0;
+		for (uint32_t k = 0; k < 4; k++) {
+			before += k < w ? wcnt[k] : 0;
+			tot += wcnt[k];
+		}
+		if (threadIdx.x == 0)
+			s_base = tot ? atomicAdd(&bc[kCntAux2], (unsigned long long)tot) : 0;
+		__syncthreads();
+		const uint64_t o = s_base + before + lane_rank(m);
+		if (on && pairs && o < pairs_cap)
+			pairs[o] = v;
+		__syncthreads();  // wcnt / s_base are rewritten by the next pass
 	}
 }
 

@@ -298,6 +298,8 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 	const int grid = (int)std::min<uint64_t>(nprog, 256 * 4);
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
+#ifdef SYZ_EXPERIMENTS
+	// measured slower: 8 waves 25 ms, 2 waves 16.1, 1 wave 21.3 vs 4 waves 14.9 at C2
 	if (ctx->edge_waves == 8)
 		k_edge_dedup<8><<<grid, 512, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
@@ -308,6 +310,7 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 		k_edge_dedup<1><<<grid, 64, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                              nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	else
+#endif
 		k_edge_dedup<4><<<grid, 256, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());

@@ -338,6 +338,30 @@ __device__ __forceinline__ int64_t tbl_lookup(const uint64_t* __restrict__ slots
 	return -1;
 }
 
+// tbl_lookup with the home bucket already loaded (B = load_bucket of
+// home_bucket(key)), so that a thread can issue several tables' home-bucket
+// loads before it waits for any.
+__device__ __forceinline__ int64_t tbl_lookup_from(const uint64_t* __restrict__ slots, uint64_t bmask, uint32_t key,
+                                                   uint64_t& val, Bucket B)
+{
+	uint64_t b = home_bucket(key, bmask);
+	for (uint64_t n = 0; n <= bmask; n++) {
+		if (n)
+			B = load_bucket(slots + (b << kBucketShift));
+#pragma unroll
+		for (int i = 0; i < (int)kBucketSlots; i++) {
+			if (B.s[i] == kSlotEmpty)
+				return -1;
+			if (slot_key(B.s[i]) == key) {
+				val = B.s[i];
+				return (int64_t)((b << kBucketShift) + i);
+			}
+		}
+		b = (b + 1) & bmask;
+	}
+	return -1;
+}
+
 // Find `key`, inserting `ins` (a slot word for `key`) at the first empty slot
 // if absent.  old = previous word (0 when this call inserted).  Returns -1
 // when max_probe buckets were scanned without success (overflow).

@@ -10,8 +10,8 @@
 // call, signal.go:90-102); the final m, if it rose, is merged into the shard
 // and newSignal (signal.go:117-131).
 //
-// So the records only need grouping by element, and each group ordering by
-// serial.  Instead of a device-wide sort:
+// So the records only need grouping by element (not even ordering: see
+// k_rp_agg).  Instead of a device-wide sort:
 //   k_rp_count    tiles of the record buffer: per partition counts, where the
 //                 partition is the top pbits of h = fmix32(e) -- the shard's
 //                 home-bucket bits, so one partition probes one slice of it
@@ -21,9 +21,10 @@
 //                 voids the run (the gate) before anything is committed
 //   k_rp_scatter  key = h_residual << 39 | serial << 15 | level << 13 | local
 //                 position, and the record's buffer index beside it
-//   k_rp_triage   one workgroup per partition: its keys into LDS, a bitonic
-//                 sort (element, serial), the run heads compacted, one thread
-//                 per element run: one shard probe, the replay, flags, merge.
+//   k_rp_agg / k_rp_elems / k_rp_flags
+//                 per partition an LDS hash of its elements with their level
+//                 firsts; per element one shard probe and the merges; per
+//                 record its flag in closed form (no ordering: see k_rp_agg).
 // No device-scope atomics per record (those run at ~20 G/s chip-wide).
 #include <algorithm>
 #include <vector>
@@ -32,15 +33,15 @@
 
 namespace syz {
 
-constexpr uint32_t kRpCap = 8192;       // records of one partition in LDS (13-bit local positions)
-constexpr uint32_t kRpTarget = 2560;    // partitions are sized for this mean
+constexpr uint32_t kRpCap = 2048;       // records of one partition in LDS (local positions < 2^13)
+constexpr uint32_t kRpTarget = 1024;    // partitions are sized for this mean
 constexpr uint32_t kRpMinBits = 7;      // h residuals of <= 25 bits fit the key
 constexpr uint32_t kRpMaxBits = 13;     // <= 32 KB of LDS counters per tile
 constexpr uint32_t kRpTileMin = 16384;  // slots per counting / scatter tile (more for big inputs: <= ~1024 tiles)
 constexpr uint32_t kRpTileThreads = 512;
 constexpr uint32_t kRpGroups = 16;      // tile groups of the column scans
-constexpr uint32_t kRpThreads = 1024;
-constexpr uint64_t kRpPosMask = kRpCap - 1;
+constexpr uint32_t kRpThreads = 256;    // k_rp_agg: 8 records per thread
+constexpr uint64_t kRpPosMask = 8191;    // the key's 13 position bits
 
 // Where the records are: segment g's cnt[g] records at recs[g * stride + hdr ...].
 struct RpSrc {
@@ -214,104 +215,239 @@ __global__ __launch_bounds__(kRpTileThreads) void k_rp_scatter(RpSrc s, uint32_t
 	}
 }
 
-// The LDS of one partition's workgroup: keys (sorted in place) and the
-// compacted run heads.
-struct RpLds {
-	uint64_t key[kRpCap];
-	uint16_t head[kRpCap];
-	uint32_t nh;
-};
-
 struct RpTables {
 	uint64_t *ms, ms_bmask, *ns, ns_bmask;
 };
 
-__global__ __launch_bounds__(kRpThreads) void k_rp_triage(const uint64_t* __restrict__ keys,
-                                                          const uint32_t* __restrict__ idx,
-                                                          const uint32_t* __restrict__ base, uint32_t pbits,
-                                                          LevelMap lm, RpTables tb, uint8_t* flags,
-                                                          unsigned long long* ctr)
+// Element e's records need no ordering.  With first[l] = the smallest serial
+// among e's records at level l, replaying checkNewSignal over them in serial
+// order from m = M0[e] flags record (s, l) exactly when
+//     prio(l) > M0[e]  and  first[l] == s  and  first[l'] > s for every l' > l
+// (m before serial s is the max of M0 and the prios of the serials before s,
+// and a serial is one call, so one level; duplicates of an element in one call
+// share (s, l) and are flagged together, as DiffRaw collapses them), and the
+// final prio is max(M0[e], the top level present).  So the owner side is the
+// K3 aggregation again, without its scatter pass (the records arrive grouped
+// by partition from k_rp_scatter), in three kernels:
+//   k_rp_agg    one workgroup per partition: an LDS hash of its elements (the h
+//               residual) with the level firsts (ds_min), its distinct
+//               elements written out at the partition's own offset (no
+//               allocation atomics: a partition has at most as many elements
+//               as records), and every record's element index;
+//   k_rp_elems  one thread per element, thousands in flight (the dependent
+//               shard probe and merges are latency chains that a
+//               partition-resident workgroup could only overlap ~80 at a time):
+//               M0[e], the merges, M0 kept for the flags;
+//   k_rp_flags  one thread per record: the closed form above.
+constexpr uint32_t kRpEmpty = 0xFFFFFFFFu;
+constexpr int16_t kRpAbsent = -32768;  // elem_m0 of an element absent from the shard
+
+struct RpElems {
+	uint32_t* e;      // element
+	uint4* f;         // level firsts (kSerialMask + 1 = none)
+	int16_t* m0;      // M0[e] (kRpAbsent: absent)
+	uint32_t* rec_el; // per partitioned record: its element's index
+	uint32_t* ecnt;   // per partition: elements
+};
+
+struct RpAggLds {
+	uint32_t key[kRpCap];
+	uint32_t fl[4][kRpCap];
+	uint16_t rank[kRpCap];
+	uint32_t wsum[kRpThreads / 64];
+};
+static_assert(sizeof(RpAggLds) <= 160 * 1024 / 3 - 64, "three workgroups per CU");
+
+__global__ __launch_bounds__(kRpThreads) void k_rp_agg(const uint64_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ base, uint32_t pbits, RpElems el,
+                                                       const unsigned long long* ctr)
 {
-	__shared__ RpLds L;
+	__shared__ RpAggLds L;
 	if (rp_gated(ctr))
 		return;
-	const uint32_t p = blockIdx.x, tid = threadIdx.x;
+	constexpr uint32_t kPer = kRpCap / kRpThreads;
+	const uint32_t p = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
 	const uint32_t b0 = base[p], n = base[p + 1] - b0;
-	uint64_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0, distinct = 0;
-	if (n) {
-		uint32_t N = 64;
-		while (N < n)
-			N <<= 1;
-		if (tid == 0)
-			L.nh = 0;
-		for (uint32_t i = tid; i < N; i += kRpThreads)
-			L.key[i] = i < n ? keys[b0 + i] : ~0ull;
-		__syncthreads();
-		// bitonic sort of N keys, ascending (element, serial, level, position)
-		for (uint32_t k = 2; k <= N; k <<= 1) {
-			for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-				for (uint32_t t = tid; t < N / 2; t += kRpThreads) {
-					const uint32_t i = 2 * t - (t & (j - 1)), l = i + j;
-					const uint64_t a = L.key[i], b = L.key[l];
-					if ((a > b) == ((i & k) == 0)) {
-						L.key[i] = b;
-						L.key[l] = a;
-					}
-				}
-				__syncthreads();
-			}
-		}
-		// run heads: the first position of each element
-		for (uint32_t i0 = 0; i0 < n; i0 += kRpThreads) {
-			const uint32_t i = i0 + tid;
-			const bool hd = i < n && (i == 0 || (L.key[i] >> 39) != (L.key[i - 1] >> 39));
-			const uint64_t m = __ballot(hd);
-			uint32_t wb = 0;
-			if (lane_id() == 0 && m)
-				wb = atomicAdd(&L.nh, (uint32_t)__popcll(m));
-			wb = __shfl(wb, 0, 64);
-			if (hd)
-				L.head[wb + lane_rank(m)] = (uint16_t)i;
-		}
-		__syncthreads();
-		const uint32_t nh = L.nh, hp = p << (32 - pbits);
-		for (uint32_t t = tid; t < nh; t += kRpThreads) {
-			const uint32_t i = L.head[t];
-			const uint32_t hr = (uint32_t)(L.key[i] >> 39);
-			const uint32_t e = fmix32_inv(hp | hr);
-			distinct++;
-			uint64_t v = 0;
-			const bool present = tbl_lookup(tb.ms, tb.ms_bmask, e, v) >= 0 && slot_live(v);
-			const int m0 = present ? (int)slot_prio(v) : -1000;  // absent: below every prio (signal.go:93-95)
-			int m = m0;
-			uint32_t last_new = 0xFFFFFFFFu;
-			for (uint32_t j = i; j < n; j++) {
-				const uint64_t kj = L.key[j];
-				if ((uint32_t)(kj >> 39) != hr)
+	for (uint32_t i = tid; i < kRpCap; i += kRpThreads) {
+		L.key[i] = kRpEmpty;
+		L.fl[0][i] = L.fl[1][i] = L.fl[2][i] = L.fl[3][i] = kSerialMask + 1;
+	}
+	__syncthreads();
+	uint32_t sl[kPer];
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; k++) {
+		const uint32_t i = k * kRpThreads + tid;
+		sl[k] = 0;
+		if (i < n) {
+			const uint64_t x = keys[b0 + i];
+			const uint32_t hr = (uint32_t)(x >> 39);
+			// linear probing (h is already mixed; the residual's width depends
+			// on pbits, so its low bits); never full: n <= kRpCap
+			uint32_t s0 = hr & (kRpCap - 1);
+			for (;;) {
+				const uint32_t cur = L.key[s0];
+				if (cur == hr)
 					break;
-				const uint32_t ser = (uint32_t)(kj >> 15) & kSerialMask;
-				const int pr = lm.val[(kj >> 13) & 3];
-				if (pr > m || ser == last_new) {
-					flags[idx[b0 + (kj & kRpPosMask)]] = 1;
-					m = max(m, pr);
-					last_new = ser;
+				if (cur == kRpEmpty) {
+					const uint32_t old = atomicCAS(&L.key[s0], kRpEmpty, hr);
+					if (old == kRpEmpty || old == hr)
+						break;
 				}
+				s0 = (s0 + 1) & (kRpCap - 1);
 			}
-			if (m > m0) {  // maxSignal.Merge / newSignal.Merge of the element's final prio
-				changed++;
-				inserted += !present;
-				ovf += tbl_merge(tb.ms, tb.ms_bmask, e, (int8_t)m) < 0;
-				const int r = tbl_merge(tb.ns, tb.ns_bmask, e, (int8_t)m);
-				ns_ins += r == 1;
-				ovf += r < 0;
-			}
+			atomicMin(&L.fl[(x >> 13) & 3][s0], (uint32_t)(x >> 15) & kSerialMask);
+			sl[k] = s0;
 		}
 	}
-	block_count(&ctr[kCntInserted], inserted);
-	block_count(&ctr[kCntChanged], changed);
-	block_count(&ctr[kCntAux], ns_ins);
-	block_count(&ctr[kCntOverflow], ovf);
-	block_count(&ctr[kCntDistinct], distinct);
+	__syncthreads();
+	// the occupied slots' ranks: thread t owns slots [t * kPer, t * kPer + kPer)
+	uint32_t occ = 0;
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; k++)
+		occ |= (uint32_t)(L.key[tid * kPer + k] != kRpEmpty) << k;
+	const uint32_t c = (uint32_t)__popc(occ);
+	uint32_t inc = c;
+#pragma unroll
+	for (uint32_t d = 1; d < 64; d <<= 1) {
+		const uint32_t t = __shfl_up(inc, d, 64);
+		inc += lane >= d ? t : 0;
+	}
+	if (lane == 63)
+		L.wsum[w] = inc;
+	__syncthreads();
+	uint32_t r = inc - c, tot = 0;
+	for (uint32_t k = 0; k < kRpThreads / 64; k++) {
+		r += k < w ? L.wsum[k] : 0;
+		tot += L.wsum[k];
+	}
+	const uint32_t hp = p << (32 - pbits);
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; k++) {
+		if ((occ >> k) & 1) {
+			const uint32_t s0 = tid * kPer + k;
+			L.rank[s0] = (uint16_t)r;
+			el.e[b0 + r] = fmix32_inv(hp | L.key[s0]);
+			el.f[b0 + r] = make_uint4(L.fl[0][s0], L.fl[1][s0], L.fl[2][s0], L.fl[3][s0]);
+			r++;
+		}
+	}
+	if (tid == 0)
+		el.ecnt[p] = tot;
+	__syncthreads();
+#pragma unroll
+	for (uint32_t k = 0; k < kPer; k++) {
+		const uint32_t i = k * kRpThreads + tid;
+		if (i < n)
+			el.rec_el[b0 + i] = b0 + L.rank[sl[k]];
+	}
+}
+
+// the per-partition counts of k_rp_elems (written by each workgroup, summed
+// by k_rp_reduce: a device atomic per workgroup and counter on five shared
+// addresses serialises thousands of workgroups)
+constexpr uint32_t kRpNumCnt = 5;
+constexpr int kRpCntIdx[kRpNumCnt] = {kCntInserted, kCntChanged, kCntAux, kCntOverflow, kCntDistinct};
+constexpr uint32_t kRpElemThreads = 128;
+
+__global__ __launch_bounds__(kRpElemThreads) void k_rp_elems(const uint32_t* __restrict__ base, LevelMap lm,
+                                                             RpTables tb, RpElems el, const unsigned long long* ctr,
+                                                             uint32_t* sums)
+{
+	__shared__ uint32_t part[kRpNumCnt][kRpElemThreads / 64];
+	if (rp_gated(ctr))
+		return;
+	const uint32_t p = blockIdx.x, b0 = base[p], ne = el.ecnt[p];
+	uint32_t inserted = 0, changed = 0, ns_ins = 0, ovf = 0;
+	for (uint32_t j = threadIdx.x; j < ne; j += kRpElemThreads) {
+		const uint32_t i = b0 + j, e = el.e[i];
+		const Bucket bm = load_bucket(tb.ms + (home_bucket(e, tb.ms_bmask) << kBucketShift));
+		const Bucket bn = load_bucket(tb.ns + (home_bucket(e, tb.ns_bmask) << kBucketShift));
+		const uint4 f4 = el.f[i];
+		const int top = f4.w <= kSerialMask ? 3 : f4.z <= kSerialMask ? 2 : f4.y <= kSerialMask ? 1 : 0;
+		uint64_t v = 0;
+		const int64_t at = tbl_lookup_from(tb.ms, tb.ms_bmask, e, v, bm);
+		const bool present = at >= 0 && slot_live(v);
+		const int m0 = present ? (int)slot_prio(v) : -1000;  // absent: below every prio (signal.go:93-95)
+		el.m0[i] = present ? (int16_t)m0 : kRpAbsent;
+		const int m = max(m0, (int)lm.val[top]);
+		if (m > m0) {  // maxSignal.Merge / newSignal.Merge of the element's final prio
+			changed++;
+			inserted += !present;
+			if (at >= 0)
+				tb.ms[at] = make_slot(e, (int8_t)m);  // e's only writer this launch
+			else
+				ovf += tbl_merge(tb.ms, tb.ms_bmask, e, (int8_t)m) < 0;
+			const int r = tbl_merge_from(tb.ns, tb.ns_bmask, e, (int8_t)m, bn);
+			ns_ins += r == 1;
+			ovf += r < 0;
+		}
+	}
+	const uint32_t v[kRpNumCnt] = {inserted, changed, ns_ins, ovf, 0};
+	const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+#pragma unroll
+	for (uint32_t k = 0; k < kRpNumCnt; k++) {
+		const uint32_t s = (uint32_t)wave_sum_u64(v[k]);
+		if (lane == 0)
+			part[k][w] = s;
+	}
+	__syncthreads();
+	if (threadIdx.x < kRpNumCnt) {
+		uint32_t t = 0;
+		for (uint32_t q = 0; q < kRpElemThreads / 64; q++)
+			t += part[threadIdx.x][q];
+		sums[(uint64_t)p * kRpNumCnt + threadIdx.x] = threadIdx.x == 4 ? ne : t;
+	}
+}
+
+__global__ __launch_bounds__(1024) void k_rp_reduce(const uint32_t* __restrict__ sums, uint32_t P,
+                                                    unsigned long long* ctr)
+{
+	if (rp_gated(ctr))
+		return;
+	__shared__ unsigned long long acc[kRpNumCnt];
+	if (threadIdx.x < kRpNumCnt)
+		acc[threadIdx.x] = 0;
+	__syncthreads();
+	uint64_t v[kRpNumCnt] = {0, 0, 0, 0, 0};
+	for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
+#pragma unroll
+		for (uint32_t k = 0; k < kRpNumCnt; k++)
+			v[k] += sums[(uint64_t)p * kRpNumCnt + k];
+#pragma unroll
+	for (uint32_t k = 0; k < kRpNumCnt; k++) {
+		const uint64_t s = wave_sum_u64(v[k]);
+		if (lane_id() == 0 && s)
+			atomicAdd(&acc[k], (unsigned long long)s);
+	}
+	__syncthreads();
+	if (threadIdx.x < kRpNumCnt)
+		ctr[kRpCntIdx[threadIdx.x]] += acc[threadIdx.x];
+}
+
+// one thread per partitioned record: the flag in closed form
+__global__ __launch_bounds__(256) void k_rp_flags(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ idx,
+                                                  const uint32_t* __restrict__ base, uint32_t P, LevelMap lm,
+                                                  RpElems el, uint8_t* flags, const unsigned long long* ctr)
+{
+	if (rp_gated(ctr))
+		return;
+	const uint32_t n = base[P];
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+		const uint64_t x = keys[i];
+		const uint32_t k = el.rec_el[i];
+		const int16_t m0 = el.m0[k];
+		const uint32_t lv = (uint32_t)(x >> 13) & 3, ser = (uint32_t)(x >> 15) & kSerialMask;
+		if ((int)lm.val[lv] <= (m0 == kRpAbsent ? -1000 : (int)m0))
+			continue;
+		const uint4 f4 = el.f[k];
+		const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
+		bool nw = f[lv] == ser;
+#pragma unroll
+		for (uint32_t l = 0; l < 4; l++)
+			nw = nw && !(l > lv && f[l] <= ser);
+		if (nw)
+			flags[idx[i]] = 1;
+	}
 }
 
 // ---- the step's owner glue ----
@@ -400,15 +536,25 @@ int rp_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set* nsp, const RpSrc& src0, 
 	const uint32_t pbits = rp_pbits(bound), P = 1u << pbits;
 	*pbits_out = pbits;
 	void *wk, *wc, *wb;
-	SYZ_TRY(ws_get(ctx, 56, bound * 12 + 256, &wk));
+	// per bound record: key 8 + index 4 + its element's index 4 + (as elements)
+	// element 4 + firsts 16 + M0 2
+	SYZ_TRY(ws_get(ctx, 56, bound * 38 + 1024, &wk));
 	SYZ_TRY(ws_get(ctx, 57, ntiles * P * 4 + 256, &wc));
-	SYZ_TRY(ws_get(ctx, 58, (uint64_t)(kRpGroups + 2) * P * 4 + 256, &wb));
+	SYZ_TRY(ws_get(ctx, 58, (uint64_t)(kRpGroups + 3 + kRpNumCnt) * P * 4 + 256, &wb));
 	uint64_t* keys = (uint64_t*)wk;
-	uint32_t* idx = (uint32_t*)(keys + bound);
+	uint4* ef = (uint4*)(keys + bound);
+	uint32_t* idx = (uint32_t*)(ef + bound);
+	RpElems el;
+	el.f = ef;
+	el.rec_el = idx + bound;
+	el.e = el.rec_el + bound;
+	el.m0 = (int16_t*)(el.e + bound);
 	uint32_t* cnt = (uint32_t*)wc;
 	uint32_t* tot = (uint32_t*)wb;
 	uint32_t* base = tot + P;               // P + 1 entries
 	uint32_t* gsum = base + P + 2;          // kRpGroups x P
+	uint32_t* sums = gsum + (uint64_t)kRpGroups * P;  // kRpNumCnt per partition
+	el.ecnt = sums + (uint64_t)kRpNumCnt * P;
 	const hipStream_t s = ctx->stream;
 	const uint32_t cg = (P + 63) / 64;
 	k_rp_count<<<(uint32_t)ntiles, kRpTileThreads, P * 4, s>>>(src, pbits, lm.n, cnt, ctr);
@@ -417,7 +563,10 @@ int rp_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set* nsp, const RpSrc& src0, 
 	k_rp_coloffs<<<cg, 1024, 0, s>>>(cnt, (uint32_t)ntiles, P, gsum, base, ctr);
 	k_rp_scatter<<<(uint32_t)ntiles, kRpTileThreads, P * 4, s>>>(src, pbits, cnt, base, keys, idx, ctr);
 	const RpTables tb{ms->slots, ms->nbuckets - 1, nsp->slots, nsp->nbuckets - 1};
-	k_rp_triage<<<P, kRpThreads, 0, s>>>(keys, idx, base, pbits, lm, tb, flags, ctr);
+	k_rp_agg<<<P, kRpThreads, 0, s>>>(keys, base, pbits, el, ctr);
+	k_rp_elems<<<P, kRpElemThreads, 0, s>>>(base, lm, tb, el, ctr, sums);
+	k_rp_reduce<<<1, 1024, 0, s>>>(sums, P, ctr);
+	k_rp_flags<<<grid_for(bound, 256, 8192), 256, 0, s>>>(keys, idx, base, P, lm, el, flags, ctr);
 	SYZ_HIP(hipGetLastError());
 	return SYZSIG_OK;
 }

@@ -133,8 +133,10 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 		c->agg_dbg &= syz::kDebugResultPreserving;
 #endif
 	}
+#ifdef SYZ_EXPERIMENTS
 	if (const char* v = getenv("SYZSIG_EDGE_WAVES"))
 		c->edge_waves = atoi(v) == 8 ? 8 : atoi(v) == 2 ? 2 : atoi(v) == 1 ? 1 : 4;
+#endif
 	if (const char* v = getenv("SYZSIG_AGG_PARTS")) {
 		const uint32_t n = (uint32_t)atoi(v);
 		if (n >= 8 && n <= 2048 && !(n & (n - 1)))
