@@ -45,7 +45,7 @@ MIN_KERNELS = ("k_min_calls+k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg"
 MIN_BYTES_PER_ENTRY, MIN_BYTES_PER_DISTINCT = 5.0, 4.0  # Minimize: (elem, prio) entry + covered[e]
 # N > 1: the source's aggregation, then the owner's records-mode triage of the staircases
 K3_DIST_KERNELS = ("k_fast_prep+k_cell_plan_fast+k_agg_scatter_blk+k_agg+k_stair_bucket+k_stair_heads"
-                   "+k_step_heads+k_rp_count+k_rp_colsum+k_rp_scan+k_rp_coloffs+k_rp_scatter+k_rp_triage+k_step_status"
+                   "+k_step_heads+k_rp_count+k_rp_colsum+k_rp_scan+k_rp_coloffs+k_rp_scatter+k_rp_agg+k_rp_elems+k_rp_reduce+k_rp_flags+k_step_status"
                    "+k_step_back")
 
 

@@ -35,17 +35,25 @@ namespace syz {
 
 constexpr uint32_t kBinShift = 3;  // 8-slot bins
 constexpr uint32_t kBins = kDedupSize >> kBinShift;
-constexpr uint32_t kEdgeDepth = 4;  // chunks in flight per buffer
+constexpr uint32_t kEdgeDepthSignals = 4;  // trace signals in flight per lane per buffer
+#ifndef SYZ_EDGE_KS
+#define SYZ_EDGE_KS 1
+#endif
+constexpr uint32_t kEdgeKS = SYZ_EDGE_KS;  // signals per lane per chunk
 
-// Geometry of one variant: W waves per program, chunks of 64 * W signals; a
-// conflict stamp is epoch << kPosBits | (chunk - 1 - position).
-template <uint32_t W>
+// Geometry of one variant: W waves per program, KS signals per lane, chunks of
+// 64 * W * KS signals (lane l of wave w holds positions k * 64 W + 64 w + l,
+// k < KS); a conflict stamp is epoch << kPosBits | (kPosMask - position).
+template <uint32_t W, uint32_t KS>
 struct EdgeGeom {
-	static constexpr uint32_t kChunk = 64 * W;
-	static constexpr uint32_t kPosBits = W <= 4 ? 8 : 9;
+	static constexpr uint32_t kLanes = 64 * W;
+	static constexpr uint32_t kChunk = kLanes * KS;
+	static constexpr uint32_t kPosBits = kChunk <= 256 ? 8 : kChunk <= 512 ? 9 : 10;
 	static constexpr uint32_t kPosMask = (1u << kPosBits) - 1;
 	static constexpr uint32_t kEpochMax = (1u << (32 - kPosBits)) - 1;
+	static constexpr uint32_t kDepth = kEdgeDepthSignals / KS;  // chunks in flight per buffer
 	static_assert(kChunk <= (1u << kPosBits), "stamp position field");
+	static_assert(KS >= 1 && KS <= 3 && kDepth >= 1, "emit counts: 8 bits per signal slot in a 31-bit payload");
 };
 
 // Workgroup barrier that orders LDS only: a plain __syncthreads() is also a
@@ -61,7 +69,7 @@ __device__ __forceinline__ void lds_barrier()
 // this epoch's markers (older epochs compare lower): it was set by a position
 // before mine this epoch  <=>  stamp > my own v = epoch << kPosBits | (kPosMask - pos).
 
-template <uint32_t W>
+template <uint32_t W, uint32_t KS>
 __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restrict__ pcs, uint64_t npc,
                                                            const uint64_t* __restrict__ call_start,
                                                            const uint32_t* __restrict__ call_len, uint64_t ncalls,
@@ -69,13 +77,14 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
                                                            uint32_t* sigs, uint32_t* sig_cnt, uint32_t* completed,
                                                            unsigned long long* cnt)
 {
-	using G = EdgeGeom<W>;
-	constexpr uint32_t kEdgeWaves = W, kEdgeChunk = G::kChunk, kEpochMax = G::kEpochMax;
+	using G = EdgeGeom<W, KS>;
+	constexpr uint32_t kEdgeWaves = W, kLanes = G::kLanes, kEdgeChunk = G::kChunk, kEpochMax = G::kEpochMax;
+	constexpr uint32_t kDepth = G::kDepth;
 	__shared__ uint32_t table[kDedupSize];
 	__shared__ uint32_t stamp[kBins];
 	__shared__ __align__(16) uint32_t s_any[2][kEdgeWaves];
-	__shared__ uint32_t s_carry[2][kEdgeWaves];
-	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, pos = threadIdx.x;  // pos: place in a chunk
+	__shared__ uint32_t s_carry[2][KS][kEdgeWaves];
+	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, pos = threadIdx.x;  // pos: place in a sub-chunk
 	uint32_t seq = 0;
 	// Workgroup OR of a predicate (one barrier): every wave writes its own
 	// flag, ds_read_b128s read them all.  Two rows alternate: a row is
@@ -114,9 +123,9 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 			continue;
 		}
 		// fresh table per program (common_linux.h:1995-2030: fork zeroes it)
-		for (uint32_t i = threadIdx.x; i < kDedupSize / 4; i += kEdgeChunk)
+		for (uint32_t i = threadIdx.x; i < kDedupSize / 4; i += kLanes)
 			reinterpret_cast<uint4*>(table)[i] = make_uint4(0, 0, 0, 0);
-		for (uint32_t i = threadIdx.x; i < kBins; i += kEdgeChunk)
+		for (uint32_t i = threadIdx.x; i < kBins; i += kLanes)
 			stamp[i] = 0;
 		epoch = 0;
 		lds_barrier();
@@ -143,120 +152,161 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 			// Loads are unconditional (index clamped into the call, value masked
 			// later): a load under a branch makes the compiler drain vmcnt(0)
 			// before the first use, i.e. wait for the whole prefetch.
-			auto fetch = [&](uint64_t (&buf)[kEdgeDepth], uint32_t g) {
+			auto fetch = [&](uint64_t (&buf)[kDepth][KS], uint32_t g) {
 #pragma unroll
-				for (uint32_t u = 0; u < kEdgeDepth; u++)
-					buf[u] = pcs[min<uint64_t>(start + (uint64_t)(g + u) * kEdgeChunk + pos, last)];
+				for (uint32_t u = 0; u < kDepth; u++)
+#pragma unroll
+					for (uint32_t k = 0; k < KS; k++)
+						buf[u][k] = pcs[min<uint64_t>(start + (uint64_t)(g + u) * kEdgeChunk + k * kLanes + pos, last)];
 			};
 			// chunk q of the call; false once the program aborts
-			auto chunk = [&](uint64_t pcv, uint32_t q) -> bool {
-				const uint32_t j = q * kEdgeChunk + pos;
-				const bool valid = j < len;
-				const uint64_t pc = valid ? pcv : 0;
-				const uint32_t h = exec_hash((uint32_t)pc);
-				uint32_t up = __shfl_up(h, 1, 64);
-				if (lane == 63)
-					s_carry[q & 1][w] = h;
-				// cover_check (executor_linux.cc:196-204): doexit(0), this call and
-				// the rest of the program publish nothing
-				if (wg_any(valid && !cover_check(pc), 0))
+			auto chunk = [&](const uint64_t (&pcv)[KS], uint32_t q) -> bool {
+				uint32_t sig[KS], b0[KS], b1[KS], v[KS], wpos[KS];
+				bool pending[KS], emit[KS], writer[KS], marker[KS], blocked[KS], mark_now[KS];
+				bool bad = false;
+#pragma unroll
+				for (uint32_t k = 0; k < KS; k++) {
+					const uint32_t j = q * kEdgeChunk + k * kLanes + pos;
+					pending[k] = j < len;
+					const uint64_t pc = pending[k] ? pcv[k] : 0;
+					// cover_check (executor_linux.cc:196-204): doexit(0), this call and
+					// the rest of the program publish nothing
+					bad |= pending[k] && !cover_check(pc);
+					const uint32_t h = exec_hash((uint32_t)pc);
+					sig[k] = __shfl_up(h, 1, 64);
+					if (lane == 63)
+						s_carry[q & 1][k][w] = h;
+					b0[k] = (uint32_t)pc;  // (the PC's low half, until the previous hash is known)
+				}
+				if (wg_any(bad, 0))
 					return false;
-				if (lane == 0)
-					up = w == 0 ? carry : s_carry[q & 1][w - 1];
-				carry = s_carry[q & 1][kEdgeWaves - 1];
-				const uint32_t sig = (uint32_t)pc ^ up;
-				const uint32_t home = sig & (kDedupSize - 1);
-				const uint32_t b0 = home >> kBinShift, b1 = ((home + 3) & (kDedupSize - 1)) >> kBinShift;
-				bool pending = valid, emit = false;
+#pragma unroll
+				for (uint32_t k = 0; k < KS; k++) {
+					uint32_t up = sig[k];
+					if (lane == 0)
+						up = w > 0 ? s_carry[q & 1][k][w - 1] : k > 0 ? s_carry[q & 1][k - 1][kEdgeWaves - 1] : carry;
+					sig[k] = b0[k] ^ up;
+					const uint32_t home = sig[k] & (kDedupSize - 1);
+					b0[k] = home >> kBinShift;
+					b1[k] = ((home + 3) & (kDedupSize - 1)) >> kBinShift;
+					emit[k] = false;
+				}
+				carry = s_carry[q & 1][KS - 1][kEdgeWaves - 1];
 				// rounds until no lane is pending (a chunk always has a valid lane, so
 				// the first round needs no test); the test after the last round also
-				// publishes every wave's emit count for the output below
+				// publishes every wave's emit counts for the output below
 				for (;;) {
 					// 1. evaluate dedup() (executor.h:692-706) on the current table,
 					// branch-free: the first probe i with T[h+i] == sig (duplicate)
 					// or T[h+i] == 0 (insert there), else the forced overwrite at h
-					uint32_t eqm = 0, zm = 0;
 #pragma unroll
-					for (uint32_t i = 0; i < 4; i++) {
-						const uint32_t t = table[(sig + i) & (kDedupSize - 1)];
-						eqm |= (uint32_t)(t == sig) << i;
-						zm |= (uint32_t)(t == 0) << i;
+					for (uint32_t k = 0; k < KS; k++) {
+						uint32_t eqm = 0, zm = 0;
+#pragma unroll
+						for (uint32_t i = 0; i < 4; i++) {
+							const uint32_t t = table[(sig[k] + i) & (kDedupSize - 1)];
+							eqm |= (uint32_t)(t == sig[k]) << i;
+							zm |= (uint32_t)(t == 0) << i;
+						}
+						const uint32_t first = __builtin_ctz(eqm | zm | 16u);
+						writer[k] = !((eqm >> first) & 1);
+						wpos[k] = (sig[k] + (first & 3)) & (kDedupSize - 1);
 					}
-					const uint32_t first = __builtin_ctz(eqm | zm | 16u);
-					const bool writer = !((eqm >> first) & 1);
-					const uint32_t wpos = (sig + (first & 3)) & (kDedupSize - 1);
 					// 2. mark / block until stable
 					if (epoch == kEpochMax) {
-						for (uint32_t i = threadIdx.x; i < kBins; i += kEdgeChunk)
+						for (uint32_t i = threadIdx.x; i < kBins; i += kLanes)
 							stamp[i] = 0;
 						epoch = 0;
 						lds_barrier();
 					}
 					epoch++;
-					const uint32_t v = (epoch << G::kPosBits) | (G::kPosMask - pos);
-					bool marker = pending && writer, blocked = false;
-					bool mark_now = marker;
+#pragma unroll
+					for (uint32_t k = 0; k < KS; k++) {
+						v[k] = (epoch << G::kPosBits) | (G::kPosMask - (k * kLanes + pos));
+						marker[k] = pending[k] && writer[k];
+						mark_now[k] = marker[k];
+						blocked[k] = false;
+					}
 					for (;;) {
-						if (mark_now) {
-							atomicMax(&stamp[b0], v);
-							if (b1 != b0)
-								atomicMax(&stamp[b1], v);
+#pragma unroll
+						for (uint32_t k = 0; k < KS; k++) {
+							if (mark_now[k]) {
+								atomicMax(&stamp[b0[k]], v[k]);
+								if (b1[k] != b0[k])
+									atomicMax(&stamp[b1[k]], v[k]);
+							}
 						}
 						lds_barrier();
-						const uint32_t s0 = stamp[b0], s1 = stamp[b1];
-						blocked = pending && (s0 > v || s1 > v);
-						mark_now = blocked && !marker;
-						marker = marker || mark_now;
-						if (!wg_any(mark_now, 0))
+						bool any_new = false;
+#pragma unroll
+						for (uint32_t k = 0; k < KS; k++) {
+							const uint32_t s0 = stamp[b0[k]], s1 = stamp[b1[k]];
+							blocked[k] = pending[k] && (s0 > v[k] || s1 > v[k]);
+							mark_now[k] = blocked[k] && !marker[k];
+							marker[k] = marker[k] || mark_now[k];
+							any_new |= mark_now[k];
+						}
+						if (!wg_any(any_new, 0))
 							break;
 					}
 					// 3. final lanes commit (visible after the next round's barrier)
-					const bool fin_w = pending && !blocked && writer;
-					if (fin_w)
-						table[wpos] = sig;
-					emit = emit || fin_w;
-					pending = pending && blocked;
-					if (!wg_any(pending, (uint32_t)__popcll(__ballot(emit))))
+					bool any_pending = false;
+					uint32_t counts = 0;
+#pragma unroll
+					for (uint32_t k = 0; k < KS; k++) {
+						const bool fin_w = pending[k] && !blocked[k] && writer[k];
+						if (fin_w)
+							table[wpos[k]] = sig[k];
+						emit[k] = emit[k] || fin_w;
+						pending[k] = pending[k] && blocked[k];
+						any_pending |= pending[k];
+						counts |= (uint32_t)__popcll(__ballot(emit[k])) << (8 * k);
+					}
+					if (!wg_any(any_pending, counts))
 						break;
 				}
-				// write_output order == trace order: waves in order, lanes in order
-				const uint64_t m = __ballot(emit);
-				uint32_t base = nsig, tot = 0;
+				// write_output order == trace order: sub-chunks in order, then waves,
+				// then lanes
 #pragma unroll
-				for (uint32_t i = 0; i < kEdgeWaves; i++) {
-					const uint32_t x = row[i] >> 1;
-					base += i < w ? x : 0;
-					tot += x;
+				for (uint32_t k = 0; k < KS; k++) {
+					const uint64_t m = __ballot(emit[k]);
+					uint32_t base = nsig, tot = 0;
+#pragma unroll
+					for (uint32_t i = 0; i < kEdgeWaves; i++) {
+						const uint32_t x = (row[i] >> (1 + 8 * k)) & 0xFF;
+						base += i < w ? x : 0;
+						tot += x;
+					}
+					if (emit[k])
+						sigs[start + base + lane_rank(m)] = sig[k];
+					nsig += tot;
 				}
-				if (emit)
-					sigs[start + base + lane_rank(m)] = sig;
-				nsig += tot;
 				return true;
 			};
-			auto run = [&](const uint64_t (&buf)[kEdgeDepth], uint32_t g) -> bool {
+			auto run = [&](const uint64_t (&buf)[kDepth][KS], uint32_t g) -> bool {
 #pragma unroll
-				for (uint32_t u = 0; u < kEdgeDepth; u++)
+				for (uint32_t u = 0; u < kDepth; u++)
 					if (g + u < nch && !chunk(buf[u], g + u))
 						return false;
 				return true;
 			};
-			uint64_t ba[kEdgeDepth], bb[kEdgeDepth];
+			uint64_t ba[kDepth][KS], bb[kDepth][KS];
 			fetch(ba, 0);
 			for (uint32_t g = 0;;) {
-				fetch(bb, g + kEdgeDepth);
+				fetch(bb, g + kDepth);
 				if (!run(ba, g)) {
 					aborted = true;
 					break;
 				}
-				g += kEdgeDepth;
+				g += kDepth;
 				if (g >= nch)
 					break;
-				fetch(ba, g + kEdgeDepth);
+				fetch(ba, g + kDepth);
 				if (!run(bb, g)) {
 					aborted = true;
 					break;
 				}
-				g += kEdgeDepth;
+				g += kDepth;
 				if (g >= nch)
 					break;
 			}
@@ -268,7 +318,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 				sig_cnt[c] = nsig;
 		}
 		// calls not published (aborted and later) report no signal (ipc.go:362-365)
-		for (uint64_t c = cb + done + threadIdx.x; c < ce; c += kEdgeChunk)
+		for (uint64_t c = cb + done + threadIdx.x; c < ce; c += kLanes)
 			sig_cnt[c] = 0;
 		if (threadIdx.x == 0)
 			completed[p] = (uint32_t)done;
@@ -301,17 +351,17 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 #ifdef SYZ_EXPERIMENTS
 	// measured slower: 8 waves 25 ms, 2 waves 16.1, 1 wave 21.3 vs 4 waves 14.9 at C2
 	if (ctx->edge_waves == 8)
-		k_edge_dedup<8><<<grid, 512, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
+		k_edge_dedup<8, kEdgeKS><<<grid, 512, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	else if (ctx->edge_waves == 2)
-		k_edge_dedup<2><<<grid, 128, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
+		k_edge_dedup<2, kEdgeKS><<<grid, 128, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	else if (ctx->edge_waves == 1)
-		k_edge_dedup<1><<<grid, 64, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
+		k_edge_dedup<1, kEdgeKS><<<grid, 64, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                              nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	else
 #endif
-		k_edge_dedup<4><<<grid, 256, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
+		k_edge_dedup<4, kEdgeKS><<<grid, 256, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
 		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)

@@ -477,13 +477,35 @@ int syzsig_set_clone(syzsig_ctx* ctx, const syzsig_set* s, syzsig_set** out)
 	return SYZSIG_OK;
 }
 
+// Whole-table clear as 16-B stores, four per thread (the runtime's fill kernel
+// reaches ~2 TB/s on a 64 MB table, this one ~2.7).
+// Tables are a whole number of 16-B buckets and hipMalloc'd (256-B aligned).
+__global__ __launch_bounds__(256) void k_tbl_fill0(uint4* __restrict__ d, uint64_t n)
+{
+	const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+	const uint4 z = make_uint4(0, 0, 0, 0);
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += 4 * T) {
+#pragma unroll
+		for (uint32_t k = 0; k < 4; k++)
+			if (i + k * T < n)
+				d[i + k * T] = z;
+	}
+}
+
+static uint32_t stream_grid(uint64_t n16)
+{
+	return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n16 + 1023) / 1024, 8192));
+}
+
 int syzsig_set_clear(syzsig_ctx* ctx, syzsig_set* s)
 {
 	SYZ_LOCK(ctx);
 	if (!ctx || !s)
 		return fail(SYZSIG_EINVAL, "set_clear: NULL argument");
 	SYZ_TRY(set_check_idle(s));
-	SYZ_HIP(hipMemsetAsync(s->slots, 0, s->nslots() * sizeof(uint64_t), ctx->stream));
+	const uint64_t n16 = s->nslots() / 2;
+	k_tbl_fill0<<<stream_grid(n16), 256, 0, ctx->stream>>>((uint4*)s->slots, n16);
+	SYZ_HIP(hipGetLastError());
 	s->len = 0;
 	return SYZSIG_OK;
 }
@@ -498,7 +520,7 @@ int syzsig_set_copy_from(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src
 	if (dst->nbuckets != src->nbuckets)
 		return fail(SYZSIG_EINVAL, "set_copy_from: capacity mismatch");
 	SYZ_HIP(hipMemcpyAsync(dst->slots, src->slots, src->nslots() * sizeof(uint64_t), hipMemcpyDeviceToDevice,
-	                       ctx->stream));
+	                       ctx->stream));  // (the runtime's copy: ~4.4 TB/s; a 4 x 16-B-per-thread kernel ran 3.8)
 	dst->len = src->len;
 	return SYZSIG_OK;
 }
