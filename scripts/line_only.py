@@ -1,5 +1,5 @@
-"""Run one of bench.py's extra lines alone (c5, c4, c1), for profiling: the
-line's JSON object on stdout."""
+"""Run one of bench.py's extra lines alone (c5, c4, c1, gw, pipe), for
+profiling: the line's JSON object on stdout."""
 import json
 import os
 import sys
@@ -19,6 +19,10 @@ if which == "c5":
     out = bench.c5_line(dev, pairs)
 elif which == "c1":
     out = bench.c1_line(dev)
+elif which == "gw":
+    out = bench.c2_global_walk_line(dev, pairs, 4096, 64, 4096)
+elif which == "pipe":
+    out = bench.pipeline_line(dev, pairs, 4096, 64, 4096)
 else:
     P, C, L = 4096, 64, 4096
     sigs, cs, cnt, prio, _, _ = bench.synth_batch(dev, synth.synth_default(), 0, P, C, L)

@@ -1,4 +1,4 @@
-"""GPU, world_size 2 over gloo with both ranks on cuda:0: the sharded step of
+"""GPU, world_size 2 and 4 over gloo with every rank on cuda:0: the sharded step of
 syzkaller_amd/dist.py driving the real kernels (GpuShardOps: the staircase
 aggregation of agg.hip, records-mode triage of triage.hip) -- the N>1 path of
 bench.py with gloo standing in for RCCL (RCCL refuses two ranks on one GPU).
@@ -79,16 +79,16 @@ def worker(rank, world, port, outdir, want_bits, cap):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("want_bits,cap", [(True, None), (False, None), (False, 256)])
-def test_gpu_sharded_step_gloo_two_ranks(want_bits, cap):
+@pytest.mark.parametrize("world,want_bits,cap", [(2, True, None), (2, False, None), (2, False, 256),
+                                                  (4, True, None), (4, False, 256)])
+def test_gpu_sharded_step_gloo(world, want_bits, cap):
     """The stream-ordered step (syzsig_step_*: staircase buckets, equal-split
     exchanges, the owners' LDS-partitioned replay, flags back) on the real
-    kernels, two ranks on one GPU over gloo, two consecutive batches; cap=256
-    overflows the first step's buckets, which is redone with a larger cap."""
+    kernels, 2 or 4 ranks on one GPU over gloo, two consecutive batches;
+    cap=256 overflows the first step's buckets, which is redone with a larger
+    cap."""
     from tests.test_gpu_triage import oracle_pairs
     from syzkaller_amd import synth
-
-    world = 2
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(worker, args=(world, _port(), d, want_bits, cap), nprocs=world, start_method="spawn")
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
