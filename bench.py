@@ -76,12 +76,25 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 streaming line")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 per-rank line")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 line")
-    ap.add_argument("--no-gw", action="store_true", help="skip the C2 global-walk line")
+    ap.add_argument("--no-gw", action="store_true", help="skip the C2 line on the other trace distribution")
+    ap.add_argument("--walk", default="global", choices=("global", "region"),
+                    help="trace distribution: SURVEY 8(d)'s walk over all 2^20 blocks (global), or walks inside "
+                         "per-syscall 256-block regions (region, rounds 1-3's headline)")
+    ap.add_argument("--batches", type=int, default=4, help="distinct batches the steps cycle through")
     ap.add_argument("--no-pipe", action="store_true", help="skip the K1+K2 -> K3 pipeline line")
     return ap.parse_args()
 
 
-TRIAGE_KEYS = ("programs_per_gpu", "calls", "pcs_per_call", "m0_per_gpu", "skew", "parallelism")
+TRIAGE_KEYS = ("programs_per_gpu", "calls", "pcs_per_call", "m0_per_gpu", "skew", "parallelism", "walk", "batches")
+# M0's known part per trace distribution (synth_m0 known_sys): the global walk's
+# whole edge universe, or every edge of syscalls 0..2047 of the region walk
+KNOWN_SYS = {"global": 1, "region": 2048}
+
+
+def walk_cfg(walk, **over):
+    from syzkaller_amd import synth
+
+    return synth.synth_default(global_walk=1 if walk == "global" else 0, **over)
 MIN_KEYS = ("workload", "contexts", "entries", "mean_len")
 
 
@@ -299,20 +312,22 @@ def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m
                          "avg_launch_ms": chain / nbatches}}
 
 
-def c2_global_walk_line(dev, pairs, P, C, L, reps=5, m0=10_000_000):
-    """BASELINE config 2 on SURVEY 8(d)'s own input distribution: every call a
-    walk b <- (4b + 1 + r%4) mod B over all B = 2^20 blocks from a uniform
-    block (csrc/common.h synth_trace, global_walk=1), so almost every PC emits
-    a signal (~1.07e9 records per batch) -- against a 10M-element M0 that holds
-    the whole 5.2M-edge universe (prio uniform 0..3) plus random elements.
-    Same step as the headline: maxSignal back to M0, then the whole batch
-    (syz-fuzzer/fuzzer.go:494-511 per call, batched)."""
+def c2_walk_line(dev, pairs, P, C, L, walk, reps=5, m0=10_000_000):
+    """BASELINE config 2 on one trace distribution (the one the headline does
+    not use): `global` is SURVEY 8(d)'s own input -- every call a walk
+    b <- (4b + 1 + r%4) mod B over all B = 2^20 blocks from a uniform block
+    (csrc/common.h synth_trace, global_walk=1), so almost every PC emits a
+    signal (~1.07e9 records per batch), against a 10M-element M0 that holds the
+    whole 5.2M-edge universe (prio uniform 0..3) plus random elements; `region`
+    walks inside per-syscall 256-block regions (rounds 1-3's headline: 321M
+    records, a 70 % K2 drop rate) against every edge of syscalls 0..2047 plus
+    random elements.  Same step as the headline: maxSignal back to M0, then the
+    whole batch (syz-fuzzer/fuzzer.go:494-511 per call, batched)."""
     from syzkaller_amd import signal as S
-    from syzkaller_amd import synth
 
-    cfg = synth.synth_default(global_walk=1)
+    cfg = walk_cfg(walk)
     sigs, cs, cnt, prio, nrec, npc = synth_batch(dev, cfg, 0, P, C, L)
-    m0e, m0p = dev.synth_m0(cfg, 1, m0)
+    m0e, m0p = dev.synth_m0(cfg, KNOWN_SYS[walk], m0)
     pristine = dev.deserialize(m0e, m0p)
     del m0e, m0p
     b, _, _ = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
@@ -335,11 +350,14 @@ def c2_global_walk_line(dev, pairs, P, C, L, reps=5, m0=10_000_000):
     wall, chain = float(np.median(walls)), float(np.median(chains))
     achieved = PROBE_BYTES_PER_REC * nrec / (chain * 1e-3) / 1e9
     wl = (f"BASELINE config 2 on SURVEY 8(d)'s global walk: {P} programs x {C} calls x {L} PCs over all 2^20 blocks "
-          f"vs a {m0}-element maxSignal holding the edge universe")
+          f"vs a {m0}-element maxSignal holding the edge universe") if walk == "global" else \
+         (f"BASELINE config 2 on per-syscall region walks: {P} programs x {C} calls x {L} PCs in 256-block regions "
+          f"vs a {m0}-element maxSignal holding every edge of syscalls 0..2047, one batch")
     traffic, src, note = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], {"workload": wl}, ("workload",),
                                      expect_ms=chain)
     del sigs, cs, cnt, prio, b
-    return {"metric": "signal elems triaged/sec (Diff+Merge), SURVEY 8(d) global-walk traces",
+    return {"metric": "signal elems triaged/sec (Diff+Merge), " +
+                      ("SURVEY 8(d) global-walk traces" if walk == "global" else "per-syscall region-walk traces"),
             "value": nrec / wall, "unit": "elems/s", "higher_is_better": True, "ms": wall * 1e3, "dtype": "u32",
             "config": {"workload": wl, "records": nrec, "pcs": npc, "distinct": st["distinct"],
                        "changed": st["changed"], "retries": st["retries"], "runs": st["runs"],
@@ -350,7 +368,7 @@ def c2_global_walk_line(dev, pairs, P, C, L, reps=5, m0=10_000_000):
                          "avg_launch_ms": chain}}
 
 
-def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_000, reps=3):
+def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, walk, world=8, m0_total=1_000_000_000, reps=3):
     """BASELINE config 4 seen from one rank of an 8-GPU node, on one GPU, with
     the stream-ordered step's own calls (syzsig_step_*): (1) the source side --
     this rank's C2 batch aggregated per element, each element's staircase into
@@ -367,7 +385,7 @@ def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_
     from syzkaller_amd._lib import STEP_HDR_COUNT
     from syzkaller_amd.dist import SIGNAL_PRIO_LEVELS
 
-    cfg = synth.synth_default()
+    cfg = walk_cfg(walk)
     levels = list(SIGNAL_PRIO_LEVELS)
     nrec0 = int(cnt.to(torch.int64).sum().item())
 
@@ -413,7 +431,7 @@ def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_
     received = sum(x.numel() for x in parts)
     del parts
     # owner 0's shard of the 1B-element M0
-    se, sp = dev.synth_m0_shard(cfg, 2048, m0_total, world, 0)
+    se, sp = dev.synth_m0_shard(cfg, KNOWN_SYS[walk], m0_total, world, 0)
     pristine = dev.deserialize(se, sp)
     shard_len = int(se.numel())
     del se, sp
@@ -444,7 +462,7 @@ def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_
     step = s_ms + o_ms + k_ms
     achieved = PROBE_BYTES_PER_REC * nrec0 / (step * 1e-3) / 1e9
     xbytes = 8 * (world - 1) * (cap + 1) + (world - 1) * (cap + 1)  # records out + flags back per rank
-    wl = (f"BASELINE config 4, one rank of {world}: this rank's {P} x {C} x {L} batch (source aggregation into "
+    wl = (f"BASELINE config 4, one rank of {world}: this rank's {P} x {C} x {L} {walk}-walk batch (source aggregation into "
           f"staircase buckets), owner 0's LDS-partitioned replay of what all {world} sources send it against its "
           f"{shard_len}-element shard of a {m0_total}-element maxSignal, the flags back")
     traffic, src, note = pmc_traffic(["syz::" + k for k in K3_DIST_KERNELS.split("+")], {"workload": wl},
@@ -465,7 +483,7 @@ def c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, world=8, m0_total=1_000_000_
                          "bytes_per_unit": PROBE_BYTES_PER_REC, "units_per_launch": nrec0, "avg_launch_ms": step}}
 
 
-def pipeline_line(dev, pairs, P, C, L, reps=3, m0=10_000_000):
+def pipeline_line(dev, pairs, P, C, L, walk, reps=3, m0=10_000_000):
     """The per-execution path end to end on one C2 batch: raw KCOV traces in
     HBM -> K1+K2 (executor write_coverage_signal + dedup, executor.h:492-512)
     -> K3 (checkNewSignal over the batch, fuzzer.go:494-511; proc.go:230-247
@@ -474,14 +492,14 @@ def pipeline_line(dev, pairs, P, C, L, reps=3, m0=10_000_000):
     from syzkaller_amd import signal as S
     from syzkaller_amd import synth
 
-    cfg = synth.synth_default()
+    cfg = walk_cfg(walk)
     cl = torch.full((P * C,), L, dtype=torch.int32)
     pcs, cs, cl, prio = dev.synth_traces(cfg, 0, P, C, cl)
     pidx = torch.arange(P + 1, dtype=torch.int32, device=dev.dev) * C
     sigs = torch.empty(pcs.numel(), dtype=torch.int32, device=dev.dev)
     cnt = torch.empty(P * C, dtype=torch.int32, device=dev.dev)
     comp = torch.empty(P, dtype=torch.int32, device=dev.dev)
-    m0e, m0p = dev.synth_m0(cfg, 2048, m0)
+    m0e, m0p = dev.synth_m0(cfg, KNOWN_SYS[walk], m0)
     pristine = dev.deserialize(m0e, m0p)
     del m0e, m0p
     ms = pristine.clone()
@@ -510,8 +528,8 @@ def pipeline_line(dev, pairs, P, C, L, reps=3, m0=10_000_000):
     return {"metric": "KCOV PCs -> checkNewSignal result per second (K1+K2 then K3 on one batch)",
             "value": npc / (t * 1e-3), "unit": "PCs/s", "higher_is_better": True, "ms": t, "dtype": "u64->u32",
             "records_per_s": nrec / (t * 1e-3),
-            "config": {"workload": f"BASELINE config 2 batch: {P} programs x {C} calls x {L} PCs from raw traces, "
-                                   f"vs a {m0}-element maxSignal",
+            "config": {"workload": f"BASELINE config 2 batch: {P} programs x {C} calls x {L} PCs from raw "
+                                   f"{walk}-walk traces, vs a {m0}-element maxSignal",
                        "pcs": npc, "records": nrec, "changed": st["changed"]}}
 
 
@@ -651,10 +669,12 @@ def main():
     progress(rank, f"device {local}, world {world}")
     dev = Device(local)
     dev.L.syzsig_ctx_set_timing(dev.eng.h, 1)
-    cfg = synth.synth_default(skew=a.skew)
+    cfg = walk_cfg(a.walk, skew=a.skew)
+    known = KNOWN_SYS[a.walk]
     P, C, L = a.programs, a.calls, a.pcs
+    NB = max(1, min(a.batches, a.steps + a.warmup))
     # ---- setup: traces -> K1+K2 (timed as a stage, not part of `value`)
-    progress(rank, f"traces {P} x {C} x {L}")
+    progress(rank, f"traces {P} x {C} x {L} ({a.walk} walk), batch 1 of {NB}")
     cl = torch.full((P * C,), L, dtype=torch.int32)
     pcs, cs, cl, prio = dev.synth_traces(cfg, rank * P, P, C, cl)
     pidx = torch.arange(P + 1, dtype=torch.int32, device=dev.dev) * C
@@ -672,6 +692,16 @@ def main():
     npc = pcs.numel()
     del pcs
     nrec = int(cnt.to(torch.int64).sum().item())
+    # the other batches the steps cycle through: batch j of rank r holds
+    # programs (j * world + r) * P .. + P, so no step replays the previous one
+    pool = [(sigs, cs, cnt, prio, nrec)]
+    for j in range(1, NB):
+        progress(rank, f"traces, batch {j + 1} of {NB}")
+        clj = torch.full((P * C,), L, dtype=torch.int32)
+        pj, csj, clj, prj = dev.synth_traces(cfg, (j * world + rank) * P, P, C, clj)
+        sj, cj, _ = dev.edge_derive(pj, csj, clj, pidx)
+        del pj
+        pool.append((sj, csj, cj, prj, int(cj.to(torch.int64).sum().item())))
     # ---- M0 (maxSignal before the batch): 10M elements per GPU
     if distributed:
         from syzkaller_amd.dist import SIGNAL_PRIO_LEVELS, GpuShardOps, ShardedTriage
@@ -679,9 +709,9 @@ def main():
         # BASELINE config 4: one maxSignal of m0_total elements, hash-sharded;
         # each rank generates only its own shard (in index order)
         progress(rank, f"M0 shard of {a.m0_total} elements")
-        m0e, m0p = dev.synth_m0_shard(cfg, 2048, a.m0_total, world, rank)
+        m0e, m0p = dev.synth_m0_shard(cfg, known, a.m0_total, world, rank)
     else:
-        m0e, m0p = dev.synth_m0(cfg, 2048, a.m0)
+        m0e, m0p = dev.synth_m0(cfg, known, a.m0)
     progress(rank, f"maxSignal of {m0e.numel()} elements")
     ms = dev.deserialize(m0e, m0p)
     if a.table_hint:
@@ -696,7 +726,7 @@ def main():
     # room for every pair the run can emit (4 per distinct element, <= 2048 x 5939 distinct):
     # the library writes them here directly instead of copying them after the run
     pairs = torch.empty(4 * 2048 * 5939 + 64, dtype=torch.int64, device=dev.dev)
-    b, bits, cnew = dev.batch(sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
+    batches = [dev.batch(x[0], x[1], x[2], x[3], new_pairs=pairs, want_bits=False) for x in pool]
     if distributed:
         ops = GpuShardOps(dev)
         # the prio levels are fixed for the workload (signalPrio gives 0..3,
@@ -718,19 +748,24 @@ def main():
         else:
             ms.restore_keys(pristine, ns)
 
-    def step():
+    def step(i):
+        # batch i % NB: serial base of rank r = its programs' place in the step's
+        # rank-major batch
         reset()
         ns.clear()
+        j = i % NB
         if distributed:
-            st = dict(sharded.step((b, bits, cnew), prio, rank * P * C)[2])
+            st = dict(sharded.step(batches[j], pool[j][3], rank * P * C)[2])
             # source aggregation + staircase buckets, the owner's replay, the flags back
             st["part_ms"], st["probe_ms"], st["decide_ms"] = st["src_ms"], st["own_ms"], st["back_ms"]
-            return st
-        return dev.triage_b(ms, ns, b)
+        else:
+            st = dev.triage_b(ms, ns, batches[j][0])
+        st["nrec"] = pool[j][4]
+        return st
 
     progress(rank, f"warmup {a.warmup}")
-    for _ in range(a.warmup):
-        step()
+    for i in range(a.warmup):
+        step(i)
         if distributed and ms.capacity() != pristine.capacity():
             # the owner reserved its shard for a step's worst case (bucket cap x
             # ranks): the snapshot gets the same room, so that the state reset
@@ -742,13 +777,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        stats.append(step())
+    for i in range(a.steps):
+        stats.append(step(a.warmup + i))
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     dt = time.perf_counter() - t0
-    total_rec = nrec
+    total_rec = sum(s["nrec"] for s in stats)  # this rank's records over the timed steps
     reset()  # (outside the timed region: the reset brought back M0 exactly)
     restore_ok = ms.equal(pristine)
     if not restore_ok:
@@ -757,18 +792,18 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64, device=dev.dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-        tr = torch.tensor([nrec], dtype=torch.int64, device=dev.dev)
+        tr = torch.tensor([total_rec], dtype=torch.int64, device=dev.dev)
         dist.all_reduce(tr)
         total_rec = int(tr.item())
     ingest_ms, ingest_ok = ingest_stage(dev, sigs, cs, cnt, prio, comp, P, C) if not distributed else (None, None)
     ms_per_step = dt / a.steps * 1e3
-    value = total_rec * a.steps / dt
+    value = total_rec / dt
     s0 = stats[-1]
     probe_ms = float(np.mean([s["probe_ms"] for s in stats]))
     decide_ms = float(np.mean([s["decide_ms"] for s in stats]))
     part_ms = float(np.mean([s["part_ms"] for s in stats]))
     k3_ms = part_ms + probe_ms + decide_ms
-    probe_units = nrec
+    probe_units = float(np.mean([s["nrec"] for s in stats]))  # records per launch (this rank)
     # roofline over the whole K3 pipeline (every kernel between the records in
     # HBM and the updated sets), not one kernel of it
     achieved = PROBE_BYTES_PER_REC * probe_units / (k3_ms * 1e-3) / 1e9
@@ -788,14 +823,18 @@ def main():
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": ("BASELINE config 2: 1xMI355X batch triage, "
-                                    f"{P} programs x {C} calls x {L} PCs vs a {a.m0}-element maxSignal")
+                                    f"{P} programs x {C} calls x {L} PCs vs a {a.m0}-element maxSignal, "
+                                    + ("SURVEY 8(d)'s global-walk traces" if a.walk == "global" else
+                                       "per-syscall region-walk traces") + f", {NB} distinct batches in turn")
                        if not distributed else
                        (f"BASELINE config 4: a {a.m0_total}-element maxSignal hash-sharded over {world} GPUs "
                         f"({m0e.numel()} elements on rank 0), each rank triaging {P} programs x {C} calls x {L} PCs "
-                        "(BASELINE config 2 per GPU), staircase records routed with RCCL all-to-all"),
+                        f"(BASELINE config 2 per GPU, {a.walk}-walk traces, {NB} distinct batches in turn), staircase "
+                        "records routed with RCCL all-to-all"),
                        "programs_per_gpu": P, "calls": C, "pcs_per_call": L,
                        "m0_per_gpu": a.m0 if not distributed else int(m0e.numel()),
-                       "records_per_gpu": nrec, "pcs_per_gpu": npc, "skew": a.skew,
+                       "records_per_gpu": probe_units, "records_per_batch": [x[4] for x in pool],
+                       "pcs_per_gpu": npc, "skew": a.skew, "walk": a.walk, "batches": NB,
                        "table_slots": ms.capacity(),
                        "parallelism": f"shard{world}" if distributed else "single",
                        **({"dist_backend": a.dist_backend} if distributed else {})},
@@ -809,7 +848,7 @@ def main():
                        "finalize_ms": decide_ms,
                        "edge_pcs_per_s": npc / (np.median(edge_ms) * 1e-3),
                        "ingest_ms": ingest_ms, "ingest_check": ingest_ok},
-            "triage": {k: v for k, v in s0.items() if k not in ("probe_ms", "decide_ms", "part_ms")},
+            "triage": {k: v for k, v in s0.items() if k not in ("probe_ms", "decide_ms", "part_ms", "nrec")},
             "state_reset": "maxSignal back to M0 before every step: a table copy, or the slots of the previous "
                            "step's newSignal elements (syzsig_set_restore_keys) when that moves fewer bytes; "
                            "checked equal to M0 after the timed steps",
@@ -838,13 +877,14 @@ def main():
     if rank == 0 and world == 1 and not a.no_c5:
         out["lines"]["c5"] = c5_line(dev, pairs)
     if rank == 0 and world == 1 and not a.no_pipe:
-        out["lines"]["pipeline"] = pipeline_line(dev, pairs, P, C, L)
+        out["lines"]["pipeline"] = pipeline_line(dev, pairs, P, C, L, a.walk)
     if rank == 0 and world == 1 and not a.no_gw:
-        out["lines"]["c2_global_walk"] = c2_global_walk_line(dev, pairs, P, C, L)
+        other = "region" if a.walk == "global" else "global"
+        out["lines"][f"c2_{other}_walk"] = c2_walk_line(dev, pairs, P, C, L, other)
     if rank == 0 and world == 1 and not a.no_c1:
         out["lines"]["c1"] = c1_line(dev)
     if rank == 0 and world == 1 and not a.no_c4:
-        out["lines"]["c4_rank"] = c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L)
+        out["lines"]["c4_rank"] = c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, a.walk)
     if rank == 0 and world == 1 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, C, a.cpu_seconds, a.cpu_threads)
     elif rank == 0:

@@ -1,4 +1,4 @@
-"""Run one of bench.py's extra lines alone (c5, c4, c1, gw, pipe), for
+"""Run one of bench.py's extra lines alone (c5, c4, c1, gw, rw, pipe; then the walk: global | region), for
 profiling: the line's JSON object on stdout."""
 import json
 import os
@@ -8,10 +8,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from syzkaller_amd import synth  # noqa: E402
 from syzkaller_amd.device import Device  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "c5"
+WALK = sys.argv[2] if len(sys.argv) > 2 else "global"  # the headline's trace distribution
 dev = Device(0)
 dev.L.syzsig_ctx_set_timing(dev.eng.h, 1)
 pairs = torch.empty(4 * 2048 * 5939 + 64, dtype=torch.int64, device=dev.dev)
@@ -20,11 +20,13 @@ if which == "c5":
 elif which == "c1":
     out = bench.c1_line(dev)
 elif which == "gw":
-    out = bench.c2_global_walk_line(dev, pairs, 4096, 64, 4096)
+    out = bench.c2_walk_line(dev, pairs, 4096, 64, 4096, "global")
+elif which == "rw":
+    out = bench.c2_walk_line(dev, pairs, 4096, 64, 4096, "region")
 elif which == "pipe":
-    out = bench.pipeline_line(dev, pairs, 4096, 64, 4096)
+    out = bench.pipeline_line(dev, pairs, 4096, 64, 4096, WALK)
 else:
     P, C, L = 4096, 64, 4096
-    sigs, cs, cnt, prio, _, _ = bench.synth_batch(dev, synth.synth_default(), 0, P, C, L)
-    out = bench.c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L)
+    sigs, cs, cnt, prio, _, _ = bench.synth_batch(dev, bench.walk_cfg(WALK), 0, P, C, L)
+    out = bench.c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, WALK)
 print(json.dumps(out), flush=True)

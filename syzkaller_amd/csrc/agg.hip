@@ -64,6 +64,7 @@ static_assert(kAggRegion == kAggSlots, "distinct-list region per partition (inte
 constexpr uint32_t kAggLimit = kAggSlots * 4 / 5;  // distinct elements before a partition overflows
 static_assert(kAggLimit == kAggLimitRecs, "internal.h mirror");
 constexpr double kAggTargetLoad = 0.4;             // partitions are sized for this LDS load
+constexpr double kAggTargetLoadEntry = 0.6;        // ... and for Minimize
 constexpr uint32_t kAggEmpty = 0xFFFFFFFFu;        // empty key (LDS keys are residuals < 2^29)
 constexpr uint32_t kAggNone = 0xFFFFFFFFu;         // no record at this level
 constexpr uint32_t kAggOverflow = 0xFFFFFFFFu;     // partition count marker
@@ -523,7 +524,7 @@ constexpr uint32_t kDummyLines = 2048;  // CapCells::dummy lines
 // Work items of 2^ibits calls own their cells (items = chunks for a triage
 // batch).  kEntry (Minimize): the level comes from each record's own prio
 // (x.elem_prio), and only the records whose element shard x.shard owns are kept.
-template <bool kEntry>
+template <bool kEntry, uint32_t kB>
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t* __restrict__ sigs,
                                                                  const uint64_t* __restrict__ call_start,
                                                                  const uint32_t* __restrict__ call_len,
@@ -532,8 +533,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
                                                                  CapCells cc, uint32_t* recs, uint32_t dbg)
 {
 	constexpr uint32_t kWaves = kAggThreads / 64, kPer = kEntry ? SYZ_SCAT_PER_ENTRY : SYZ_SCAT_PER, kQuota = kPer * 64;
-	__shared__ uint32_t buf[kAggMaxParts][kBlk];  // per partition: the block being filled
-	__shared__ uint32_t fillc[kAggMaxParts + 1];   // slots handed out in it (may overshoot kBlk)
+	constexpr uint32_t kG = 64 / kB;  // blocks a wave writes per store (kB lanes each)
+	static_assert(kB == 16 || kB == 32, "block of 64 or 128 B");
+	__shared__ uint32_t buf[kAggMaxParts * kBlk];  // per partition: the block being filled (P * kB <= this)
+	__shared__ uint32_t fillc[kAggMaxParts + 1];   // slots handed out in it (may overshoot kB)
 	__shared__ uint32_t written[kAggMaxParts + 1]; // records of the cell written so far (+ a spare)
 	__shared__ uint16_t flist[kAggMaxParts];       // partitions whose block filled this sub-round
 	__shared__ uint32_t nfl[2];                    // their count, by sub-round parity
@@ -543,7 +546,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 	__shared__ uint8_t s_lvl[kEntry ? 256 : 1];
 	__shared__ uint32_t s_or[2][kWaves];
 	const uint32_t P = 1u << g.pbits, cb = g.cbits(), ib = g.ibits;
-	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), grp = lane >> 4, slot = lane & (kBlk - 1);
+	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), grp = lane / kB, slot = lane & (kB - 1);
 	// Workgroup OR in one barrier (__syncthreads_or takes three): every wave
 	// writes its flag to a row, all read the row; two rows alternate, so a row
 	// is rewritten only after every wave passed the barrier of the call between.
@@ -627,30 +630,30 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 				nfl[(rnd + 1) & 1] = 0;  // the next sub-round's list (last read a sub-round ago)
 			// a uniform loop; a lane group past the list stores its block to this
 			// block's dummy line instead (a store without a branch)
-			for (uint32_t jb = 0; jb < nf; jb += 4 * kWaves * 4) {
+			for (uint32_t jb = 0; jb < nf; jb += 4 * kWaves * kG) {
 				uint32_t pp[4], wr[4], v[4];
 #pragma unroll
 				for (uint32_t t = 0; t < 4; t++)
-					pp[t] = flist[min(jb + t * kWaves * 4 + w * 4 + grp, nf - 1)];
+					pp[t] = flist[min(jb + t * kWaves * kG + w * kG + grp, nf - 1)];
 #pragma unroll
 				for (uint32_t t = 0; t < 4; t++) {
 					wr[t] = written[pp[t]];
-					v[t] = buf[pp[t]][slot];
+					v[t] = buf[pp[t] * kB + slot];
 				}
 #pragma unroll
 				for (uint32_t t = 0; t < 4; t++) {
-					const bool ok = jb + t * kWaves * 4 + w * 4 + grp < nf, fits = wr[t] + kBlk <= cap;
+					const bool ok = jb + t * kWaves * kG + w * kG + grp < nf, fits = wr[t] + kB <= cap;
 					spilled |= ok && !fits;  // the cell is full: the run is redone with counted cells
 					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp[t] * cap + wr[t]
-					                         : cc.dummy + (blockIdx.x % kDummyLines) * kBlk;
+					                         : cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
 					d[slot] = v[t];
 				}
 				__builtin_amdgcn_wave_barrier();
 				if (slot == 0) {  // (a group past the list updates the spare entry kAggMaxParts)
 #pragma unroll
 					for (uint32_t t = 0; t < 4; t++) {
-						const uint32_t q = jb + t * kWaves * 4 + w * 4 + grp < nf ? pp[t] : kAggMaxParts;
-						written[q] = wr[t] + kBlk;
+						const uint32_t q = jb + t * kWaves * kG + w * kG + grp < nf ? pp[t] : kAggMaxParts;
+						written[q] = wr[t] + kB;
 						fillc[q] = 0;
 					}
 				}
@@ -684,13 +687,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			uint32_t sl[kPer], full = 0;
 #pragma unroll
 			for (uint32_t u = 0; u < kPer; u++)
-				sl[u] = (pend >> u) & 1 ? atomicAdd(&fillc[pt[u]], 1u) : kBlk;
+				sl[u] = (pend >> u) & 1 ? atomicAdd(&fillc[pt[u]], 1u) : kB;
 #pragma unroll
 			for (uint32_t u = 0; u < kPer; u++) {
-				if (sl[u] < kBlk) {
-					buf[pt[u]][sl[u]] = rec[u];
+				if (sl[u] < kB) {
+					buf[pt[u] * kB + sl[u]] = rec[u];
 					pend &= ~(1u << u);
-					full |= (uint32_t)(sl[u] == kBlk - 1) << u;
+					full |= (uint32_t)(sl[u] == kB - 1) << u;
 				}
 			}
 			while (__ballot(full != 0)) {
@@ -729,12 +732,12 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 				break;
 		}
 		// the chunk's last partial block of every cell, and the cell counts
-		for (uint32_t p = w * 4 + grp; p < P; p += kWaves * 4) {
+		for (uint32_t p = w * kG + grp; p < P; p += kWaves * kG) {
 			const uint32_t c = fillc[p], wr = written[p];
 			if (wr + c > cap)
 				spilled = true;
 			else if (slot < c)
-				recs[cbase + (uint64_t)p * cap + wr + slot] = buf[p][slot];
+				recs[cbase + (uint64_t)p * cap + wr + slot] = buf[p * kB + slot];
 			if (slot == 0)
 				cc.cnt[(uint64_t)p * cc.nchunks + ch] = min(wr + c, cap);
 		}
@@ -744,6 +747,20 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 		*cc.ovf = 1u;
 	if (kEntry && x.bad_level && __ballot(badlv) && lane == 0)
 		atomicOr(x.bad_level, 1u);
+}
+
+// The scatter's write-combining blocks fill the same 128 KB of LDS: 64 B per
+// partition at 2048 partitions, whole 128-B lines at <= 1024.
+#ifndef SYZ_SCAT_WIDE
+#define SYZ_SCAT_WIDE 1
+#endif
+template <bool kEntry, typename... A>
+static void scatter_blk(uint32_t grid, hipStream_t s, uint32_t pbits, A... a)
+{
+	if (SYZ_SCAT_WIDE && pbits < kAggMaxBits)
+		k_agg_scatter_blk<kEntry, 32><<<grid, kAggThreads, 0, s>>>(a...);
+	else
+		k_agg_scatter_blk<kEntry, 16><<<grid, kAggThreads, 0, s>>>(a...);
 }
 
 // Capped cells of a run: records per chunk -> cell capacity and chunk base.
@@ -1926,7 +1943,7 @@ static uint64_t pow2_at_least(uint64_t x)
 	return p;
 }
 
-static AggGeom agg_geom_for(syzsig_ctx* ctx, uint64_t nrec, double distinct_hint)
+static AggGeom agg_geom_for(syzsig_ctx* ctx, uint64_t nrec, double distinct_hint, double load = kAggTargetLoad)
 {
 	AggGeom g;
 	if (ctx->agg_parts) {
@@ -1939,7 +1956,7 @@ static AggGeom agg_geom_for(syzsig_ctx* ctx, uint64_t nrec, double distinct_hint
 	const double ratio = ctx->agg_distinct_ratio > 0 ? ctx->agg_distinct_ratio : 1.0 / 32;
 	const double d = distinct_hint > 0 ? distinct_hint : ratio * (double)nrec;
 	uint32_t pb = nrec >= (1ull << 24) ? 8 : kAggMinBits;
-	while (pb < kAggMaxBits && d > kAggTargetLoad * kAggSlots * (double)(1u << pb))
+	while (pb < kAggMaxBits && d > load * kAggSlots * (double)(1u << pb))
 		pb++;
 	g.pbits = pb;
 	return g;
@@ -1996,10 +2013,10 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
 	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
 	if (xp)
-		k_agg_scatter_blk<true><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
+		scatter_blk<true>(pg, s, gs.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
 		                                                   c1, gs, *xp, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 	else
-		k_agg_scatter_blk<false><<<pg, kAggThreads, 0, s>>>(b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
+		scatter_blk<false>(pg, s, gs.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
 		                                                    c1, gs, AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs,
 		                                                    ctx->agg_dbg >> 10);
 	SYZ_HIP(hipGetLastError());
@@ -2061,7 +2078,10 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 {
 	const AggSrc x = xp ? *xp : AggSrc{nullptr, 1, 0, 0};
 	const bool entry = xp != nullptr;
-	AggGeom g = agg_geom_for(ctx, run_recs, x.distinct_hint);
+	// Minimize: fuller LDS tables, so half the partitions and whole 128-B
+	// scatter blocks (C3: 2.70-2.78 -> 2.65 ms; a triage run's finalize and
+	// k_agg lose more than its scatter gains)
+	AggGeom g = agg_geom_for(ctx, run_recs, x.distinct_hint, entry ? kAggTargetLoadEntry : kAggTargetLoad);
 	const uint32_t P = 1u << g.pbits;
 	const uint64_t nchunks = (c1 - c0 + (1ull << g.cbits()) - 1) >> g.cbits();
 	// Work items of the count/scatter: whole chunks for a batch (its calls are
@@ -2345,7 +2365,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap);
 	}
 	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
-	k_agg_scatter_blk<false><<<(int)std::min<uint64_t>(nchunks, 2048), kAggThreads, 0, s>>>(
+	scatter_blk<false>((uint32_t)std::min<uint64_t>(nchunks, 2048), s, g.pbits,
 	    b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, g, AggSrc{nullptr, 1, 0, 0}, cc,
 	    (uint32_t*)recs, ctx->agg_dbg >> 10);
 	SYZ_HIP(hipGetLastError());
@@ -3068,7 +3088,7 @@ int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial
 		                                              b->nrec, sizes, (uint64_t*)dpart, b->call_new, lm);
 		k_cell_plan_fast<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap, (const uint64_t*)dpart, b->nrec, 0, sc);
 		const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
-		k_agg_scatter_blk<false><<<(int)std::min<uint64_t>(nchunks, 2048), kAggThreads, 0, s>>>(
+		scatter_blk<false>((uint32_t)std::min<uint64_t>(nchunks, 2048), s, g.pbits,
 		    b->sigs, b->call_start, b->call_len, b->call_prio, lm, 0, b->ncalls, g, AggSrc{nullptr, 1, 0, 0}, cc,
 		    (uint32_t*)recs, ctx->agg_dbg >> 10);
 		const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),
