@@ -446,9 +446,10 @@ int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial
 /* Owner side: the buckets every source sent this owner (d_recv, nshards *
  * (cap + 1) words) triaged against its shard and newSignal shard (both
  * non-NULL); d_flags gets one byte per word.  exact = 0: records partitioned by
- * element hash through LDS (one workgroup per partition sorts its records by
- * element and serial and replays checkNewSignal per element); a partition
- * over the LDS capacity makes this owner skip its records (owners_void).
+ * element hash through LDS (per partition its elements' level firsts, per
+ * element one shard probe, per record checkNewSignal's verdict in closed form;
+ * no sort); a partition over the LDS capacity makes this owner skip its
+ * records (owners_void).
  * exact = 1: the per-record path (host round trips), for that redo.  Until
  * syzsig_step_finish, `shard` and `new_signal` take no other call. */
 int syzsig_step_own_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set* new_signal, const uint64_t* d_recv,
