@@ -538,17 +538,18 @@ int rp_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set* nsp, const RpSrc& src0, 
 	void *wk, *wc, *wb;
 	// per bound record: key 8 + index 4 + its element's index 4 + (as elements)
 	// element 4 + firsts 16 + M0 2
-	SYZ_TRY(ws_get(ctx, 56, bound * 38 + 1024, &wk));
+	const uint64_t nb = (bound + 3) & ~3ull;  // array strides: the firsts stay 16-B aligned
+	SYZ_TRY(ws_get(ctx, 56, nb * 38 + 1024, &wk));
 	SYZ_TRY(ws_get(ctx, 57, ntiles * P * 4 + 256, &wc));
 	SYZ_TRY(ws_get(ctx, 58, (uint64_t)(kRpGroups + 3 + kRpNumCnt) * P * 4 + 256, &wb));
 	uint64_t* keys = (uint64_t*)wk;
-	uint4* ef = (uint4*)(keys + bound);
-	uint32_t* idx = (uint32_t*)(ef + bound);
+	uint4* ef = (uint4*)(keys + nb);
+	uint32_t* idx = (uint32_t*)(ef + nb);
 	RpElems el;
 	el.f = ef;
-	el.rec_el = idx + bound;
-	el.e = el.rec_el + bound;
-	el.m0 = (int16_t*)(el.e + bound);
+	el.rec_el = idx + nb;
+	el.e = el.rec_el + nb;
+	el.m0 = (int16_t*)(el.e + nb);
 	uint32_t* cnt = (uint32_t*)wc;
 	uint32_t* tot = (uint32_t*)wb;
 	uint32_t* base = tot + P;               // P + 1 entries
