@@ -17,14 +17,18 @@
 //      (read only): duplicate, or a write at some slot of its window;
 //   2. writers mark the 8-slot bins their window touches (LDS stamps keep the
 //      earliest marking position per bin); a pending lane with an EARLIER
-//      marker in its bins is blocked -- and marks its own bins too, since its
+//      marker in the bin of its DECISION slot (the first match or zero of its
+//      window, or h for the forced overwrite) is blocked -- an earlier write of
+//      a nonzero value != sig anywhere else in the window changes none of the
+//      predicates it evaluated, and an earlier lane with the same sig has the
+//      same decision slot -- and marks its own window's bins too, since its
 //      re-run may turn into a write (repeated until no new marks);
 //   3. unblocked lanes are final: writers store, everyone leaves the round.
-// A final lane has only final duplicates before it inside its window, and
-// duplicates change nothing, so it saw exactly the sequential table state;
+// A final lane has no earlier pending writer that could touch its decision
+// slot, and duplicates change nothing, so its outcome is the sequential one;
 // a lane after it that writes into its window does so after it read.  Mostly
 // duplicates (repeated edges) therefore finish in few rounds (3.1 per 256-signal
-// chunk at C2, against 1.8 per 64-signal chunk: 2.3x fewer rounds per signal).
+// chunk at C2 with window conflicts, against 1.8 per 64-signal chunk).
 // Rounds need workgroup barriers; they are LDS-only (lds_barrier), so the
 // trace loads in flight are never drained.  The trace is read kEdgeDepth
 // chunks ahead of the chunk being deduplicated, ping-ponging between two
@@ -40,6 +44,12 @@ constexpr uint32_t kEdgeDepthSignals = 4;  // trace signals in flight per lane p
 #define SYZ_EDGE_KS 1
 #endif
 constexpr uint32_t kEdgeKS = SYZ_EDGE_KS;  // signals per lane per chunk
+#ifndef SYZ_EDGE_DEC
+// blocking test by decision slot, marks by window (2); marks by decision slot
+// too (1: a blocked writer then needs another marking pass); by window (0,
+// rounds 1-3).  C2: 12.7 / 14.5 / 13.6 ms global walk, 13.8 / 13.8 / 15.1 region
+#define SYZ_EDGE_DEC 2
+#endif
 
 // Geometry of one variant: W waves per program, KS signals per lane, chunks of
 // 64 * W * KS signals (lane l of wave w holds positions k * 64 W + 64 w + l,
@@ -162,7 +172,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 			// chunk q of the call; false once the program aborts
 			auto chunk = [&](const uint64_t (&pcv)[KS], uint32_t q) -> bool {
 				uint32_t sig[KS], b0[KS], b1[KS], v[KS], wpos[KS];
-				bool pending[KS], emit[KS], writer[KS], marker[KS], blocked[KS], mark_now[KS];
+				bool pending[KS], emit[KS], writer[KS], blocked[KS], mark_now[KS];
 				bool bad = false;
 #pragma unroll
 				for (uint32_t k = 0; k < KS; k++) {
@@ -220,6 +230,59 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						lds_barrier();
 					}
 					epoch++;
+#if SYZ_EDGE_DEC
+					// Exact dependences, at bin granularity: a lane's outcome depends on
+					// its decision slot only (the first match or zero of its window, or
+					// h for the forced overwrite = its write position): an earlier write
+					// of a nonzero value != sig elsewhere in the window changes no
+					// predicate the lane evaluated, and an earlier lane with the same
+					// sig has the same decision slot.  So a final-candidate writer marks
+					// the bin of its write position, a lane is blocked by an earlier
+					// mark in the bin of its decision slot, and a blocked lane (whose
+					// re-run may write anywhere in its window) marks its window's bins.
+					uint32_t dbin[KS];
+					bool mark_win[KS], win_marked[KS];
+#pragma unroll
+					for (uint32_t k = 0; k < KS; k++) {
+						v[k] = (epoch << G::kPosBits) | (G::kPosMask - (k * kLanes + pos));
+						dbin[k] = wpos[k] >> kBinShift;
+#if SYZ_EDGE_DEC == 2
+						// writers mark their whole window at once (a blocked writer then
+						// needs no second marking pass); only the test is by decision slot
+						mark_now[k] = false;
+						mark_win[k] = win_marked[k] = pending[k] && writer[k];
+#else
+						mark_now[k] = pending[k] && writer[k];
+						mark_win[k] = win_marked[k] = false;
+#endif
+						blocked[k] = false;
+					}
+					for (;;) {
+#pragma unroll
+						for (uint32_t k = 0; k < KS; k++) {
+							if (mark_now[k])
+								atomicMax(&stamp[dbin[k]], v[k]);
+							if (mark_win[k]) {
+								atomicMax(&stamp[b0[k]], v[k]);
+								if (b1[k] != b0[k])
+									atomicMax(&stamp[b1[k]], v[k]);
+							}
+						}
+						lds_barrier();
+						bool any_new = false;
+#pragma unroll
+						for (uint32_t k = 0; k < KS; k++) {
+							blocked[k] = pending[k] && stamp[dbin[k]] > v[k];
+							mark_now[k] = false;
+							mark_win[k] = blocked[k] && !win_marked[k];
+							win_marked[k] = win_marked[k] || mark_win[k];
+							any_new |= mark_win[k];
+						}
+						if (!wg_any(any_new, 0))
+							break;
+					}
+#else
+					bool marker[KS];
 #pragma unroll
 					for (uint32_t k = 0; k < KS; k++) {
 						v[k] = (epoch << G::kPosBits) | (G::kPosMask - (k * kLanes + pos));
@@ -249,6 +312,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						if (!wg_any(any_new, 0))
 							break;
 					}
+#endif
 					// 3. final lanes commit (visible after the next round's barrier)
 					bool any_pending = false;
 					uint32_t counts = 0;
