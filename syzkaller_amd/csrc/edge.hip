@@ -15,14 +15,16 @@
 // writes nothing.  Per chunk, lanes run in rounds:
 //   1. every pending lane evaluates dedup() against the table as it stands
 //      (read only): duplicate, or a write at some slot of its window;
-//   2. writers mark the 8-slot bins their window touches (LDS stamps keep the
+//   2. writers mark 8-slot bins of their window (LDS stamps keep the
 //      earliest marking position per bin); a pending lane with an EARLIER
 //      marker in the bin of its DECISION slot (the first match or zero of its
 //      window, or h for the forced overwrite) is blocked -- an earlier write of
 //      a nonzero value != sig anywhere else in the window changes none of the
 //      predicates it evaluated, and an earlier lane with the same sig has the
-//      same decision slot -- and marks its own window's bins too, since its
-//      re-run may turn into a write (repeated until no new marks);
+//      same decision slot -- and marks its own bins too, since its re-run may
+//      turn into a write (repeated until no new marks).  Marks cover the slots
+//      a lane can write, now or after a re-run: h, and the slots of its window
+//      that are empty now (a slot never becomes empty again);
 //   3. unblocked lanes are final: writers store, everyone leaves the round.
 // A final lane has no earlier pending writer that could touch its decision
 // slot, and duplicates change nothing, so its outcome is the sequential one;
@@ -45,10 +47,12 @@ constexpr uint32_t kEdgeDepthSignals = 4;  // trace signals in flight per lane p
 #endif
 constexpr uint32_t kEdgeKS = SYZ_EDGE_KS;  // signals per lane per chunk
 #ifndef SYZ_EDGE_DEC
-// blocking test by decision slot, marks by window (2); marks by decision slot
-// too (1: a blocked writer then needs another marking pass); by window (0,
-// rounds 1-3).  C2: 12.7 / 14.5 / 13.6 ms global walk, 13.8 / 13.8 / 15.1 region
-#define SYZ_EDGE_DEC 2
+// 3: blocking test by decision slot, marks on the bins of the slots a lane can
+// write now or after a re-run (h and the slots empty now); 2: marks by window;
+// 1: writers mark their write position only (a blocked writer then needs
+// another marking pass); 0: test and marks by window (rounds 1-3).  C2:
+// 12.2 / 12.7 / 14.5 / 13.6 ms global walk, 13.4 / 13.9 / 13.8 / 15.1 region
+#define SYZ_EDGE_DEC 3
 #endif
 
 // Geometry of one variant: W waves per program, KS signals per lane, chunks of
@@ -205,6 +209,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 				// rounds until no lane is pending (a chunk always has a valid lane, so
 				// the first round needs no test); the test after the last round also
 				// publishes every wave's emit counts for the output below
+				bool wb1[KS];  // the window's second bin takes a mark
 				for (;;) {
 					// 1. evaluate dedup() (executor.h:692-706) on the current table,
 					// branch-free: the first probe i with T[h+i] == sig (duplicate)
@@ -221,6 +226,14 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						const uint32_t first = __builtin_ctz(eqm | zm | 16u);
 						writer[k] = !((eqm >> first) & 1);
 						wpos[k] = (sig[k] + (first & 3)) & (kDedupSize - 1);
+#if SYZ_EDGE_DEC >= 3
+						// whatever it writes, now or after a re-run, goes to h or to a slot
+						// that is empty now (a slot never becomes empty again): the second
+						// bin of the window is marked only if such a slot lies in it
+						wb1[k] = b1[k] != b0[k] && ((1u | zm) >> (8u - (sig[k] & 7u))) != 0;
+#else
+						wb1[k] = b1[k] != b0[k];
+#endif
 					}
 					// 2. mark / block until stable
 					if (epoch == kEpochMax) {
@@ -236,17 +249,17 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 					// h for the forced overwrite = its write position): an earlier write
 					// of a nonzero value != sig elsewhere in the window changes no
 					// predicate the lane evaluated, and an earlier lane with the same
-					// sig has the same decision slot.  So a final-candidate writer marks
-					// the bin of its write position, a lane is blocked by an earlier
-					// mark in the bin of its decision slot, and a blocked lane (whose
-					// re-run may write anywhere in its window) marks its window's bins.
+					// sig has the same decision slot.  So a lane is blocked by an
+					// earlier mark in the bin of its decision slot, and a writer or a
+					// blocked lane marks the bins of every slot it could write, now or
+					// after a re-run (SYZ_EDGE_DEC 3: h and the slots empty now).
 					uint32_t dbin[KS];
 					bool mark_win[KS], win_marked[KS];
 #pragma unroll
 					for (uint32_t k = 0; k < KS; k++) {
 						v[k] = (epoch << G::kPosBits) | (G::kPosMask - (k * kLanes + pos));
 						dbin[k] = wpos[k] >> kBinShift;
-#if SYZ_EDGE_DEC == 2
+#if SYZ_EDGE_DEC >= 2
 						// writers mark their whole window at once (a blocked writer then
 						// needs no second marking pass); only the test is by decision slot
 						mark_now[k] = false;
@@ -264,7 +277,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 								atomicMax(&stamp[dbin[k]], v[k]);
 							if (mark_win[k]) {
 								atomicMax(&stamp[b0[k]], v[k]);
-								if (b1[k] != b0[k])
+								if (wb1[k])
 									atomicMax(&stamp[b1[k]], v[k]);
 							}
 						}
