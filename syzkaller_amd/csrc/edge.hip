@@ -24,7 +24,12 @@
 //      same decision slot -- and marks its own bins too, since its re-run may
 //      turn into a write (repeated until no new marks).  Marks cover the slots
 //      a lane can write, now or after a re-run: h, and the slots of its window
-//      that are empty now (a slot never becomes empty again);
+//      that are empty now (a slot never becomes empty again), and a blocked
+//      lane's decision slot (a later lane must not write what it will read
+//      again).  The test is at slot resolution: an earlier mark in the slot's
+//      bin, and a mark on the slot itself by another lane (per-slot bits,
+//      conservative about which lane: the earliest pending lane is never
+//      blocked, so every round finalises at least one lane);
 //   3. unblocked lanes are final: writers store, everyone leaves the round.
 // A final lane has no earlier pending writer that could touch its decision
 // slot, and duplicates change nothing, so its outcome is the sequential one;
@@ -47,12 +52,16 @@ constexpr uint32_t kEdgeDepthSignals = 4;  // trace signals in flight per lane p
 #endif
 constexpr uint32_t kEdgeKS = SYZ_EDGE_KS;  // signals per lane per chunk
 #ifndef SYZ_EDGE_DEC
-// 3: blocking test by decision slot, marks on the bins of the slots a lane can
-// write now or after a re-run (h and the slots empty now); 2: marks by window;
-// 1: writers mark their write position only (a blocked writer then needs
-// another marking pass); 0: test and marks by window (rounds 1-3).  C2:
-// 12.2 / 12.7 / 14.5 / 13.6 ms global walk, 13.4 / 13.9 / 13.8 / 15.1 region
-#define SYZ_EDGE_DEC 3
+// 4: blocking test by decision slot at slot resolution (a bin mark earlier
+// than the lane, and a mark on the slot itself by another lane: per-slot
+// once/twice bits, cleared every round), marks on the slots a lane can write
+// now or after a re-run (h and the slots empty now) plus, for a blocked lane,
+// its decision slot; 3: the same at 8-slot bins; 2: marks by window; 1:
+// writers mark their write position only (a blocked writer then needs
+// another marking pass); 0: test and marks by window (rounds 1-3).  C2 K1+K2:
+// 11.4 / 12.2 / 12.7 / 14.5 / 13.6 ms global walk, 13.5 / 13.3 / 13.9 / 13.8 /
+// 15.1 region
+#define SYZ_EDGE_DEC 4
 #endif
 
 // Geometry of one variant: W waves per program, KS signals per lane, chunks of
@@ -96,6 +105,11 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 	constexpr uint32_t kDepth = G::kDepth;
 	__shared__ uint32_t table[kDedupSize];
 	__shared__ uint32_t stamp[kBins];
+#if SYZ_EDGE_DEC >= 4
+	// per-slot marks of the current round: fm1 = marked at least once, fm2 =
+	// marked at least twice (2 KB: four programs still fit a CU's LDS)
+	__shared__ uint32_t fm1[kDedupSize / 32], fm2[kDedupSize / 32];
+#endif
 	__shared__ __align__(16) uint32_t s_any[2][kEdgeWaves];
 	__shared__ uint32_t s_carry[2][KS][kEdgeWaves];
 	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, pos = threadIdx.x;  // pos: place in a sub-chunk
@@ -141,6 +155,10 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 			reinterpret_cast<uint4*>(table)[i] = make_uint4(0, 0, 0, 0);
 		for (uint32_t i = threadIdx.x; i < kBins; i += kLanes)
 			stamp[i] = 0;
+#if SYZ_EDGE_DEC >= 4
+		for (uint32_t i = threadIdx.x; i < kDedupSize / 32; i += kLanes)
+			fm1[i] = fm2[i] = 0;
+#endif
 		epoch = 0;
 		lds_barrier();
 		uint64_t done = ce - cb;
@@ -210,6 +228,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 				// the first round needs no test); the test after the last round also
 				// publishes every wave's emit counts for the output below
 				bool wb1[KS];  // the window's second bin takes a mark
+				uint32_t pset[KS];  // window offsets the lane can write: 0 (h) and the empty slots
 				for (;;) {
 					// 1. evaluate dedup() (executor.h:692-706) on the current table,
 					// branch-free: the first probe i with T[h+i] == sig (duplicate)
@@ -226,6 +245,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						const uint32_t first = __builtin_ctz(eqm | zm | 16u);
 						writer[k] = !((eqm >> first) & 1);
 						wpos[k] = (sig[k] + (first & 3)) & (kDedupSize - 1);
+						pset[k] = 1u | zm;
 #if SYZ_EDGE_DEC >= 3
 						// whatever it writes, now or after a re-run, goes to h or to a slot
 						// that is empty now (a slot never becomes empty again): the second
@@ -279,13 +299,40 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 								atomicMax(&stamp[b0[k]], v[k]);
 								if (wb1[k])
 									atomicMax(&stamp[b1[k]], v[k]);
+#if SYZ_EDGE_DEC >= 4
+								// the slots themselves, counted up to two
+								const uint32_t hs = sig[k] & (kDedupSize - 1), off = hs & 31;
+								// (a blocked lane also its decision slot: a later lane must not
+								// write what it will read again)
+								const uint64_t m = (uint64_t)(pset[k] | 1u << ((wpos[k] - sig[k]) & 3)) << off;
+								const uint32_t wa = hs >> 5, wbw = (wa + 1) & (kDedupSize / 32 - 1);
+								const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+								const uint32_t oa = atomicOr(&fm1[wa], lo);
+								if (oa & lo)
+									atomicOr(&fm2[wa], oa & lo);
+								if (hi) {
+									const uint32_t ob = atomicOr(&fm1[wbw], hi);
+									if (ob & hi)
+										atomicOr(&fm2[wbw], ob & hi);
+								}
+#endif
 							}
 						}
 						lds_barrier();
 						bool any_new = false;
 #pragma unroll
 						for (uint32_t k = 0; k < KS; k++) {
+#if SYZ_EDGE_DEC >= 4
+							// an earlier mark in the decision slot's bin, and a mark on the slot
+							// itself by some other lane (conservative: that lane may be a later
+							// one; the earliest pending lane is never blocked)
+							const uint32_t fb = 1u << (wpos[k] & 31);
+							const bool mine = win_marked[k];  // (its marks include its decision slot)
+							const uint32_t fw = mine ? fm2[wpos[k] >> 5] : fm1[wpos[k] >> 5];
+							blocked[k] = pending[k] && stamp[dbin[k]] > v[k] && (fw & fb);
+#else
 							blocked[k] = pending[k] && stamp[dbin[k]] > v[k];
+#endif
 							mark_now[k] = false;
 							mark_win[k] = blocked[k] && !win_marked[k];
 							win_marked[k] = win_marked[k] || mark_win[k];
@@ -294,6 +341,12 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						if (!wg_any(any_new, 0))
 							break;
 					}
+#if SYZ_EDGE_DEC >= 4
+					// this round's slot marks are read: cleared for the next round (the
+					// commit's barrier orders this before the next round's marks)
+					for (uint32_t i = threadIdx.x; i < kDedupSize / 32; i += kLanes)
+						fm1[i] = fm2[i] = 0;
+#endif
 #else
 					bool marker[KS];
 #pragma unroll
