@@ -65,6 +65,9 @@ constexpr uint32_t kAggLimit = kAggSlots * 4 / 5;  // distinct elements before a
 static_assert(kAggLimit == kAggLimitRecs, "internal.h mirror");
 constexpr double kAggTargetLoad = 0.4;             // partitions are sized for this LDS load
 constexpr double kAggTargetLoadEntry = 0.6;        // ... and for Minimize
+#ifndef SYZ_MIN_ITEMS
+#define SYZ_MIN_ITEMS 2048  // Minimize: at least this many partitioning work items
+#endif
 constexpr uint32_t kAggEmpty = 0xFFFFFFFFu;        // empty key (LDS keys are residuals < 2^29)
 constexpr uint32_t kAggNone = 0xFFFFFFFFu;         // no record at this level
 constexpr uint32_t kAggOverflow = 0xFFFFFFFFu;     // partition count marker
@@ -2089,7 +2092,7 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	// order) make the first chunks far heavier than the last: >= ~2048 items.
 	g.ibits = g.cbits();
 	if (entry)
-		while (g.ibits > 0 && ((c1 - c0) >> g.ibits) < 2048)
+		while (g.ibits > 0 && ((c1 - c0) >> g.ibits) < SYZ_MIN_ITEMS)
 			g.ibits--;
 	const bool counted_once = ctx->agg_counted_once;
 	ctx->agg_counted_once = false;
