@@ -75,12 +75,16 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
  * of the aggregation path;
  * SYZSIG_DEBUG_EXACT_CELLS = large triage runs partition records into counted
  * cells (count pass + scan) instead of capped cells;
+ * SYZSIG_DEBUG_RECS_GATE = the LDS-partitioned records path (records mode,
+ * the owner side of a sharded step) reports every input as over its capacity,
+ * so the per-record path and the step's owner fix-up run (tests).
  * SYZSIG_DEBUG_CAP_SPILL = capped cells of 64 records, so that dense runs
  * overflow them and take the redo with counted cells. */
 #define SYZSIG_DEBUG_FIN_DEFER 32u
 #define SYZSIG_DEBUG_MIN_ATOMIC 64u
 #define SYZSIG_DEBUG_EXACT_CELLS 128u
 #define SYZSIG_DEBUG_CAP_SPILL 256u
+#define SYZSIG_DEBUG_RECS_GATE 512u
 int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
 
 /* ---- pkg/signal/signal.go ---- */

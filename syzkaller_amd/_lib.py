@@ -20,6 +20,7 @@ SYZSIG_DEBUG_FIN_DEFER = 32
 SYZSIG_DEBUG_MIN_ATOMIC = 64
 SYZSIG_DEBUG_EXACT_CELLS = 128
 SYZSIG_DEBUG_CAP_SPILL = 256
+SYZSIG_DEBUG_RECS_GATE = 512
 
 
 class SyzsigError(RuntimeError):

@@ -71,7 +71,8 @@ struct Workspace {
 
 // the debug flags that change only the path taken, never a result
 constexpr uint32_t kDebugResultPreserving =
-    SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL;
+    SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL |
+    SYZSIG_DEBUG_RECS_GATE;
 
 // capped cells of the aggregation path (agg.hip): default slack, in standard deviations
 constexpr float kCapSdDefault = 6.0f;

@@ -127,7 +127,7 @@ __global__ __launch_bounds__(1024) void k_rp_colsum(const uint32_t* __restrict__
 // partition bases (exclusive scan of tot into base[0..P]); the gate when a
 // partition has more than kRpCap records; records and the largest partition
 __global__ __launch_bounds__(1024) void k_rp_scan(const uint32_t* __restrict__ tot, uint32_t P, uint32_t* base,
-                                                  unsigned long long* ctr)
+                                                  unsigned long long* ctr, uint32_t force_gate)
 {
 	__shared__ uint32_t part[1024];
 	__shared__ uint32_t mx[1024];
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(1024) void k_rp_scan(const uint32_t* __restrict__ t
 		base[P] = run;
 		ctr[kCntRecords] = run;
 		ctr[kCntAux2] = mm;
-		if (mm > kRpCap)
+		if (mm > kRpCap || force_gate)  // (force_gate: SYZSIG_DEBUG_RECS_GATE, tests)
 			ctr[kCntSpill] |= 2ull;
 	}
 	__syncthreads();
@@ -560,7 +560,7 @@ int rp_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set* nsp, const RpSrc& src0, 
 	const uint32_t cg = (P + 63) / 64;
 	k_rp_count<<<(uint32_t)ntiles, kRpTileThreads, P * 4, s>>>(src, pbits, lm.n, cnt, ctr);
 	k_rp_colsum<<<cg, 1024, 0, s>>>(cnt, (uint32_t)ntiles, P, gsum, tot, ctr);
-	k_rp_scan<<<1, 1024, 0, s>>>(tot, P, base, ctr);
+	k_rp_scan<<<1, 1024, 0, s>>>(tot, P, base, ctr, ctx->agg_dbg & SYZSIG_DEBUG_RECS_GATE);
 	k_rp_coloffs<<<cg, 1024, 0, s>>>(cnt, (uint32_t)ntiles, P, gsum, base, ctr);
 	k_rp_scatter<<<(uint32_t)ntiles, kRpTileThreads, P * 4, s>>>(src, pbits, cnt, base, keys, idx, ctr);
 	const RpTables tb{ms->slots, ms->nbuckets - 1, nsp->slots, nsp->nbuckets - 1};

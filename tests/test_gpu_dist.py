@@ -30,7 +30,7 @@ def _port():
     return p
 
 
-def worker(rank, world, port, outdir, want_bits, cap):
+def worker(rank, world, port, outdir, want_bits, cap, gate=False):
     import torch
     import torch.distributed as dist
 
@@ -43,6 +43,10 @@ def worker(rank, world, port, outdir, want_bits, cap):
     torch.cuda.set_device(0)
     dev = Device(0)
     dev.L.syzsig_ctx_set_timing(dev.eng.h, 1)
+    if gate:  # every owner's LDS records pass reports an overflow: the fix-up path
+        from syzkaller_amd._lib import SYZSIG_DEBUG_RECS_GATE
+
+        dev.L.syzsig_ctx_set_debug(dev.eng.h, SYZSIG_DEBUG_RECS_GATE)
     cfg = synth.synth_default(skew=1)
     se, sp = dev.synth_m0_shard(cfg, KNOWN, NM0, world, rank)  # this rank's shard of M0, in index order
     ms = dev.deserialize(se, sp)
@@ -79,19 +83,24 @@ def worker(rank, world, port, outdir, want_bits, cap):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,want_bits,cap", [(2, True, None), (2, False, None), (2, False, 256),
-                                                  (4, True, None), (4, False, 256)])
-def test_gpu_sharded_step_gloo(world, want_bits, cap):
+@pytest.mark.parametrize("world,want_bits,cap,gate", [(2, True, None, False), (2, False, None, False),
+                                                       (2, False, 256, False), (4, True, None, False),
+                                                       (4, False, 256, False), (2, True, None, True)])
+def test_gpu_sharded_step_gloo(world, want_bits, cap, gate):
     """The stream-ordered step (syzsig_step_*: staircase buckets, equal-split
     exchanges, the owners' LDS-partitioned replay, flags back) on the real
     kernels, 2 or 4 ranks on one GPU over gloo, two consecutive batches;
     cap=256 overflows the first step's buckets, which is redone with a larger
-    cap."""
+    cap; gate: every owner skips its LDS pass, so every step takes the owner
+    fix-up (per-record redo, a second flags exchange)."""
     from tests.test_gpu_triage import oracle_pairs
     from syzkaller_amd import synth
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(worker, args=(world, _port(), d, want_bits, cap), nprocs=world, start_method="spawn")
+        mp.start_processes(worker, args=(world, _port(), d, want_bits, cap, gate), nprocs=world,
+                           start_method="spawn")
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
+    if gate:
+        assert all(int(x["redos"][1]) == 2 for x in res)  # one fix-up per step
     cfg = synth.synth_default(skew=1)
     m0e, m0p = synth.m0(cfg, KNOWN, NM0)
     oms = O.deserialize(m0e, m0p)
