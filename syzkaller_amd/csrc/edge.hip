@@ -51,18 +51,6 @@ constexpr uint32_t kEdgeDepthSignals = 4;  // trace signals in flight per lane p
 #define SYZ_EDGE_KS 1
 #endif
 constexpr uint32_t kEdgeKS = SYZ_EDGE_KS;  // signals per lane per chunk
-#ifndef SYZ_EDGE_DEC
-// 4: blocking test by decision slot at slot resolution (a bin mark earlier
-// than the lane, and a mark on the slot itself by another lane: per-slot
-// once/twice bits, cleared every round), marks on the slots a lane can write
-// now or after a re-run (h and the slots empty now) plus, for a blocked lane,
-// its decision slot; 3: the same at 8-slot bins; 2: marks by window; 1:
-// writers mark their write position only (a blocked writer then needs
-// another marking pass); 0: test and marks by window (rounds 1-3).  C2 K1+K2:
-// 11.4 / 12.2 / 12.7 / 14.5 / 13.6 ms global walk, 13.5 / 13.3 / 13.9 / 13.8 /
-// 15.1 region
-#define SYZ_EDGE_DEC 4
-#endif
 
 // Geometry of one variant: W waves per program, KS signals per lane, chunks of
 // 64 * W * KS signals (lane l of wave w holds positions k * 64 W + 64 w + l,
@@ -105,11 +93,9 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 	constexpr uint32_t kDepth = G::kDepth;
 	__shared__ uint32_t table[kDedupSize];
 	__shared__ uint32_t stamp[kBins];
-#if SYZ_EDGE_DEC >= 4
 	// per-slot marks of the current round: fm1 = marked at least once, fm2 =
 	// marked at least twice (2 KB: four programs still fit a CU's LDS)
 	__shared__ uint32_t fm1[kDedupSize / 32], fm2[kDedupSize / 32];
-#endif
 	__shared__ __align__(16) uint32_t s_any[2][kEdgeWaves];
 	__shared__ uint32_t s_carry[2][KS][kEdgeWaves];
 	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, pos = threadIdx.x;  // pos: place in a sub-chunk
@@ -155,10 +141,8 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 			reinterpret_cast<uint4*>(table)[i] = make_uint4(0, 0, 0, 0);
 		for (uint32_t i = threadIdx.x; i < kBins; i += kLanes)
 			stamp[i] = 0;
-#if SYZ_EDGE_DEC >= 4
 		for (uint32_t i = threadIdx.x; i < kDedupSize / 32; i += kLanes)
 			fm1[i] = fm2[i] = 0;
-#endif
 		epoch = 0;
 		lds_barrier();
 		uint64_t done = ce - cb;
@@ -194,7 +178,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 			// chunk q of the call; false once the program aborts
 			auto chunk = [&](const uint64_t (&pcv)[KS], uint32_t q) -> bool {
 				uint32_t sig[KS], b0[KS], b1[KS], v[KS], wpos[KS];
-				bool pending[KS], emit[KS], writer[KS], blocked[KS], mark_now[KS];
+				bool pending[KS], emit[KS], writer[KS], blocked[KS];
 				bool bad = false;
 #pragma unroll
 				for (uint32_t k = 0; k < KS; k++) {
@@ -246,14 +230,10 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						writer[k] = !((eqm >> first) & 1);
 						wpos[k] = (sig[k] + (first & 3)) & (kDedupSize - 1);
 						pset[k] = 1u | zm;
-#if SYZ_EDGE_DEC >= 3
 						// whatever it writes, now or after a re-run, goes to h or to a slot
 						// that is empty now (a slot never becomes empty again): the second
 						// bin of the window is marked only if such a slot lies in it
 						wb1[k] = b1[k] != b0[k] && ((1u | zm) >> (8u - (sig[k] & 7u))) != 0;
-#else
-						wb1[k] = b1[k] != b0[k];
-#endif
 					}
 					// 2. mark / block until stable
 					if (epoch == kEpochMax) {
@@ -263,47 +243,26 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						lds_barrier();
 					}
 					epoch++;
-#if SYZ_EDGE_DEC
-					// Exact dependences, at bin granularity: a lane's outcome depends on
-					// its decision slot only (the first match or zero of its window, or
-					// h for the forced overwrite = its write position): an earlier write
-					// of a nonzero value != sig elsewhere in the window changes no
-					// predicate the lane evaluated, and an earlier lane with the same
-					// sig has the same decision slot.  So a lane is blocked by an
-					// earlier mark in the bin of its decision slot, and a writer or a
-					// blocked lane marks the bins of every slot it could write, now or
-					// after a re-run (SYZ_EDGE_DEC 3: h and the slots empty now).
+					// (the conflict rule: header of this file)
 					uint32_t dbin[KS];
 					bool mark_win[KS], win_marked[KS];
 #pragma unroll
 					for (uint32_t k = 0; k < KS; k++) {
 						v[k] = (epoch << G::kPosBits) | (G::kPosMask - (k * kLanes + pos));
 						dbin[k] = wpos[k] >> kBinShift;
-#if SYZ_EDGE_DEC >= 2
-						// writers mark their whole window at once (a blocked writer then
-						// needs no second marking pass); only the test is by decision slot
-						mark_now[k] = false;
 						mark_win[k] = win_marked[k] = pending[k] && writer[k];
-#else
-						mark_now[k] = pending[k] && writer[k];
-						mark_win[k] = win_marked[k] = false;
-#endif
 						blocked[k] = false;
 					}
 					for (;;) {
 #pragma unroll
 						for (uint32_t k = 0; k < KS; k++) {
-							if (mark_now[k])
-								atomicMax(&stamp[dbin[k]], v[k]);
 							if (mark_win[k]) {
 								atomicMax(&stamp[b0[k]], v[k]);
 								if (wb1[k])
 									atomicMax(&stamp[b1[k]], v[k]);
-#if SYZ_EDGE_DEC >= 4
-								// the slots themselves, counted up to two
+								// the slots themselves, counted up to two (a blocked lane also its
+								// decision slot: a later lane must not write what it will read again)
 								const uint32_t hs = sig[k] & (kDedupSize - 1), off = hs & 31;
-								// (a blocked lane also its decision slot: a later lane must not
-								// write what it will read again)
 								const uint64_t m = (uint64_t)(pset[k] | 1u << ((wpos[k] - sig[k]) & 3)) << off;
 								const uint32_t wa = hs >> 5, wbw = (wa + 1) & (kDedupSize / 32 - 1);
 								const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
@@ -315,14 +274,12 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 									if (ob & hi)
 										atomicOr(&fm2[wbw], ob & hi);
 								}
-#endif
 							}
 						}
 						lds_barrier();
 						bool any_new = false;
 #pragma unroll
 						for (uint32_t k = 0; k < KS; k++) {
-#if SYZ_EDGE_DEC >= 4
 							// an earlier mark in the decision slot's bin, and a mark on the slot
 							// itself by some other lane (conservative: that lane may be a later
 							// one; the earliest pending lane is never blocked)
@@ -330,10 +287,6 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 							const bool mine = win_marked[k];  // (its marks include its decision slot)
 							const uint32_t fw = mine ? fm2[wpos[k] >> 5] : fm1[wpos[k] >> 5];
 							blocked[k] = pending[k] && stamp[dbin[k]] > v[k] && (fw & fb);
-#else
-							blocked[k] = pending[k] && stamp[dbin[k]] > v[k];
-#endif
-							mark_now[k] = false;
 							mark_win[k] = blocked[k] && !win_marked[k];
 							win_marked[k] = win_marked[k] || mark_win[k];
 							any_new |= mark_win[k];
@@ -341,44 +294,10 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						if (!wg_any(any_new, 0))
 							break;
 					}
-#if SYZ_EDGE_DEC >= 4
 					// this round's slot marks are read: cleared for the next round (the
 					// commit's barrier orders this before the next round's marks)
 					for (uint32_t i = threadIdx.x; i < kDedupSize / 32; i += kLanes)
 						fm1[i] = fm2[i] = 0;
-#endif
-#else
-					bool marker[KS];
-#pragma unroll
-					for (uint32_t k = 0; k < KS; k++) {
-						v[k] = (epoch << G::kPosBits) | (G::kPosMask - (k * kLanes + pos));
-						marker[k] = pending[k] && writer[k];
-						mark_now[k] = marker[k];
-						blocked[k] = false;
-					}
-					for (;;) {
-#pragma unroll
-						for (uint32_t k = 0; k < KS; k++) {
-							if (mark_now[k]) {
-								atomicMax(&stamp[b0[k]], v[k]);
-								if (b1[k] != b0[k])
-									atomicMax(&stamp[b1[k]], v[k]);
-							}
-						}
-						lds_barrier();
-						bool any_new = false;
-#pragma unroll
-						for (uint32_t k = 0; k < KS; k++) {
-							const uint32_t s0 = stamp[b0[k]], s1 = stamp[b1[k]];
-							blocked[k] = pending[k] && (s0 > v[k] || s1 > v[k]);
-							mark_now[k] = blocked[k] && !marker[k];
-							marker[k] = marker[k] || mark_now[k];
-							any_new |= mark_now[k];
-						}
-						if (!wg_any(any_new, 0))
-							break;
-					}
-#endif
 					// 3. final lanes commit (visible after the next round's barrier)
 					bool any_pending = false;
 					uint32_t counts = 0;
