@@ -423,8 +423,9 @@ int syzsig_shard_agg_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uin
 #define SYZSIG_STEP_HDR_OVF (1ull << 62)
 #define SYZSIG_STEP_HDR_COUNT ((1ull << 40) - 1)
 typedef struct {
-	uint64_t src_void;     /* this source's run was void: 1 = a cell spilled or a partition overflowed the LDS
-	                          table (redo with exact = 1), 2 = a call's prio is not among `levels` */
+	uint64_t src_void;     /* this source's run was void: 1 = a cell spilled, a partition overflowed the LDS
+	                          table, a call range is bad or the records exceed b->nrec (redo with exact = 1,
+	                          which validates), 2 = a call's prio is not among `levels` */
 	uint64_t global_void;  /* some bucket was void or over cap: nothing was committed on any rank */
 	uint64_t owners_void;  /* bit g: owner g skipped its records (redo them exactly); 0 when global_void */
 	uint64_t records;      /* this source's records */

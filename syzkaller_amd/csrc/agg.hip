@@ -877,8 +877,8 @@ __global__ __launch_bounds__(256) void k_fast_prep(const uint64_t* __restrict__ 
 
 // k_cell_plan for the one-sync run: the counters are zeroed here (npairs
 // preset), the assumptions checked from k_fast_prep's partials -- prios in
-// 0..3, valid ranges, at most `guess` records -- and the run's void flag
-// (ctr[kCntSpill]) set before anything reads it.
+// 0..3 (else flag 2), valid ranges and at most `guess` records (else flag 4)
+// -- and the run's void flag (ctr[kCntSpill]) set before anything reads it.
 __global__ __launch_bounds__(1024) void k_cell_plan_fast(const uint64_t* __restrict__ sizes, uint64_t nchunks,
                                                          uint32_t P, float sd, uint64_t* base, uint32_t* cap,
                                                          const uint64_t* __restrict__ part, uint64_t guess,
@@ -907,7 +907,9 @@ __global__ __launch_bounds__(1024) void k_cell_plan_fast(const uint64_t* __restr
 	__syncthreads();
 	if (threadIdx.x == 0) {
 		ctr[kCntRecords] = s_tot;
-		ctr[kCntSpill] = s_flag || s_tot > guess ? 2u : 0u;
+		// 2: a prio outside the levels; 4: a bad call range or more records than
+		// `guess` (the caller's exact path validates and sizes those)
+		ctr[kCntSpill] = (s_flag >> 63 ? 2u : 0u) | ((s_flag & ~(1ull << 63)) || s_tot > guess ? 4u : 0u);
 	}
 	cell_plan(sizes, nchunks, P, sd, base, cap);
 }
@@ -2442,7 +2444,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		st->probe_ms += t1;
 		st->decide_ms += t2;
 	}
-	if (*hov & 2) {  // an optimistic run's assumptions failed: nothing committed
+	if (*hov & 6) {  // an optimistic run's assumptions failed: nothing committed
 		*assumed_bad = true;
 		if (fresh_ns) {
 			syzsig_set_free(nsp);

@@ -14,28 +14,37 @@
 // (insert at the first empty slot, or the forced overwrite at h); a duplicate
 // writes nothing.  Per chunk, lanes run in rounds:
 //   1. every pending lane evaluates dedup() against the table as it stands
-//      (read only): duplicate, or a write at some slot of its window;
-//   2. writers mark 8-slot bins of their window (LDS stamps keep the
-//      earliest marking position per bin); a pending lane with an EARLIER
-//      marker in the bin of its DECISION slot (the first match or zero of its
-//      window, or h for the forced overwrite) is blocked -- an earlier write of
-//      a nonzero value != sig anywhere else in the window changes none of the
-//      predicates it evaluated, and an earlier lane with the same sig has the
-//      same decision slot -- and marks its own bins too, since its re-run may
-//      turn into a write (repeated until no new marks).  Marks cover the slots
-//      a lane can write, now or after a re-run: h, and the slots of its window
-//      that are empty now (a slot never becomes empty again), and a blocked
-//      lane's decision slot (a later lane must not write what it will read
-//      again).  The test is at slot resolution: an earlier mark in the slot's
-//      bin, and a mark on the slot itself by another lane (per-slot bits,
-//      conservative about which lane: the earliest pending lane is never
-//      blocked, so every round finalises at least one lane);
+//      (read only): its DECISION slot d (the first match or zero of its
+//      window, or h for the forced overwrite), and whether it writes there;
+//   2. lanes mark slots (8-slot bin stamps keep the earliest marking position
+//      per bin; per-slot bits count markers up to two).  A pending lane is
+//      blocked iff an earlier lane marked d's bin and another lane marked d
+//      itself (conservative about which lane: the earliest pending lane is
+//      never blocked, so every round finalises at least one); a blocked lane
+//      marks too, and marking repeats until no new marks.  Writers mark in the
+//      first pass.  What a lane marks: every slot it can write, now or after a
+//      re-run -- h and its window's slots that are empty now -- and, when
+//      blocked, d (a later lane must not write what it will read again);
 //   3. unblocked lanes are final: writers store, everyone leaves the round.
-// A final lane has no earlier pending writer that could touch its decision
-// slot, and duplicates change nothing, so its outcome is the sequential one;
-// a lane after it that writes into its window does so after it read.  Mostly
-// duplicates (repeated edges) therefore finish in few rounds (3.1 per 256-signal
-// chunk at C2 with window conflicts, against 1.8 per 64-signal chunk).
+// Why that is exact: a lane's outcome depends on d only, as long as no slot
+// of its window becomes empty again.  An earlier write of a nonzero value !=
+// sig before d changes none of the predicates it evaluated (and an earlier
+// lane with the same sig has the same d), a write at d is marked, and a later
+// final lane writes only slots no pending earlier lane can still read.  The
+// one write that empties a slot is the forced overwrite of sig == 0, which
+// stores 0 at slot 0 (executor.h:704).  Inside a window holding slot 0 (h in
+// 8189..8191, 0) a slot can therefore hold sig while slot 0 before it is
+// empty, so the lane's decision can move past today's d once slot 0 fills
+// again, and a later zero write changes a slot it read.  Hence two more marks
+// (tests/test_edge_rounds_cpu.py restates them and stresses them against
+// sequential dedup on zero-heavy chunks; golden executor_zero2 pins them):
+//   - a lane whose window holds slot 0 marks its whole window;
+//   - a sig == 0 lane marks 8189..8191 and 0..3: every decision slot of a
+//     window holding slot 0, so such a later lane waits for the zero write.
+// A final lane has no earlier pending writer that could touch what it read,
+// and duplicates change nothing, so its outcome is the sequential one.
+// Mostly duplicates (repeated edges) finish in few rounds (2.3 per 256-signal
+// chunk on the global walk, 2.5 on the region walk: host simulation).
 // Rounds need workgroup barriers; they are LDS-only (lds_barrier), so the
 // trace loads in flight are never drained.  The trace is read kEdgeDepth
 // chunks ahead of the chunk being deduplicated, ping-ponging between two
@@ -229,11 +238,13 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						const uint32_t first = __builtin_ctz(eqm | zm | 16u);
 						writer[k] = !((eqm >> first) & 1);
 						wpos[k] = (sig[k] + (first & 3)) & (kDedupSize - 1);
-						pset[k] = 1u | zm;
 						// whatever it writes, now or after a re-run, goes to h or to a slot
-						// that is empty now (a slot never becomes empty again): the second
-						// bin of the window is marked only if such a slot lies in it
-						wb1[k] = b1[k] != b0[k] && ((1u | zm) >> (8u - (sig[k] & 7u))) != 0;
+						// that is empty now (only slot 0 ever becomes empty again); a window
+						// holding slot 0 is marked whole (header); the second bin of the
+						// window is marked only if a marked slot lies in it
+						const uint32_t hs = sig[k] & (kDedupSize - 1);
+						pset[k] = hs >= kDedupSize - 3 || hs == 0 ? 15u : 1u | zm;
+						wb1[k] = b1[k] != b0[k] && (pset[k] >> (8u - (sig[k] & 7u))) != 0;
 					}
 					// 2. mark / block until stable
 					if (epoch == kEpochMax) {
@@ -273,6 +284,15 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 									const uint32_t ob = atomicOr(&fm1[wbw], hi);
 									if (ob & hi)
 										atomicOr(&fm2[wbw], ob & hi);
+								}
+								if (sig[k] == 0) {
+									// the zero write empties slot 0: it also marks 8189..8191 (with
+									// 0..3, every decision slot of a window that holds slot 0)
+									constexpr uint32_t zw = kDedupSize / 32 - 1, zb = 7u << 29;
+									atomicMax(&stamp[kBins - 1], v[k]);
+									const uint32_t oz = atomicOr(&fm1[zw], zb);
+									if (oz & zb)
+										atomicOr(&fm2[zw], oz & zb);
 								}
 							}
 						}

@@ -685,61 +685,70 @@ int syzsig_step_own_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set* new_sign
 	shard->step_busy = new_signal->step_busy = true;
 	ctx->step_ms = shard;
 	ctx->step_ns = new_signal;
-	if (!exact) {
-		const RpSrc src{d_recv, stride, 1, nshards, seg_cnt, 0, 0};
-		uint32_t pbits = 0;
-		SYZ_TRY(rp_run(ctx, shard, new_signal, src, bound, lm, d_flags, oc, &pbits));
-		ctx->step_parts = 1ull << pbits;
-	} else {
-		// the per-record path over this owner's records, compacted (host round trips)
-		ctx->step_parts = 0;
-		unsigned long long* hc = ctx->h_step + kStepOwn;
-		SYZ_HIP(hipMemcpyAsync(hc, oc, kNumCounters * 8, hipMemcpyDeviceToHost, s));
-		std::vector<uint64_t> cnt(nshards);
-		SYZ_HIP(hipMemcpyAsync(cnt.data(), seg_cnt, nshards * 8, hipMemcpyDeviceToHost, s));
-		SYZ_HIP(hipStreamSynchronize(s));
-		const uint64_t gate = hc[kCntSpill];
-		if (!gate) {
-			std::vector<uint64_t> off(nshards);
-			uint64_t n = 0;
-			for (uint32_t g = 0; g < nshards; g++) {
-				off[g] = n;
-				n += cnt[g];
-			}
-			syzsig_batch_stats st;
-			memset(&st, 0, sizeof(st));
-			if (n) {
-				void *wr, *wf;
-				SYZ_TRY(ws_get(ctx, 61, n * 16 + 64, &wr));
-				SYZ_TRY(ws_get(ctx, 62, n + 64, &wf));
-				uint64_t* comp = (uint64_t*)wr;
-				uint64_t* slot = comp + n;
-				SYZ_HIP(hipMemcpyAsync(seg_off, off.data(), nshards * 8, hipMemcpyHostToDevice, s));
-				k_step_compact<<<dim3(grid_for(n, 256, 1024), nshards), 256, 0, s>>>(d_recv, nshards, cap, seg_cnt,
-				                                                                     seg_off, comp, slot);
-				SYZ_HIP(hipGetLastError());
-				syzsig_set* nsp = new_signal;
-				SYZ_TRY(triage_records_impl(ctx, shard, &nsp, comp, n, levels, nlevels, (uint8_t*)wf, &st, false));
-				k_step_uncompact<<<grid_for(n, 256, 8192), 256, 0, s>>>((const uint8_t*)wf, slot, n, d_flags);
-				SYZ_HIP(hipGetLastError());
-			}
-			// the owner counters as the LDS path leaves them; the lengths are
-			// already committed by the per-record path
-			hc[kCntInserted] = 0;
-			hc[kCntAux] = 0;
-			hc[kCntChanged] = st.changed;
-			hc[kCntDistinct] = st.distinct;
-			hc[kCntRecords] = n;
-			hc[kCntOverflow] = 0;
-			SYZ_HIP(hipMemcpyAsync(oc, hc, kNumCounters * 8, hipMemcpyHostToDevice, s));
+	// on an error past this point the sets are released again (no finish will
+	// come for this step)
+	const int rc = [&]() -> int {
+		if (!exact) {
+			const RpSrc src{d_recv, stride, 1, nshards, seg_cnt, 0, 0};
+			uint32_t pbits = 0;
+			SYZ_TRY(rp_run(ctx, shard, new_signal, src, bound, lm, d_flags, oc, &pbits));
+			ctx->step_parts = 1ull << pbits;
+		} else {
+			// the per-record path over this owner's records, compacted (host round trips)
+			ctx->step_parts = 0;
+			unsigned long long* hc = ctx->h_step + kStepOwn;
+			SYZ_HIP(hipMemcpyAsync(hc, oc, kNumCounters * 8, hipMemcpyDeviceToHost, s));
+			std::vector<uint64_t> cnt(nshards);
+			SYZ_HIP(hipMemcpyAsync(cnt.data(), seg_cnt, nshards * 8, hipMemcpyDeviceToHost, s));
 			SYZ_HIP(hipStreamSynchronize(s));
+			const uint64_t gate = hc[kCntSpill];
+			if (!gate) {
+				std::vector<uint64_t> off(nshards);
+				uint64_t n = 0;
+				for (uint32_t g = 0; g < nshards; g++) {
+					off[g] = n;
+					n += cnt[g];
+				}
+				syzsig_batch_stats st;
+				memset(&st, 0, sizeof(st));
+				if (n) {
+					void *wr, *wf;
+					SYZ_TRY(ws_get(ctx, 61, n * 16 + 64, &wr));
+					SYZ_TRY(ws_get(ctx, 62, n + 64, &wf));
+					uint64_t* comp = (uint64_t*)wr;
+					uint64_t* slot = comp + n;
+					SYZ_HIP(hipMemcpyAsync(seg_off, off.data(), nshards * 8, hipMemcpyHostToDevice, s));
+					k_step_compact<<<dim3(grid_for(n, 256, 1024), nshards), 256, 0, s>>>(d_recv, nshards, cap, seg_cnt,
+					                                                                     seg_off, comp, slot);
+					SYZ_HIP(hipGetLastError());
+					syzsig_set* nsp = new_signal;
+					SYZ_TRY(triage_records_impl(ctx, shard, &nsp, comp, n, levels, nlevels, (uint8_t*)wf, &st, false));
+					k_step_uncompact<<<grid_for(n, 256, 8192), 256, 0, s>>>((const uint8_t*)wf, slot, n, d_flags);
+					SYZ_HIP(hipGetLastError());
+				}
+				// the owner counters as the LDS path leaves them; the lengths are
+				// already committed by the per-record path
+				hc[kCntInserted] = 0;
+				hc[kCntAux] = 0;
+				hc[kCntChanged] = st.changed;
+				hc[kCntDistinct] = st.distinct;
+				hc[kCntRecords] = n;
+				hc[kCntOverflow] = 0;
+				SYZ_HIP(hipMemcpyAsync(oc, hc, kNumCounters * 8, hipMemcpyHostToDevice, s));
+				SYZ_HIP(hipStreamSynchronize(s));
+			}
 		}
+		k_step_status<<<1, 64, 0, s>>>(d_flags, nshards, cap, oc);
+		SYZ_HIP(hipGetLastError());
+		if (ctx->timing)
+			SYZ_HIP(hipEventRecord(ctx->ev_step[3], s));
+		return SYZSIG_OK;
+	}();
+	if (rc != SYZSIG_OK) {
+		shard->step_busy = new_signal->step_busy = false;
+		ctx->step_ms = ctx->step_ns = nullptr;
 	}
-	k_step_status<<<1, 64, 0, s>>>(d_flags, nshards, cap, oc);
-	SYZ_HIP(hipGetLastError());
-	if (ctx->timing)
-		SYZ_HIP(hipEventRecord(ctx->ev_step[3], s));
-	return SYZSIG_OK;
+	return rc;
 }
 
 int syzsig_step_finish(syzsig_ctx* ctx, syzsig_step_status* out)
@@ -753,10 +762,13 @@ int syzsig_step_finish(syzsig_ctx* ctx, syzsig_step_status* out)
 	const unsigned long long* h = ctx->h_step;
 	const unsigned long long *src = h + kStepSrc, *own = h + kStepOwn, *bk = h + kStepBack;
 	memset(out, 0, sizeof(*out));
-	out->src_void = src[kCntSpill] & 1 ? 1 : src[kCntSpill] ? 2 : src[kCntAggOvf] ? 1 : 0;
+	// 2 only for a prio outside the levels (an error); a spill (1), a bad call
+	// range or more records than assumed (4, k_cell_plan_fast) and LDS
+	// overflows send the source to its exact path, which validates and sizes
+	out->src_void = src[kCntSpill] & 2 ? 2 : src[kCntSpill] || src[kCntAggOvf] ? 1 : 0;
 	if (src[kCntSpill] & 1)  // a capped cell spilled: more slack for the next runs (as agg_capped does)
 		ctx->cap_sd = ctx->cap_sd * 2 > 24.0f ? 0.0f : ctx->cap_sd * 2;
-	if (!(src[kCntSpill] & 2) && src[kCntAggOvf] && src[kCntRecords]) {
+	if (!(src[kCntSpill] & 6) && src[kCntAggOvf] && src[kCntRecords]) {
 		// LDS partitions overflowed: the distinct-ratio guess was low; size the
 		// next runs for at least what was seen (as the one-sync triage run does)
 		const double P = (double)ctx->step_src_parts, novf = (double)src[kCntAggOvf];

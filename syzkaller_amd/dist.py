@@ -28,6 +28,9 @@ the exact serial semantics via the serial index carried in every record.
 import torch
 import torch.distributed as dist
 
+# include/syzsig.h SYZSIG_STEP_HDR_VOID (bit 63) as an int64 bucket word
+HDR_VOID = -(1 << 63)
+
 __all__ = ["owner_of_torch", "ShardedTriage", "GpuShardOps", "GpuMinimizeOps", "SIGNAL_PRIO_LEVELS",
            "sharded_minimize"]
 
@@ -163,23 +166,50 @@ class ShardedTriage:
         for attempt in range(4):
             cap = self.cap
             send, recv, flags, back = self._buffers(cap)
-            self.ops.send(batch, serial_base, levels, W, cap, send, self._exact)
+            # A rank whose send or own fails (a host-side check: ERANGE on its
+            # serial range, EINVAL, an allocation) must not leave its peers in
+            # the exchange, and the steady state has no host collective to
+            # agree on errors.  So the failure travels in-band: a failed send
+            # puts VOID headers in every bucket, a failed own the "void" status
+            # (1) in every flags bucket; every rank then sees a void step and
+            # the redo's agreement below raises on every rank alike.
+            err = None
+            try:
+                self.ops.send(batch, serial_base, levels, W, cap, send, self._exact)
+            except Exception as e:  # noqa: BLE001 -- raised on every rank below
+                err = e
+                send.view(W, cap + 1)[:, 0] = HDR_VOID
             dist.all_to_all_single(recv, send, group=g)
-            self.ops.own(self.shard, self.new_signal, recv, W, cap, levels, flags)
+            try:
+                self.ops.own(self.shard, self.new_signal, recv, W, cap, levels, flags)
+            except Exception as e:  # noqa: BLE001
+                err = err or e
+                flags.view(W, cap + 1)[:, 0] = 1
             dist.all_to_all_single(back, flags, group=g)
             self.ops.back(batch, serial_base, send, W, cap, back)
             st = self.ops.finish()  # the step's one host synchronisation
             if not st["global_void"]:
+                if err is not None:  # (not reachable: the failing rank's VOID reaches everyone)
+                    raise err
                 break
             # nothing was committed on any rank (every owner saw the same headers):
             # agree on a cap for what the sources counted, a void source takes its
             # exact path, and the step runs again
             self.redos += 1
-            need, bad = self._agree([st["max_out"], 1 if st["src_void"] == 2 else 0])
+            need, bad, failed = self._agree([st["max_out"] if err is None else 0,
+                                             1 if err is None and st["src_void"] == 2 else 0,
+                                             1 if err is not None else 0])
+            if failed:
+                if err is not None:
+                    raise err
+                raise RuntimeError("sharded step: the step failed on another rank")
             if bad:  # a call's prio outside the agreed levels: an error on every rank alike
                 raise ValueError("sharded step: a call's prio is not among the step's levels")
             self.cap = max(self.cap, self._cap_for(need)) if need > cap else self.cap
-            self._exact = st["src_void"] != 0
+            # a source that voided its run stays on its exact path for the rest of
+            # the step (a later cap overflow must not send it back to the capped
+            # cells, which would spill again)
+            self._exact = self._exact or st["src_void"] != 0
         else:
             raise RuntimeError("sharded step: still void after 4 attempts")
         self._exact = False
@@ -187,13 +217,22 @@ class ShardedTriage:
             # owners whose records overflowed the LDS partitions skipped them:
             # they redo them on the per-record path, the flags go back once more
             self.fixups += 1
+            err = None
             if (st["owners_void"] >> self.rank) & 1:
-                self.ops.own(self.shard, self.new_signal, recv, W, cap, levels, flags, True)
+                try:
+                    self.ops.own(self.shard, self.new_signal, recv, W, cap, levels, flags, True)
+                except Exception as e:  # noqa: BLE001 -- raised on every rank below
+                    err = e
+                    flags.view(W, cap + 1)[:, 0] = 1
             else:
                 flags.zero_()
             dist.all_to_all_single(back, flags, group=g)
             self.ops.back(batch, serial_base, send, W, cap, back)
             st2 = self.ops.finish()
+            if err is not None:
+                raise err
+            if st2["global_void"]:  # an owner's fix-up failed: every source sees its status
+                raise RuntimeError("sharded step: an owner's exact fix-up failed on another rank")
             for k in ("inserted", "changed", "own_distinct"):
                 st[k] += st2[k]
             st["new_pairs"] = st2["new_pairs"]

@@ -1,7 +1,7 @@
 """Generate the executor golden vectors from the REFERENCE executor itself.
 
 Run in the build container (needs /root/reference and `make -C oracle ref`):
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [fixture names]
 Inputs are synthetic KCOV traces (the engine's deterministic generator plus
 hand-crafted corner cases); expected outputs are the per-call signal records
 written by the reference's own handle_completion -> write_coverage_signal
@@ -54,6 +54,62 @@ def craft_call(targets, start_low=0x81000000):
     raise RuntimeError("no pc_0 found")
 
 
+def craft_free(targets, seed, far=(2048, 6144)):
+    """Like craft_call, for chains of any length: where the next target's PC
+    would fail cover_check, a free PC is put in between whose own signal is a
+    fresh value homed in `far` (away from the slots under test; it changes no
+    window there).  sig_0 = pc_0 is homed in `far` too."""
+    rng = np.random.default_rng(seed)
+    valid = lambda lo: KERNEL_LO <= lo < KERNEL_HI  # noqa: E731
+    used = set(int(t) for t in targets)
+
+    def free_pc(prev, nxt):
+        for _ in range(100000):
+            p = int(rng.integers(KERNEL_LO, KERNEL_HI))
+            s = p ^ (exec_hash(prev) if prev is not None else 0)
+            if far[0] <= s % 8192 < far[1] and s not in used and (nxt is None or valid(nxt ^ exec_hash(p))):
+                used.add(s)
+                return p
+        raise RuntimeError("no free pc")
+
+    pcs = [free_pc(None, None)]
+    prev = pcs[0]
+    for t in targets:
+        lo = int(t) ^ exec_hash(prev)
+        if not valid(lo):
+            pcs.append(free_pc(prev, int(t)))
+            prev = pcs[-1]
+            lo = int(t) ^ exec_hash(prev)
+        pcs.append(lo)
+        prev = lo
+    return np.array([0xFFFFFFFF00000000 | x for x in pcs], dtype=np.uint64)
+
+
+def zero_stress_programs(nprog, seed):
+    """Programs for the sig == 0 rule of K2 (csrc/edge.hip header): a fill
+    call that sets slots 8184..8 to random values homed there (or leaves them
+    empty), then calls dense in sig == 0 and in signals homed at 8184..8, with
+    few distinct values, so forced overwrites, zero writes (slot 0 emptied)
+    and re-inserts meet inside one 256-signal chunk."""
+    rng = np.random.default_rng(seed)
+    M = 8192
+    homes = list(range(M - 8, M)) + list(range(0, 9))
+    progs = []
+    for p in range(nprog):
+        dens = [0.0, 0.5, 0.9, 1.0][p % 4]
+        fill = [int(rng.integers(1, 6)) * M + h for h in homes if rng.random() < dens]
+        calls = [(False, craft_free(fill, seed * 1000 + p * 10))] if fill else []
+        vals = np.array([0] + [k * M + h for h in homes for k in range(1, 4)], np.uint64)
+        pr = np.full(vals.size, 1.0)
+        pr[0] = [2.0, 6.0, 20.0][p % 3]
+        pr /= pr.sum()
+        for c in range(3):
+            tg = vals[rng.choice(vals.size, int(rng.integers(40, 200)), p=pr)]
+            calls.append((False, craft_free(tg.tolist(), seed * 1000 + p * 10 + c + 1)))
+        progs.append(calls)
+    return progs
+
+
 def pack(programs):
     """programs = [[(failed, pcs), ...], ...] -> flat arrays"""
     pcs, cs, cl, cf, pc = [], [], [], [], [0]
@@ -100,7 +156,8 @@ def synth_programs(cfg, nprog, cpp, ragged, seed, prog_base=0):
     return progs
 
 
-def main():
+def main(only=None):
+    """Writes every fixture, or only those named on the command line."""
     out = {}
     # 1. the survey's KAT: call 0 gives 4 signals (one dup dropped), the same trace
     #    as call 1 gives none (the dedup table is shared across a program's calls)
@@ -118,10 +175,26 @@ def main():
     zero_dup = craft_call([0, 5, 0])
     zero_emit = craft_call([8192, 8193, 8194, 8195, 0, 8192, 0, 8196])
     out["executor_zero"] = [[(False, zero_dup)], [(False, zero_emit), (False, zero_emit)]]
+    # 4b. sig == 0 inside one round-chunk (the round-4 verdict's case: after
+    #    8192, 8193, 16384, 8195 fill slots 0..3, 0 is emitted and empties slot
+    #    0, so the next 16384 is a new insert at slot 0), the same with the later
+    #    lane homed at 8190 / 8191, an earlier lane blocked across a zero write,
+    #    an overwrite of a match that lies after the emptied slot 0, and
+    #    randomized zero-heavy programs
+    out["executor_zero2"] = [
+        [(False, craft_call([8192, 8193, 16384, 8195, 0, 16384]))],
+        [(False, craft_free([16382, 16383, 24574, 8193, 8194, 8195, 0, 24574], 1))],
+        [(False, craft_free([16383, 24575, 8193, 8194, 8195, 0, 24575], 2))],
+        [(False, craft_free([8192, 8193, 8194, 32771, 16383], 3)), (False, craft_free([32766, 16382, 0], 4))],
+        [(False, craft_free([40960, 40961, 40963, 8196, 24568, 32761, 16380, 40958], 5)),
+         (False, craft_free([32768, 16377, 24580, 16376, 0, 24574, 24570, 24573, 32768, 32770], 6))],
+    ] + zero_stress_programs(16, 7)
     # 5. a call at the per-call limit region boundary (kCoverSize - 1 PCs)
     big = synth_programs(synth.synth_default(region_log2=14), 1, 1, (262143, 262143), 14, prog_base=300)
     out["executor_big"] = big
     for name, programs in out.items():
+        if only and name not in only:
+            continue
         fx = pack(programs)
         fx.update(expected(fx, programs))
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **fx)
@@ -130,4 +203,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

@@ -34,10 +34,14 @@ class NumpyStepOps:
 
     device = "cpu"
 
-    def __init__(self, rank, stair=True, fail_owner=False):
+    def __init__(self, rank, stair=True, fail_owner=False, spill=False, raise_send=False, raise_own=False):
         self.rank, self.stair, self.fail_owner = rank, stair, fail_owner
+        self.spill = spill            # every capped (non-exact) run spills a cell: VOID headers, src_void 1
+        self.raise_send = raise_send  # send raises (as ERANGE on the serial range would), host side
+        self.raise_own = raise_own    # own raises (as a failed reserve would), host side
+        self.exact_sends = 0
         self.pairs = set()
-        self.st = {}
+        self.st = {"src_void": 0, "global_void": 0, "owners_void": 0, "max_out": 0}
 
     @staticmethod
     def alloc(n, dtype):
@@ -48,6 +52,18 @@ class NumpyStepOps:
         return int(batch["sigs"].size)
 
     def send(self, batch, serial_base, levels, nshards, cap, send, exact=False):
+        if self.raise_send:
+            raise OverflowError("step_send: batch serial order exceeds 2^24 calls")
+        self.exact_sends += bool(exact)
+        if self.spill and not exact:
+            # a void run (k_stair_heads): every bucket VOID with count 0
+            sv = send.numpy().view(np.uint64)
+            for g in range(nshards):
+                sv[g * (cap + 1)] = HDR_VOID
+            self.pairs = set()
+            self.st = {"src_void": 1, "global_void": 0, "owners_void": 0, "records": int(batch["sigs"].size),
+                       "sent": 0, "max_out": 0, "inserted": 0, "changed": 0, "own_distinct": 0, "new_pairs": 0}
+            return
         sigs, cs, cl, prio = batch["sigs"], batch["call_start"], batch["call_len"], batch["call_prio"]
         lvl = {(v & 0xFF): i for i, v in enumerate(levels)}
         groups = [[] for _ in range(nshards)]
@@ -82,6 +98,8 @@ class NumpyStepOps:
                    "own_distinct": 0, "new_pairs": 0}
 
     def own(self, shard, new_signal, recv, nshards, cap, levels, flags, exact=False):
+        if self.raise_own:
+            raise MemoryError("step_own: out of device memory")
         rv = recv.numpy().view(np.uint64)
         fl = flags.numpy()
         fl[:] = 0
@@ -400,3 +418,75 @@ def test_sharded_minimize_split_failure_raises_on_every_rank():
         res = [json.load(open(os.path.join(d, f"f{r}.json")))["err"] for r in range(world)]
     assert res[1] == "ValueError: split failed on part 1"
     assert res[0] and res[2] and "another rank" in res[0] and "another rank" in res[2]
+
+
+def mode_worker(rank, world, port, outdir, seed, cap, mode):
+    """One step with a per-rank failure mode: {"spill": [ranks], "raise_send":
+    [ranks], "raise_own": [ranks]}."""
+    from syzkaller_amd.dist import ShardedTriage
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    ncalls = mode.get("ncalls", [40] * world)
+    batch = make_rank_batch(rank, ncalls[rank], seed)
+    shard = {e: p for e, p in m0_global(seed).items() if _owner(e, world) == rank}
+    ops = NumpyStepOps(rank, True, spill=rank in mode.get("spill", ()),
+                       raise_send=rank in mode.get("raise_send", ()), raise_own=rank in mode.get("raise_own", ()))
+    st = ShardedTriage(ops, shard, {}, cap=cap, levels=[0, 1, 2, 3])
+    out = {"err": None}
+    try:
+        bits, cnew, stats = st.step(batch, torch.from_numpy(batch["call_prio"]), sum(ncalls[:rank]))
+        out.update(bits=bits.tolist(), redos=st.redos, exact_sends=ops.exact_sends)
+    except Exception as e:  # noqa: BLE001
+        out["err"] = f"{type(e).__name__}: {e}"
+    json.dump(out, open(os.path.join(outdir, f"x{rank}.json"), "w"))
+    dist.destroy_process_group()
+
+
+def _run_mode(world, seed, cap, mode):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(mode_worker, args=(world, free_port(), d, seed, cap, mode), nprocs=world,
+                           start_method="spawn")
+        return [json.load(open(os.path.join(d, f"x{r}.json"))) for r in range(world)]
+
+
+@pytest.mark.timeout(120)
+def test_sharded_step_spill_and_cap_overflow_same_step():
+    """Rank 1's capped run spills (a void source: it must take its exact path)
+    while rank 0's one call fits the cap of 64 records: attempt 1 is void (the
+    spill), attempt 2 is void again (rank 1 exact, but over the cap), attempt
+    3 succeeds.  Rank 1 stays exact across attempts 2 and 3 -- it must not return
+    to the capped cells after the overflow -- and the bits equal
+    sequential checkNewSignal."""
+    from oracle import oracle as O
+
+    world, seed = 2, 11
+    ncalls = [1, 40]
+    res = _run_mode(world, seed, 64, {"spill": [1], "ncalls": ncalls})
+    assert all(r["err"] is None for r in res), res
+    assert res[1]["exact_sends"] == 2 and res[0]["exact_sends"] == 0, res
+    assert all(r["redos"] == 2 for r in res), res
+    parts = [make_rank_batch(r, ncalls[r], seed) for r in range(world)]
+    sigs = np.concatenate([p["sigs"] for p in parts])
+    cs = np.concatenate([parts[0]["call_start"], parts[1]["call_start"] + parts[0]["sigs"].size])
+    cl = np.concatenate([p["call_len"] for p in parts])
+    prio = np.concatenate([p["call_prio"] for p in parts])
+    m0 = m0_global(seed)
+    _, _, obits, _ = O.triage_batch(np.array(list(m0), np.uint32), np.array(list(m0.values()), np.int8),
+                                    sigs, cs, cl, prio)
+    exp = np.array([(obits[i >> 5] >> (i & 31)) & 1 for i in range(sigs.size)], np.uint8)
+    np.testing.assert_array_equal(np.concatenate([np.array(r["bits"], np.uint8) for r in res]), exp)
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("mode,own_err", [({"raise_send": [2]}, "OverflowError"), ({"raise_own": [1]}, "MemoryError")])
+def test_sharded_step_failure_raises_on_every_rank(mode, own_err):
+    """A host-side failure of send or own on one rank travels in-band (VOID
+    headers / a void status byte), so every rank raises at the redo's
+    agreement instead of its peers blocking in the all-to-all:
+    the failing rank its own error, the others a RuntimeError."""
+    world = 3
+    res = _run_mode(world, 12, None, mode)
+    bad = (mode.get("raise_send") or mode.get("raise_own"))[0]
+    for r, x in enumerate(res):
+        assert x["err"] is not None, (r, x)
+        assert x["err"].startswith(own_err if r == bad else "RuntimeError"), (r, x)

@@ -10,7 +10,19 @@ decision slot d (first match or zero of its window, or h when forced), its
 write slots now or after a re-run (h and the window's empty slots).  Writers
 mark those slots; a lane is blocked when an earlier lane marked the bin of d
 and some other lane marked d itself; a blocked lane marks its write slots and
-d.  Unblocked writers store; blocked lanes run again next round."""
+d.  Unblocked writers store; blocked lanes run again next round.
+
+sig == 0 is the one write that empties a slot: its forced overwrite stores 0
+at slot 0 (executor.h:704), which changes the predicates of every later lane
+whose window holds slot 0 (h in 8189..8191, 0).  Such a lane's decision slot
+lies in 8189..8191, 0..3, so a sig-0 lane marks all seven of those slots
+(ZERO_SLOTS) instead of its window.  And inside a window that holds slot 0
+the rest of the argument fails too: a slot there can hold sig while an earlier
+slot (slot 0) is empty, so once slot 0 fills again the lane decides at a slot
+after today's decision slot, and a later zero write changes a slot it has
+read.  A lane whose window holds slot 0 (h in 8189..8191, 0) therefore marks
+its whole window, so that every later write into it waits while it is
+pending."""
 import os
 
 import numpy as np
@@ -39,6 +51,21 @@ def seq_dedup(T, s):
             return True
     T[s % M] = s
     return True
+
+
+ZERO_SLOTS = [M - 3, M - 2, M - 1, 0, 1, 2, 3]
+
+
+def write_slots(s, ps, h):
+    """Slots a pending lane marks: those it can write, now or after a re-run
+    (h and its window's empty slots); its whole window when that holds slot 0;
+    for sig == 0, every decision slot of a window that holds slot 0 (its
+    forced overwrite makes slot 0 empty again)."""
+    if s == 0:
+        return list(ZERO_SLOTS)
+    if h >= M - 3 or h == 0:  # the window holds slot 0: all of it
+        ps = 15
+    return [(h + k) % M for k in range(4) if ps >> k & 1]
 
 
 def round_chunk(T, ch, binsh=3):
@@ -71,7 +98,7 @@ def round_chunk(T, ch, binsh=3):
         for i in pend:
             w, d, ps, h = ev[i]
             if w:
-                mark(i, [(h + k) % M for k in range(4) if ps >> k & 1])
+                mark(i, write_slots(ch[i], ps, h))
         while True:
             new = []
             for i in pend:
@@ -84,7 +111,7 @@ def round_chunk(T, ch, binsh=3):
                 break
             for i in new:
                 w, d, ps, h = ev[i]
-                mark(i, [(h + k) % M for k in range(4) if ps >> k & 1] + [d])
+                mark(i, write_slots(ch[i], ps, h) + [d])
         nxt = []
         for i in pend:
             if blocked[i]:
@@ -97,12 +124,18 @@ def round_chunk(T, ch, binsh=3):
     return emit, rounds
 
 
-@pytest.mark.parametrize("name,progs", [("executor_wide", (0, 5)), ("executor_synth", (1, 3)),
-                                        ("executor_big", (0,))])
-def test_rounds_equal_sequential_dedup(name, progs):
+def _golden_names():
+    return sorted(f[:-4] for f in os.listdir(HERE) if f.startswith("executor_") and f.endswith(".npz"))
+
+
+@pytest.mark.parametrize("name", _golden_names())
+def test_rounds_equal_sequential_dedup(name):
+    """Every program of every reference-executor fixture, chunk by chunk.
+    A program aborted by cover_check is replayed over all its calls: the
+    rounds are checked against sequential dedup, not against the abort."""
     d = np.load(os.path.join(HERE, name + ".npz"))
     pcs, cs, cl, pc = d["pcs"], d["call_start"], d["call_len"], d["prog_call"]
-    for p in progs:
+    for p in range(pc.size - 1):
         Tp, Ts = [0] * M, [0] * M
         for c in range(int(pc[p]), int(pc[p + 1])):
             trace = pcs[int(cs[c]): int(cs[c]) + int(cl[c])].tolist()
@@ -138,3 +171,48 @@ def test_rounds_equal_sequential_dedup_synthetic(global_walk, region_log2):
             got, _ = round_chunk(Tp, ch)
             assert got == [seq_dedup(Ts, s) for s in ch], (c, c0)
             assert Tp == Ts
+
+
+def _zero_stress_chunk(rng, n):
+    """A chunk dense in sig == 0 and in signals whose window holds slot 0 (or
+    neighbours it), over a few values each, so that forced overwrites, zero
+    writes and re-inserts meet inside one round."""
+    homes = [M - 4, M - 3, M - 2, M - 1, 0, 1, 2, 3, 4]
+    vals = [0] + [k * M + h for h in homes for k in range(1, 4)]
+    p = np.full(len(vals), 1.0)
+    p[0] = 6.0
+    p /= p.sum()
+    return [int(vals[j]) for j in rng.choice(len(vals), n, p=p)]
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_rounds_zero_writer_stress(seed):
+    """Randomized: chunks seeded with zero signals over a table whose slots
+    8188..4 start full, empty or mixed; every chunk's flags and the table
+    after it equal sequential dedup (executor.h:693-706)."""
+    rng = np.random.default_rng(seed)
+    for trial in range(40):
+        T = [0] * M
+        fill = trial % 3  # 0: full near slot 0, 1: empty, 2: mixed
+        for sl in list(range(M - 6, M)) + list(range(0, 7)):
+            if fill == 0 or (fill == 2 and rng.random() < 0.6):
+                T[sl] = int(rng.integers(1, 5)) * M + sl
+        Tp, Ts = list(T), list(T)
+        for _ in range(3):
+            ch = _zero_stress_chunk(rng, int(rng.integers(8, 257)))
+            got, _ = round_chunk(Tp, ch)
+            want = [seq_dedup(Ts, s) for s in ch]
+            assert got == want, (seed, trial)
+            assert Tp == Ts, (seed, trial)
+
+
+def test_rounds_zero_writer_verdict_case():
+    """The round-4 verdict's trace: after 8192, 8193, 16384, 8195 fill slots
+    0..3, sig 0 is emitted and empties slot 0, so the following 16384 (then at
+    slot 2) is a NEW insert at slot 0 -- 7 signals, as the reference executor
+    emits (golden executor_zero2)."""
+    sigs = [0x81000005, 8192, 8193, 16384, 8195, 0, 16384]
+    Tp, Ts = [0] * M, [0] * M
+    got, _ = round_chunk(Tp, sigs)
+    assert got == [seq_dedup(Ts, s) for s in sigs] == [True] * 7
+    assert Tp == Ts
