@@ -82,6 +82,7 @@ def parse():
                          "per-syscall 256-block regions (region, rounds 1-3's headline)")
     ap.add_argument("--batches", type=int, default=4, help="distinct batches the steps cycle through")
     ap.add_argument("--no-pipe", action="store_true", help="skip the K1+K2 -> K3 pipeline line")
+    ap.add_argument("--no-poll", action="store_true", help="skip the manager Poll line")
     return ap.parse_args()
 
 
@@ -136,6 +137,29 @@ def pmc_traffic(kernel_prefixes, cfg, keys=TRIAGE_KEYS, expect_ms=None, tol=0.15
         return best[1], best[2], None
     return None, None, ("no PMC summary of this workload and code: " + "; ".join(rejected)) if rejected else \
         "no PMC summary of this workload"
+
+
+def achievable_bw(dev, nbytes=1 << 30, reps=5):
+    """the achievable HBM bandwidth beside the spec peak -- a plain
+    device copy (csrc/runtime.hip k_copy16, 16 B per lane, nontemporal) of
+    `nbytes` between two HBM buffers, read + write bytes / device time (HIP
+    events), median of `reps` after one warm-up."""
+    src = torch.ones(nbytes // 8, dtype=torch.int64, device=dev.dev)
+    dst = torch.empty_like(src)
+    ms = [dev.copy_bw(dst, src, nbytes) for _ in range(reps + 1)][1:]
+    ok = bool(torch.equal(dst, src))
+    t = float(np.median(ms))
+    del src, dst
+    return {"value": 2 * nbytes / (t * 1e-3) / 1e9, "unit": "GB/s", "ms": t, "bytes_copied": nbytes,
+            "kernel": "k_copy16 (16 B per lane, nontemporal loads and stores)", "check": ok}
+
+
+def with_achievable(roof, ach):
+    """roofline + the achievable bandwidth and the fraction of it."""
+    if roof and ach and roof.get("unit") == "GB/s":
+        roof["achievable"] = ach["value"]
+        roof["frac_achievable"] = roof["achieved"] / ach["value"]
+    return roof
 
 
 def cpu_model():
@@ -239,6 +263,61 @@ def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
                          "avg_launch_ms": t}}
 
 
+POLL_BYTES_PER_ENTRY = 5.0  # Poll: a polled (elem u32, prio i8) entry (SURVEY 8(d)'s Minimize-style figure)
+
+
+def poll_line(dev, F=16, K=256, per=16384, fresh=0.05, m0=10_000_000, reps=3, seed=1027):
+    """syz-manager's Poll (manager.go:1027-1052) over a
+    batch of K polls from F fuzzers, each carrying a Serial of `per` entries,
+    against a 10M-element maxSignal (random u32, prio 0..3): a steady-state
+    manager, where a fuzzer's newSignal since its last poll is mostly signal
+    the manager already has -- a (1 - fresh) share of the entries are
+    elements of maxSignal at a prio no higher than maxSignal's, the rest
+    random u32 at prio 0..3 (new).  Every fuzzer starts with an empty
+    newMaxSignal.  One signal.manager_poll call (syzsig_manager_poll_batch: the
+    Serials are host arrays, i.e. RPC payloads, so the time includes their
+    upload and the replies' Serialize); wall time, median of `reps`, state
+    restored between reps."""
+    from syzkaller_amd import signal as S
+
+    rng = np.random.default_rng(seed)
+    e0 = rng.integers(0, 1 << 32, m0, dtype=np.uint64).astype(np.uint32)
+    p0 = rng.integers(0, 4, m0).astype(np.int8)
+    polls = []
+    for _ in range(K):
+        known = rng.random(per) >= fresh
+        pick = rng.integers(0, m0, per)
+        e = np.where(known, e0[pick], rng.integers(0, 1 << 32, per, dtype=np.uint64).astype(np.uint32))
+        p = np.where(known, np.minimum(p0[pick], rng.integers(0, 4, per)), rng.integers(0, 4, per)).astype(np.int8)
+        polls.append((int(rng.integers(0, F)), S.Serial(e.astype(np.uint32), p)))
+    pristine = S.Serial(e0, p0).Deserialize(dev.eng)
+    walls = []
+    for r in range(reps + 1):
+        ms = pristine.clone()
+        nm = [S.Signal(None, dev.eng) for _ in range(F)]
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        replies = S.manager_poll(ms, nm, polls, dev.eng)
+        torch.cuda.synchronize()
+        if r:
+            walls.append(time.perf_counter() - t)
+        nrep = sum(int(np.asarray(x.Elems).size) for x in replies)
+        del ms, nm, replies
+    wall = float(np.median(walls))
+    n = K * per
+    achieved = POLL_BYTES_PER_ENTRY * n / wall / 1e9
+    return {"metric": "manager Poll: polled entries/sec (Diff into maxSignal, Merge, fan-out)",
+            "value": n / wall, "unit": "entries/s", "higher_is_better": True, "ms": wall * 1e3, "dtype": "u32",
+            "config": {"workload": f"{K} polls from {F} fuzzers x {per} entries ({fresh:.0%} new, the rest already in "
+                                   f"maxSignal) vs a {m0}-element maxSignal, one batch (host Serials: upload and "
+                                   "replies' Serialize included)",
+                       "entries": n, "reply_entries": nrep},
+            "roofline": {"bound": "hbm", "kernel": "syzsig_manager_poll_batch (all kernels + uploads, wall time)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "bytes_per_unit": POLL_BYTES_PER_ENTRY, "units_per_launch": n,
+                         "avg_launch_ms": wall * 1e3}}
+
+
 def synth_batch(dev, cfg, prog_base, P, C, L):
     """Synthetic KCOV traces of P programs x C calls x L PCs -> K1+K2 on device.
     Returns (sigs, call_start, sig_cnt, prio, records, pcs)."""
@@ -255,20 +334,24 @@ def chain_ms(st):
     return st["part_ms"] + st["probe_ms"] + st["decide_ms"]
 
 
-def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m0=10_000_000):
+def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m0=10_000_000, walk="global"):
     """BASELINE config 5 (sustained streaming triage, skewed PC distribution)
     at one rank's share of an 8-GPU node: batches of `programs` x `calls` x
-    `pcs` (skew=1: Zipf-like hot syscalls, so hot edges repeat across the
-    batch), each triaged against the maxSignal/newSignal state the previous
+    `pcs`, each triaged against the maxSignal/newSignal state the previous
     batch left (syz-fuzzer/proc.go:230-247 -> fuzzer.go:494-511 per
-    execution, batched).  The sequence of `nbatches` batches starts from a
-    10M-element M0 and is replayed `reps` times (state restored between
-    replays, outside the timed region); value = records / wall time of the
-    sequence, chain = device time of the K3 kernels."""
+    execution, batched).  walk="global" is SURVEY 8(d)'s C5 input: every
+    call a walk over all 2^20 blocks started from the entry of a
+    Zipf(1.1)-chosen syscall (skew=2, csrc/common.h synth_zipf4096), so the
+    walks' first edges are hot across the batch, against a 10M-element M0
+    holding the edge universe; walk="region" is rounds 1-4's line (power-skewed
+    syscalls, u^4, walking their 256-block regions).  The sequence of
+    `nbatches` batches starts from M0 and is replayed `reps` times (state
+    restored between replays, outside the timed region); value = records /
+    wall time of the sequence, chain = device time of the K3 kernels."""
     from syzkaller_amd import signal as S
     from syzkaller_amd import synth
 
-    cfg = synth.synth_default(skew=1)
+    cfg = walk_cfg(walk, skew=2 if walk == "global" else 1)
     keep, bs = [], []
     total = 0
     for i in range(nbatches):
@@ -277,7 +360,7 @@ def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m
         keep.append((sigs, cs, cnt, prio, cnew))
         bs.append(b)
         total += nrec
-    m0e, m0p = dev.synth_m0(cfg, 2048, m0)
+    m0e, m0p = dev.synth_m0(cfg, KNOWN_SYS[walk], m0)
     pristine = dev.deserialize(m0e, m0p)
     del m0e, m0p
     walls, chains, sts = [], [], []
@@ -295,7 +378,9 @@ def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m
     wall, chain = float(np.median(walls)), float(np.median(chains))
     achieved = PROBE_BYTES_PER_REC * total / (chain * 1e-3) / 1e9
     wl = (f"BASELINE config 5 at one rank's share of 8 GPUs: {nbatches} consecutive batches of {programs} programs "
-          f"x {calls} calls x {pcs} PCs, skew=1, each against the state the previous one left (M0 {m0})")
+          f"x {calls} calls x {pcs} PCs, " +
+          ("SURVEY 8(d)'s global walks from Zipf(1.1) entries" if walk == "global" else "skew=1") +
+          f", each against the state the previous one left (M0 {m0})")
     traffic, src, note = pmc_traffic(["syz::" + k for k in K3_KERNELS.split("+")], {"workload": wl}, ("workload",),
                                      expect_ms=chain / nbatches)
     return {"metric": "signal elems triaged/sec (Diff+Merge), streaming skewed batches",
@@ -669,6 +754,7 @@ def main():
     progress(rank, f"device {local}, world {world}")
     dev = Device(local)
     dev.L.syzsig_ctx_set_timing(dev.eng.h, 1)
+    ach = achievable_bw(dev)
     cfg = walk_cfg(a.walk, skew=a.skew)
     known = KNOWN_SYS[a.walk]
     P, C, L = a.programs, a.calls, a.pcs
@@ -876,6 +962,8 @@ def main():
         out["lines"]["minimize"] = minimize_line(dev, a.min_contexts)
     if rank == 0 and world == 1 and not a.no_c5:
         out["lines"]["c5"] = c5_line(dev, pairs)
+        # rounds 1-4's C5 input (power-skewed region walks), kept comparable
+        out["lines"]["c5_region_power"] = c5_line(dev, pairs, walk="region")
     if rank == 0 and world == 1 and not a.no_pipe:
         out["lines"]["pipeline"] = pipeline_line(dev, pairs, P, C, L, a.walk)
     if rank == 0 and world == 1 and not a.no_gw:
@@ -883,6 +971,8 @@ def main():
         out["lines"][f"c2_{other}_walk"] = c2_walk_line(dev, pairs, P, C, L, other)
     if rank == 0 and world == 1 and not a.no_c1:
         out["lines"]["c1"] = c1_line(dev)
+    if rank == 0 and world == 1 and not a.no_poll:
+        out["lines"]["poll"] = poll_line(dev)
     if rank == 0 and world == 1 and not a.no_c4:
         out["lines"]["c4_rank"] = c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, a.walk)
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -890,6 +980,10 @@ def main():
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
+        out["achievable_bw"] = ach
+        with_achievable(out["roofline"], ach)
+        for ln in out["lines"].values():
+            with_achievable(ln.get("roofline"), ach)
         print(json.dumps(out), flush=True)
     if distributed:
         dist.destroy_process_group()

@@ -62,6 +62,11 @@ int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable);
 /* With timing on: device time (ms, HIP events on the context stream) of the
  * kernels of the last syzsig_edge_derive_dev / syzsig_minimize_dev call. */
 double syzsig_ctx_last_ms(syzsig_ctx* ctx);
+/* Measurement: a plain device copy of `bytes` (16-B aligned buffers and size)
+ * on the context stream, 16 B per lane per step; *ms = its device time (HIP
+ * events).  The achievable-bandwidth companion of the bench's rooflines
+ * (SURVEY.md 8(d)); not part of pkg/signal.  Synchronises. */
+int syzsig_copy_bw_dev(syzsig_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes, double* ms);
 /* Large-batch triage path selection (tests and tuning; results never depend on it):
  * mode 0 = per-call probe path only, 1 = aggregation path for runs of >= 2^20
  * records (default), 2 = aggregation path always; parts = fixed partition
@@ -169,7 +174,10 @@ int syzsig_minimize_dev(syzsig_ctx* ctx, const uint64_t* d_ctx_off, const uint32
  * Limits of one call (SYZSIG_ERANGE, nothing touched): npolls + nfuzzers <
  * 2^24 - 1, npolls * nfuzzers <= 2^28, total entries * nfuzzers <= 2^31.  A
  * caller splits a larger batch into consecutive calls (the loop is sequential,
- * so that is the same result: signal.py manager_poll does). */
+ * so that is the same result: signal.py manager_poll does).  A call of more
+ * than 2^23 entries, or whose entries crowd one element partition past 2048
+ * (a hot element in thousands of polls), runs the reference loop poll by poll
+ * over the set ops instead of the batch kernels (same result, slower). */
 int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_max, uint32_t nfuzzers,
                               const uint32_t* poll_fuzzer, const uint64_t* poll_off, const uint32_t* elems,
                               const int8_t* prios, uint32_t npolls, syzsig_set** replies);

@@ -129,7 +129,7 @@ struct SynthCfg {
 	uint32_t nblocks_log2;  // basic blocks B = 2^nblocks_log2 (20)
 	uint32_t region_log2;   // per-syscall region W = 2^region_log2 blocks (8)
 	uint32_t nsys;          // distinct syscalls (4096)
-	uint32_t skew;          // 0 uniform syscall choice, 1 power-skewed (hot edges)
+	uint32_t skew;          // 0 uniform syscall choice, 1 power-skewed (u^4), 2 Zipf(1.1) (synth_zipf4096)
 	uint32_t restart_log2;  // walk returns to the syscall entry w.p. 2^-restart_log2 (5)
 	uint32_t errno_permille;// call fails (errno != 0) w.p. /1000 (300)
 	uint32_t any_permille;  // call contains an ANY pointer w.p. /1000 (100)
@@ -145,6 +145,22 @@ SYZ_HD uint32_t synth_entry(const SynthCfg& c, uint32_t s)
 	return fmix32(s * 0x9E3779B1u + 0x01234567u) & ((1u << c.nblocks_log2) - 1);
 }
 
+// Zipf(s = 1.1) rank in 1..4096 from 32 random bits (C5's walks
+// start from a Zipf(1.1) entry), in integer arithmetic only, so host and
+// device draw the same ranks.  Inverse CDF of the power law x^-1.1 on
+// [0.5, 4096.5), rounded to the nearest rank: P(k) is proportional to
+// (k - 0.5)^-0.1 - (k + 0.5)^-0.1, i.e. 0.1 k^-1.1 to within 1 % for k >= 3
+// (rank 1: about 10 % above).  x = t^-10 with t = a - u (a - b), a = 0.5^-0.1,
+// b = 4096.5^-0.1, t in Q31 fixed point (t < 2, so every square fits 64 bits).
+SYZ_HD uint32_t synth_zipf4096(uint32_t r)
+{
+	constexpr uint64_t kA = 2301615985ull, kAB = 1366880845ull;  // a and a - b in Q31
+	const uint64_t t = kA - ((kAB * r) >> 32);
+	const uint64_t t2 = (t * t) >> 31, t4 = (t2 * t2) >> 31, t8 = (t4 * t4) >> 31, t10 = (t8 * t2) >> 31;
+	const uint64_t x = ((1ull << 62) / t10 + (1ull << 30)) >> 31;  // round(t^-10)
+	return x < 1 ? 1u : x > 4096 ? 4096u : (uint32_t)x;
+}
+
 struct SynthCall {
 	uint32_t sysno;
 	uint8_t failed;  // errno != 0
@@ -156,7 +172,9 @@ SYZ_HD SynthCall synth_call(const SynthCfg& c, uint64_t prog, uint32_t call)
 	uint64_t s = seed_mix(c.seed, prog, 0x100000000ull + call);
 	uint64_t r = splitmix64(&s);
 	SynthCall sc;
-	if (c.skew) {
+	if (c.skew == 2) {
+		sc.sysno = (synth_zipf4096((uint32_t)(r >> 32)) - 1) % c.nsys;
+	} else if (c.skew) {
 		uint64_t x = (r >> 40) & 0xFFFFFF;  // u in [0,1) as 24-bit fixed point
 		uint64_t t = (x * x) >> 24;
 		t = (t * t) >> 24;                  // u^4
@@ -192,6 +210,8 @@ SYZ_HD void synth_trace(const SynthCfg& c, uint64_t prog, uint32_t call, uint64_
 	uint64_t s = seed_mix(c.seed, prog, call);
 	if (c.global_walk) {  // b <- (4b + 1 + r%4) mod B from a uniform block, no restarts
 		uint32_t b = (uint32_t)(splitmix64(&s) >> 20) & bmask;
+		if (c.skew == 2)  // (C5) from the entry of a Zipf(1.1)-chosen syscall
+			b = entry;
 		for (uint32_t i = 0; i < n; i++) {
 			uint64_t r = splitmix64(&s);
 			uint64_t pc = synth_pc(b);

@@ -227,6 +227,15 @@ int triage_records_impl(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const 
 // *done = false: the LDS path voided itself (nothing committed), take the per-record path
 int rp_triage_records(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t nrec,
                       const LevelMap& lm, uint8_t* new_flags, syzsig_batch_stats* st, bool* done);
+// Entries x[r] = e << 32 | r (r < 2^32) grouped by element through the LDS
+// partitions of recs.hip, for Poll (poll.hip): on return (enqueued only)
+// keys[base[p] .. base[p + 1]) = h_residual << 32 | r of partition p's entries
+// (partition = the top pbits of fmix32(e)), base on device (P + 1 entries);
+// ctr zeroed, then ctr[kCntSpill] != 0 when a partition exceeds kRpGroupCap
+// entries (nothing after it is valid).
+constexpr uint32_t kRpGroupCap = 2048;
+int rp_group(syzsig_ctx* ctx, const uint64_t* x, uint64_t n, uint64_t** keys, uint32_t** base, uint32_t* pbits,
+             unsigned long long* ctr);
 // a set an owner step holds until syzsig_step_finish takes no other call
 inline int set_check_idle(const syzsig_set* s)
 {

@@ -16,15 +16,16 @@
 // batch goes into the reply of g's first poll.  Merge is max-prio, so every
 // target (a reply, or a fuzzer's final newMaxSignal) is the max-merge of the
 // (e, p) routed to it:
-//   k_poll_keys / radix sort   records by (e, poll), input order kept
-//   k_poll_walk                one thread per element: the events (read-only)
+//   k_poll_x / rp_group        the entries grouped by element through the LDS
+//                              partitions of recs.hip (no device-wide sort)
+//   k_poll_part_walk           one workgroup per partition: its entries sorted
+//                              by (element, entry index) in LDS (bitonic), then
+//                              one thread per element: the events (read-only)
 //   k_poll_commit              maxSignal.Merge of the events, once every target exists
 //   k_poll_fanout              (target, e, p) of every event for every other
 //                              fuzzer into one max-table keyed by (target, e)
 //   k_poll_pre                 pre-batch newMaxSignal of polling fuzzers
 //   k_poll_count / k_poll_scatter   the table into the target sets
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <vector>
 
@@ -36,6 +37,7 @@ constexpr uint64_t kPollEmpty = ~0ull;
 constexpr uint32_t kPollMaxTargets = (1u << 24) - 2;  // targets < 2^24 - 1 keep a word != kPollEmpty
 constexpr uint64_t kPollMaxNext = 1ull << 28;     // polls x fuzzers per batch (the dense next-target table)
 constexpr uint64_t kPollMaxFanout = 1ull << 31;   // polled entries x fuzzers per batch (bounds the fan-out table)
+constexpr uint64_t kPollMaxEntries = 1ull << 23;  // polled entries per batch (the element partitions' capacity)
 
 // target-table word: target << 40 | elem << 8 | prio ^ 0x80 (key = the top 56 bits)
 __device__ __forceinline__ uint64_t poll_word(uint32_t t, uint32_t e, uint32_t pb)
@@ -74,41 +76,93 @@ __device__ __forceinline__ void poll_put(uint64_t* T, uint64_t C, uint64_t w)
 	}
 }
 
-__global__ void k_poll_keys(const uint32_t* __restrict__ elems, const uint32_t* __restrict__ rec_poll, uint64_t n,
-                            uint64_t* keys, uint32_t* vals)
+// the entries for rp_group: e << 32 | entry index
+__global__ void k_poll_x(const uint32_t* __restrict__ elems, uint64_t n, uint64_t* x)
 {
-	for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-		keys[r] = ((uint64_t)elems[r] << 32) | rec_poll[r];
-		vals[r] = (uint32_t)r;
-	}
+	for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x)
+		x[r] = ((uint64_t)elems[r] << 32) | r;
 }
 
-// One thread per element run of the sorted records: M0[e], then the polls in
-// order, each poll's last entry of e (Deserialize: a later duplicate wins).
-// Read-only on maxSignal: the events are committed by k_poll_commit once every
-// target set exists, so a failed allocation leaves the manager untouched.
-__global__ void k_poll_walk(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint64_t n,
-                            const int8_t* __restrict__ prios, const uint64_t* ms, uint64_t ms_bmask, uint64_t* ev,
-                            unsigned long long* nev)
+// One workgroup per element partition (<= kRpGroupCap entries, keys
+// h_residual << 32 | entry index from rp_group).  The keys are sorted in LDS
+// (bitonic, padded to a power of two), so each element's entries are one run
+// in entry order -- poll order, and inside a poll the Serial's order -- and
+// one thread per run walks it: M0[e], then each poll's last entry of e
+// (Deserialize: a later duplicate wins), an event wherever the prio exceeds
+// the running maximum.  Read-only on maxSignal: the events are committed by
+// k_poll_commit once every target set exists, so a failed allocation leaves
+// the manager untouched.  The block's events are gathered in LDS and written
+// with one device atomic.
+constexpr uint32_t kPollWalkThreads = 256;
+__global__ __launch_bounds__(kPollWalkThreads) void k_poll_part_walk(const uint64_t* __restrict__ keys,
+                                                                     const uint32_t* __restrict__ base, uint32_t pbits,
+                                                                     const uint32_t* __restrict__ rec_poll,
+                                                                     const int8_t* __restrict__ prios, const uint64_t* ms,
+                                                                     uint64_t ms_bmask, uint64_t* ev,
+                                                                     unsigned long long* nev,
+                                                                     const unsigned long long* ctr)
 {
-	for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-		const uint32_t e = (uint32_t)(sk[r] >> 32);
-		if (r > 0 && (uint32_t)(sk[r - 1] >> 32) == e)
+	__shared__ uint64_t k[kRpGroupCap];
+	__shared__ uint64_t out[kRpGroupCap];
+	__shared__ uint32_t s_n;
+	__shared__ unsigned long long s_base;
+	if (ctr[kCntSpill])
+		return;  // a partition past kRpGroupCap: the batch takes the sequential path
+	const uint32_t p = blockIdx.x, tid = threadIdx.x, b0 = base[p], n = base[p + 1] - b0;
+	if (n == 0)
+		return;
+	uint32_t N = 2;
+	while (N < n)
+		N <<= 1;
+	for (uint32_t i = tid; i < N; i += kPollWalkThreads)
+		k[i] = i < n ? keys[b0 + i] : ~0ull;
+	if (tid == 0)
+		s_n = 0;
+	for (uint32_t size = 2; size <= N; size <<= 1) {
+		for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+			__syncthreads();
+			for (uint32_t t = tid; t < N / 2; t += kPollWalkThreads) {
+				const uint32_t i = 2 * t - (t & (stride - 1)), j = i + stride;
+				const uint64_t a = k[i], b = k[j];
+				if ((a > b) == ((i & size) == 0)) {
+					k[i] = b;
+					k[j] = a;
+				}
+			}
+		}
+	}
+	__syncthreads();
+	const uint32_t hp = p << (32 - pbits);
+	for (uint32_t i = tid; i < n; i += kPollWalkThreads) {
+		const uint32_t hr = (uint32_t)(k[i] >> 32);
+		if (i > 0 && (uint32_t)(k[i - 1] >> 32) == hr)
 			continue;  // not the head of e's run
+		const uint32_t e = fmix32_inv(hp | hr);
 		uint64_t v = 0;
 		int m = -1000;  // absent: below every prio (signal.go:79-81)
 		if (tbl_lookup(ms, ms_bmask, e, v) >= 0 && slot_live(v))
 			m = slot_prio(v);
-		for (uint64_t q = r; q < n && (uint32_t)(sk[q] >> 32) == e; q++) {
-			if (q + 1 < n && sk[q + 1] == sk[q])
+		uint32_t poll_next = 0;
+		for (uint32_t q = i; q < n && (uint32_t)(k[q] >> 32) == hr; q++) {
+			const uint32_t r = (uint32_t)k[q], poll = q == i ? rec_poll[r] : poll_next;
+			const bool more = q + 1 < n && (uint32_t)(k[q + 1] >> 32) == hr;
+			poll_next = more ? rec_poll[(uint32_t)k[q + 1]] : 0;
+			if (more && poll_next == poll)
 				continue;  // an earlier duplicate inside one Serial
-			const int p = prios[sv[q]];
-			if (p > m) {
-				ev[atomicAdd(nev, 1ull)] = ((uint64_t)e << 32) | ((sk[q] & 0xFFFFFFull) << 8) | prio_biased((int8_t)p);
-				m = p;
+			const int pr = prios[r];
+			if (pr > m) {
+				out[atomicAdd(&s_n, 1u)] = ((uint64_t)e << 32) | ((uint64_t)(poll & 0xFFFFFFu) << 8) | prio_biased((int8_t)pr);
+				m = pr;
 			}
 		}
 	}
+	__syncthreads();
+	const uint32_t ne = s_n;
+	if (tid == 0)
+		s_base = ne ? atomicAdd(nev, (unsigned long long)ne) : 0;
+	__syncthreads();
+	for (uint32_t i = tid; i < ne; i += kPollWalkThreads)
+		ev[s_base + i] = out[i];
 }
 
 // maxSignal.Merge(newMax_i) for every poll: the events, max-merged (an
@@ -197,6 +251,40 @@ static uint64_t pow2_ge(uint64_t x)
 
 using namespace syz;
 
+// The reference loop itself (manager.go:1027-1052), one poll after the other
+// over the set ops: the exact path for a batch whose entries crowd one element
+// partition past kRpGroupCap (a hot element polled thousands of times).
+static int poll_sequential(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_max, const uint32_t* poll_fuzzer,
+                           const uint64_t* poll_off, const uint32_t* elems, const int8_t* prios, uint32_t npolls,
+                           uint32_t nfuzzers, syzsig_set** replies)
+{
+	for (uint32_t i = 0; i < npolls; i++) {
+		const uint32_t f = poll_fuzzer[i];
+		const uint64_t a = poll_off[i], z = poll_off[i + 1];
+		syzsig_set *d = nullptr, *nm = nullptr;
+		SYZ_TRY(syzsig_deserialize(ctx, elems + a, z - a, prios + a, z - a, &d));
+		const int rc = syzsig_diff(ctx, *max_signal, d, &nm);
+		syzsig_set_free(d);
+		SYZ_TRY(rc);
+		if (!syzsig_empty(nm)) {
+			int r = syzsig_merge(ctx, max_signal, nm);
+			for (uint32_t g = 0; g < nfuzzers && r == SYZSIG_OK; g++)
+				if (g != f)
+					r = syzsig_merge(ctx, &new_max[g], nm);
+			if (r != SYZSIG_OK) {
+				syzsig_set_free(nm);
+				return r;
+			}
+		}
+		syzsig_set_free(nm);
+		if (!syzsig_empty(new_max[f])) {
+			replies[i] = new_max[f];
+			new_max[f] = nullptr;
+		}
+	}
+	return SYZSIG_OK;
+}
+
 // Sets this call made, freed again if it fails before the commit.
 struct PollFresh {
 	std::vector<syzsig_set*> sets;
@@ -227,6 +315,9 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 	const uint64_t n = poll_off[npolls] - poll_off[0];
 	if (n && (!elems || !prios))
 		return fail(SYZSIG_EINVAL, "manager_poll_batch: NULL Serial arrays");
+	if (n > kPollMaxEntries)  // (one poll past it: signal.manager_poll cuts batches at it otherwise)
+		return poll_sequential(ctx, max_signal, new_max, poll_fuzzer, poll_off, elems, prios, npolls, nfuzzers,
+		                       replies);
 	const uint32_t F = nfuzzers, K = npolls;
 	// the dense next-target table (K * F) and the fan-out table (<= n * (F - 1)
 	// events) are bounded before any state is touched
@@ -256,15 +347,12 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 		fresh.sets.push_back(ms);
 	}
 	SYZ_TRY(set_reserve(ms, n));  // (a growth keeps the contents)
-	// uploads and scratch: records, sorted records, events, the target table
-	void *de, *dp, *drp, *dk, *dv, *dk2, *dv2, *dev, *dnext, *dtmp = nullptr;
+	// uploads and scratch: entries, their grouping input, events, the target table
+	void *de, *dp, *drp, *dx, *dev, *dnext;
 	SYZ_TRY(ws_get(ctx, 40, n * 4 + 64, &de));
 	SYZ_TRY(ws_get(ctx, 41, n + 64, &dp));
 	SYZ_TRY(ws_get(ctx, 42, n * 4 + 64, &drp));
-	SYZ_TRY(ws_get(ctx, 43, n * 24 + 64, &dk));
-	dk2 = (uint64_t*)dk + n;
-	dv = (uint64_t*)dk2 + n;
-	dv2 = (uint32_t*)dv + n;
+	SYZ_TRY(ws_get(ctx, 43, n * 8 + 64, &dx));
 	SYZ_TRY(ws_get(ctx, 44, n * 8 + ((uint64_t)K * F + K) * 4 + 64, &dev));
 	dnext = (uint64_t*)dev + n;
 	uint32_t* dpf = (uint32_t*)dnext + (uint64_t)K * F;
@@ -279,20 +367,26 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 	SYZ_TRY(counters_reset(ctx));
 	unsigned long long* nev = &ctx->d_cnt[kCntAux];
 	if (n) {
-		k_poll_keys<<<grid_for(n, 256), 256, 0, s>>>((const uint32_t*)de, (const uint32_t*)drp, n, (uint64_t*)dk,
-		                                             (uint32_t*)dv);
-		size_t tmp_bytes = 0;
-		SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint64_t*)dk, (uint64_t*)dk2, (uint32_t*)dv,
-		                                           (uint32_t*)dv2, (int)n, 0, 64, s));
-		SYZ_TRY(ws_get(ctx, 45, tmp_bytes + 64, &dtmp));
-		SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, (uint64_t*)dk, (uint64_t*)dk2, (uint32_t*)dv,
-		                                           (uint32_t*)dv2, (int)n, 0, 64, s));
-		k_poll_walk<<<grid_for(n, 256), 256, 0, s>>>((const uint64_t*)dk2, (const uint32_t*)dv2, n,
-		                                             (const int8_t*)dp, ms->slots, ms->nbuckets - 1, (uint64_t*)dev,
-		                                             nev);
+		k_poll_x<<<grid_for(n, 256), 256, 0, s>>>((const uint32_t*)de, n, (uint64_t*)dx);
+		uint64_t* keys;
+		uint32_t* base;
+		uint32_t pbits;
+		SYZ_TRY(rp_group(ctx, (const uint64_t*)dx, n, &keys, &base, &pbits, ctx->d_cnt));  // (zeroes the counters)
+		k_poll_part_walk<<<1u << pbits, kPollWalkThreads, 0, s>>>(keys, base, pbits, (const uint32_t*)drp,
+		                                                          (const int8_t*)dp, ms->slots, ms->nbuckets - 1,
+		                                                          (uint64_t*)dev, nev, ctx->d_cnt);
 		SYZ_HIP(hipGetLastError());
 	}
 	SYZ_TRY(counters_fetch(ctx));
+	if (ctx->h_cnt[kCntSpill]) {
+		// an element partition past the LDS capacity: nothing was touched; the
+		// reference loop instead (a fresh maxSignal made above is dropped again)
+		fresh.sets.clear();
+		if (fresh_ms)
+			syzsig_set_free(ms);
+		return poll_sequential(ctx, max_signal, new_max, poll_fuzzer, poll_off, elems, prios, npolls, nfuzzers,
+		                       replies);
+	}
 	const uint64_t E = ctx->h_cnt[kCntAux];
 	// the target table: every event for every other fuzzer + pre-batch sets of polling fuzzers
 	uint64_t entries = E * (F ? F - 1 : 0);

@@ -576,12 +576,74 @@ int rp_run(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set* nsp, const RpSrc& src0, 
 
 namespace syz {
 
+// Poll's grouping (rp_group): key = h_residual << 32 | the entry's index
+__global__ __launch_bounds__(kRpTileThreads) void k_rp_scatter_idx(RpSrc s, uint32_t pbits,
+                                                                   const uint32_t* __restrict__ off,
+                                                                   uint64_t* keys, const unsigned long long* ctr)
+{
+	extern __shared__ uint32_t cur[];  // P cursors
+	if (rp_gated(ctr))
+		return;
+	const uint32_t P = 1u << pbits;
+	const uint32_t* row = off + (uint64_t)blockIdx.x * P;
+	for (uint32_t p = threadIdx.x; p < P; p += blockDim.x)
+		cur[p] = row[p];
+	__syncthreads();
+	uint32_t g;
+	uint64_t j0, n;
+	rp_tile(s, blockIdx.x, g, j0, n);
+	const uint64_t* r = s.recs + g * s.stride + s.hdr + j0;
+	const uint32_t rmask = (uint32_t)((1ull << (32 - pbits)) - 1);
+	for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+		const uint64_t x = r[k];
+		const uint32_t h = fmix32((uint32_t)(x >> 32)), p = h >> (32 - pbits);
+		keys[atomicAdd(&cur[p], 1u)] = ((uint64_t)(h & rmask) << 32) | (uint32_t)x;
+	}
+}
+
 __global__ void k_rp_one_seg(uint64_t* seg, uint64_t n, unsigned long long* ctr)
 {
 	if (threadIdx.x < kNumCounters)
 		ctr[threadIdx.x] = 0;
 	if (threadIdx.x == 0)
 		seg[0] = n;
+}
+
+static_assert(kRpGroupCap == kRpCap, "internal.h mirror");
+
+int rp_group(syzsig_ctx* ctx, const uint64_t* x, uint64_t n, uint64_t** keys_out, uint32_t** base_out,
+             uint32_t* pbits_out, unsigned long long* ctr)
+{
+	if (n >= (1ull << 32))
+		return fail(SYZSIG_ERANGE, "group: 2^32 entries or more");
+	void *wseg, *wk, *wc, *wb;
+	SYZ_TRY(ws_get(ctx, 48, 64, &wseg));
+	RpSrc src{x, n, 0, 1, (const uint64_t*)wseg, 0, 0};
+	const uint64_t tile = std::max<uint64_t>(kRpTileMin, (n / 1024 + 4095) & ~4095ull);
+	src.tile = (uint32_t)tile;
+	src.tiles_per_seg = (uint32_t)std::max<uint64_t>(1, (n + tile - 1) / tile);
+	const uint64_t ntiles = src.tiles_per_seg;
+	const uint32_t pbits = rp_pbits(n), P = 1u << pbits;
+	SYZ_TRY(ws_get(ctx, 49, n * 8 + 64, &wk));
+	SYZ_TRY(ws_get(ctx, 50, ntiles * P * 4 + 256, &wc));
+	SYZ_TRY(ws_get(ctx, 51, (uint64_t)(kRpGroups + 3) * P * 4 + 256, &wb));
+	uint32_t* cnt = (uint32_t*)wc;
+	uint32_t* tot = (uint32_t*)wb;
+	uint32_t* base = tot + P;       // P + 1 entries
+	uint32_t* gsum = base + P + 2;  // kRpGroups x P
+	const hipStream_t s = ctx->stream;
+	const uint32_t cg = (P + 63) / 64;
+	k_rp_one_seg<<<1, 64, 0, s>>>((uint64_t*)wseg, n, ctr);
+	k_rp_count<<<(uint32_t)ntiles, kRpTileThreads, P * 4, s>>>(src, pbits, 256, cnt, ctr);
+	k_rp_colsum<<<cg, 1024, 0, s>>>(cnt, (uint32_t)ntiles, P, gsum, tot, ctr);
+	k_rp_scan<<<1, 1024, 0, s>>>(tot, P, base, ctr, ctx->agg_dbg & SYZSIG_DEBUG_RECS_GATE);
+	k_rp_coloffs<<<cg, 1024, 0, s>>>(cnt, (uint32_t)ntiles, P, gsum, base, ctr);
+	k_rp_scatter_idx<<<(uint32_t)ntiles, kRpTileThreads, P * 4, s>>>(src, pbits, cnt, (uint64_t*)wk, ctr);
+	SYZ_HIP(hipGetLastError());
+	*keys_out = (uint64_t*)wk;
+	*base_out = base;
+	*pbits_out = pbits;
+	return SYZSIG_OK;
 }
 
 int rp_triage_records(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const uint64_t* recs, uint64_t nrec,

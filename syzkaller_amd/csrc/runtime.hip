@@ -81,6 +81,28 @@ int counters_fetch(syzsig_ctx* ctx)
 
 }  // namespace syz
 
+namespace syz {
+// A plain device copy, 16 B per lane per step (the achievable-bandwidth
+// companion of the rooflines: SURVEY 8(d) "also measure achievable BW with a
+// device copy kernel"); four steps in flight per lane.
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_copy16(const v4u* __restrict__ src, v4u* __restrict__ dst, uint64_t n)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+	uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+	for (; i + 3 * stride < n; i += 4 * stride) {
+		const v4u a = __builtin_nontemporal_load(&src[i]), b = __builtin_nontemporal_load(&src[i + stride]);
+		const v4u c = __builtin_nontemporal_load(&src[i + 2 * stride]), d = __builtin_nontemporal_load(&src[i + 3 * stride]);
+		__builtin_nontemporal_store(a, &dst[i]);
+		__builtin_nontemporal_store(b, &dst[i + stride]);
+		__builtin_nontemporal_store(c, &dst[i + 2 * stride]);
+		__builtin_nontemporal_store(d, &dst[i + 3 * stride]);
+	}
+	for (; i < n; i += stride)
+		dst[i] = src[i];
+}
+}  // namespace syz
+
 extern "C" {
 
 int syzsig_abi_version(void) { return SYZSIG_ABI_VERSION; }
@@ -218,6 +240,36 @@ double syzsig_ctx_last_ms(syzsig_ctx* ctx)
 {
 	SYZ_LOCK(ctx);
 	return ctx ? ctx->last_ms : 0;
+}
+
+int syzsig_copy_bw_dev(syzsig_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes, double* ms)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !ms || (bytes && (!d_dst || !d_src)))
+		return syz::fail(SYZSIG_EINVAL, "copy_bw: NULL argument");
+	if ((bytes & 15) || ((uintptr_t)d_dst & 15) || ((uintptr_t)d_src & 15))
+		return syz::fail(SYZSIG_EINVAL, "copy_bw: 16-B aligned buffers and size");
+	hipEvent_t ev[2];
+	SYZ_HIP(hipEventCreate(&ev[0]));
+	SYZ_HIP(hipEventCreate(&ev[1]));
+	const uint64_t n = bytes / 16;
+	// one 16-B load and store per lane per step, 8 workgroups per CU
+	const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((n + 1023) / 1024, 1), 256 * 8);
+	int rc = SYZSIG_OK;
+	if (hipEventRecord(ev[0], ctx->stream) != hipSuccess)
+		rc = syz::fail(SYZSIG_EIO, "copy_bw: event record");
+	if (rc == SYZSIG_OK && n)
+		syz::k_copy16<<<grid, 256, 0, ctx->stream>>>((const syz::v4u*)d_src, (syz::v4u*)d_dst, n);
+	if (rc == SYZSIG_OK && (hipGetLastError() != hipSuccess || hipEventRecord(ev[1], ctx->stream) != hipSuccess ||
+	                        hipEventSynchronize(ev[1]) != hipSuccess))
+		rc = syz::fail(SYZSIG_EIO, "copy_bw: kernel");
+	float t = 0;
+	if (rc == SYZSIG_OK && hipEventElapsedTime(&t, ev[0], ev[1]) != hipSuccess)
+		rc = syz::fail(SYZSIG_EIO, "copy_bw: elapsed time");
+	*ms = t;
+	(void)hipEventDestroy(ev[0]);
+	(void)hipEventDestroy(ev[1]);
+	return rc;
 }
 
 int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable)

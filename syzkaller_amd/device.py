@@ -55,6 +55,17 @@ class Device:
             if t is not None and not t.is_contiguous():
                 raise ValueError("tensors must be contiguous")
 
+    def copy_bw(self, dst, src, nbytes):
+        """Device time (ms) of a plain 16-B-per-lane copy of nbytes from src to
+        dst (syzsig_copy_bw_dev): the achievable-bandwidth companion of the
+        bench's rooflines."""
+        self._check_dev(dst, src)
+        if nbytes > min(dst.numel() * dst.element_size(), src.numel() * src.element_size()):
+            raise ValueError("copy_bw: nbytes exceeds a buffer")
+        ms = ctypes.c_double()
+        check(self.L.syzsig_copy_bw_dev(self.eng.h, _p(dst), _p(src), int(nbytes), ctypes.byref(ms)))
+        return ms.value
+
     # ---------------------------------------------------------------- sets
     def new_set(self, hint=0):
         return Signal.make(hint, self.eng)

@@ -332,6 +332,7 @@ def check_new_signal(max_signal, new_signal, calls, eng=None, want_bits=False):
 POLL_MAX_TARGETS = (1 << 24) - 2
 POLL_MAX_NEXT = 1 << 28
 POLL_MAX_FANOUT = 1 << 31
+POLL_MAX_ENTRIES = 1 << 23  # past it one call takes the sequential loop (csrc/poll.hip kPollMaxEntries)
 
 
 def manager_poll(max_signal, new_max, polls, eng=None):
@@ -349,7 +350,7 @@ def manager_poll(max_signal, new_max, polls, eng=None):
     cuts, k0, n_acc = [], 0, 0
     for k in range(K):
         if k > k0 and ((k + 1 - k0) * F > POLL_MAX_NEXT or (n_acc + lens[k]) * F > POLL_MAX_FANOUT
-                       or (k + 1 - k0) + F > POLL_MAX_TARGETS):
+                       or (k + 1 - k0) + F > POLL_MAX_TARGETS or n_acc + lens[k] > POLL_MAX_ENTRIES):
             cuts.append((k0, k))
             k0, n_acc = k, 0
         n_acc += lens[k]

@@ -83,6 +83,26 @@ def test_synth_prio_distribution():
     assert set(np.unique(prio).tolist()) <= {0, 1, 2, 3}
 
 
+def test_synth_zipf_entries_global_walk():
+    """skew=2 on the global walk (SURVEY 8(d)'s C5 input): a call's walk
+    starts at the entry block of a Zipf(1.1)-chosen syscall (csrc/common.h
+    synth_zipf4096), and then walks b <- (4b + 1 + r%4) mod 2^20."""
+    cfg = synth.synth_default(global_walk=1, skew=2)
+    n = 40000
+    pcs, cs, _ = synth.traces(cfg, 0, n, 1, np.full(n, 2, np.uint32))
+    first = ((pcs[cs.astype(np.int64)] - 0xFFFFFFFF81000000) // 5).astype(np.int64)
+    second = ((pcs[cs.astype(np.int64) + 1] - 0xFFFFFFFF81000000) // 5).astype(np.int64)
+    assert (((second - (4 * first + 1)) % (1 << 20)) < 4).all()  # the global walk's step
+    # the start blocks' frequencies follow the ranks' k^-1.1
+    k = np.arange(1, 4097, dtype=np.float64)
+    w = k ** -1.1
+    w /= w.sum()
+    vals, counts = np.unique(first, return_counts=True)
+    top = counts[np.argsort(-counts)][:5] / n
+    assert abs(top[0] - w[0]) < 0.03 and abs(top[1] - w[1]) < 0.015 and abs(top[4] - w[4]) < 0.01
+    assert vals.size > 1500  # a long tail of distinct entries
+
+
 def test_synth_m0_known_edges_cover_the_syscalls_signals():
     """Every signal the executor derives for a call to a syscall < known_sys is
     an element of M0's known part (M0 enumerates the region's edges)."""

@@ -51,10 +51,11 @@ def test_edge_c1_batch_vs_oracle(gpu, over, ragged):
     _check(*exp, cs, *out)
 
 
-def test_device_synth_matches_host(gpu):
+@pytest.mark.parametrize("over", [{"skew": 1}, {"skew": 2, "global_walk": 1}])
+def test_device_synth_matches_host(gpu, over):
     from syzkaller_amd import synth
 
-    cfg = synth.synth_default(skew=1)
+    cfg = synth.synth_default(**over)
     cl = synth.call_lengths(16, 8, 0, ragged=(0, 3000), seed=4)
     pcs, cs, prio = synth.traces(cfg, 5, 16, 8, cl)
     dpcs, dcs, dcl, dprio = gpu.synth_traces(cfg, 5, 16, 8, torch.from_numpy(cl.view(np.int32)))

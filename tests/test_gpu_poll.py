@@ -59,3 +59,42 @@ def test_poll_batch_empty_and_nil_max(gpu):
     assert dict(zip(rep[2].Elems.tolist(), rep[2].Prios.tolist())) == {7: 0, 8: 2}
     assert ms.to_dict() == {7: 0, 8: 2}
     assert nm[0].is_nil() and nm[1].is_nil() and nm[2].to_dict() == {7: 0, 8: 2}
+
+
+@pytest.mark.parametrize("case", ["forced_sequential", "hot_element"])
+def test_poll_batch_sequential_path_vs_oracle(gpu, case):
+    """The batch's exact fallback (csrc/poll.hip poll_sequential: the
+    reference loop over the set ops) -- forced (SYZSIG_DEBUG_RECS_GATE gates
+    every element partition), or taken because one element is in every one of
+    3000 polls (its partition holds more than 2048 entries) -- against the
+    oracle's sequential loop."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd._lib import SYZSIG_DEBUG_RECS_GATE
+
+    rng = np.random.default_rng(11)
+    F, U = 6, 4000
+    K, n = (40, 300) if case == "forced_sequential" else (3000, 20)
+    m0 = _serial(rng, 1000, U, dup=False)
+    pre = [None if g % 3 == 0 else _serial(rng, 50, U, dup=False) for g in range(F)]
+    polls = []
+    for _ in range(K):
+        e, p = _serial(rng, int(rng.integers(0, n)), U)
+        if case == "hot_element":
+            e, p = np.append(e, np.uint32(7)), np.append(p, np.int8(rng.integers(-3, 5)))
+        polls.append((int(rng.integers(0, F)), (e, p)))
+    ms = S.Serial(*m0).Deserialize(gpu.eng)
+    nm = [S.Serial(*p).Deserialize(gpu.eng) if p is not None else S.Signal(None, gpu.eng) for p in pre]
+    gpu.eng.set_debug(SYZSIG_DEBUG_RECS_GATE if case == "forced_sequential" else 0)
+    try:
+        replies = S.manager_poll(ms, nm, [(f, S.Serial(e, p)) for f, (e, p) in polls], gpu.eng)
+    finally:
+        gpu.eng.set_debug(0)
+    oms = O.deserialize(*m0)
+    onm = [O.deserialize(*p) if p is not None else O.OSig() for p in pre]
+    for i, (f, ser) in enumerate(polls):
+        re, rp = O.poll(oms, onm, f, ser)
+        got = dict(zip(replies[i].Elems.tolist(), replies[i].Prios.tolist()))
+        assert got == dict(zip(re.tolist(), rp.tolist())), f"reply {i}"
+    assert ms.to_dict() == oms.to_dict()
+    for g in range(F):
+        assert (nm[g].to_dict() if not nm[g].is_nil() else {}) == onm[g].to_dict(), f"fuzzer {g}"
