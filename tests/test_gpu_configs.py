@@ -306,7 +306,7 @@ def test_c4_step_api_1b_global_walk_vs_unsharded(gpu):
     src = []
     for s in range(G):  # 1. every source's staircase into fixed buckets
         a, z = bounds[s], bounds[s + 1]
-        sp = torch.full((8 << 20,), -1, dtype=torch.int64, device=gpu.dev)
+        sp = torch.full((32 << 20,), -1, dtype=torch.int64, device=gpu.dev)
         b, _, scnew = gpu.batch(sigs, cs[a:z].contiguous(), cnt[a:z].contiguous(), prio[a:z].contiguous(),
                                 new_pairs=sp, want_bits=False)
         send = torch.empty(G * W, dtype=torch.int64, device=gpu.dev)
@@ -326,13 +326,18 @@ def test_c4_step_api_1b_global_walk_vs_unsharded(gpu):
         flags.append(f)
         del recv
     got_pairs = []
+    # (one context plays all 8 ranks: the pairs counter a rank's step_send
+    # resets keeps running over these 8 step_back calls, so source s's pairs
+    # are the ones it added, at [before, after) of its own buffer)
+    before = 0
     for s, (b, scnew, sp, send) in enumerate(src):  # 4. the flags back; 5. each source's outputs
         back = torch.cat([flags[g][s * W: (s + 1) * W] for g in range(G)])
         gpu.step_back(b, bounds[s], send, G, cap, back)
         bst = gpu.step_finish()
         assert not bst["global_void"] and not bst["owners_void"], bst
         assert torch.equal(scnew, ref_cnew[bounds[s]: bounds[s + 1]])
-        got_pairs.append(_u(sp[: bst["new_pairs"]], np.uint64) + (np.uint64(bounds[s]) << np.uint64(32)))
+        got_pairs.append(_u(sp[before: bst["new_pairs"]], np.uint64) + (np.uint64(bounds[s]) << np.uint64(32)))
+        before = bst["new_pairs"]
     np.testing.assert_array_equal(np.sort(np.concatenate(got_pairs)), ref_pairs)
     del src, flags
     assert sum(x.Len() for x in shards) == ms.Len()
