@@ -514,9 +514,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __r
 // buffer that fills is written out whole, 16 lanes per block; a record that
 // finds its buffer full waits for the flush (next sub-round).  No tile sort,
 // no scan.  A cell's last partial block is written when its chunk ends.
-#ifndef SYZ_SCAT_DBG
-#define SYZ_SCAT_DBG 0  // experiment builds only: 2 = records dropped after the fetch, 4 = no block stores
-#endif
 constexpr uint32_t kBlk = 16;            // records per written block (64 B)
 constexpr uint32_t kDummyLines = 2048;  // CapCells::dummy lines
 // records per lane per tile
@@ -540,7 +537,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 {
 	constexpr uint32_t kWaves = kAggThreads / 64, kPer = kEntry ? SYZ_SCAT_PER_ENTRY : SYZ_SCAT_PER, kQuota = kPer * 64;
 	constexpr uint32_t kG = 64 / kB;  // blocks a wave writes per store (kB lanes each)
-	constexpr uint32_t kSegs = 2;  // calls per wave tile
 	static_assert(kB == 16 || kB == 32, "block of 64 or 128 B");
 	__shared__ uint32_t buf[kAggMaxParts * kBlk];  // per partition: the block being filled (P * kB <= this)
 	__shared__ uint32_t fillc[kAggMaxParts + 1];   // slots handed out in it (may overshoot kB)
@@ -570,7 +566,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 	if (*cc.ovf)
 		return;  // the run is already void (an optimistic run's assumptions failed, or a cell spilled)
 	bool spilled = false, badlv = false;
-	uint32_t* const dummy = cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
 	if (kEntry) {
 		for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
 			s_lvl[kEntry ? i : 0] = lm.lvl[i];
@@ -583,7 +578,6 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
 		const uint32_t cap = cc.cap[ch];
 		const uint64_t cbase = cc.base[ch];
-		uint32_t* const cell0 = recs + cbase;
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
 			fillc[i] = 0;
 			written[i] = 0;
@@ -597,62 +591,39 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 		__syncthreads();
 		uint32_t wc = w, wo = 0;  // this wave's walk: local call wc (then +kWaves), offset wo inside it
 		uint32_t pv[kEntry ? kPer : 1];  // kEntry: the records' prios (of the last fetch)
-		// Issue the loads of this wave's next quota: up to kSegs calls (segment k
-		// = records [se[k-1], se[k]) of the tile at sb[k] + i, meta sm[k]), all of
-		// it wave-uniform, so a record costs a compare and a select per extra
-		// segment instead of LDS lookups of its call.  t.q = the records.
-		struct Tile {
-			uint32_t se[kSegs], sm[kSegs], ns, q;
-		};
-		auto fetch = [&](uint32_t (&ev)[kPer], Tile& t) {
-			uint64_t sb[kSegs];
-			t.q = 0;
-			t.ns = 0;
+		// issue the loads of this wave's next quota; returns how many records it has
+		auto fetch = [&](uint32_t (&ev)[kPer], uint32_t (&loc)[kPer]) -> uint32_t {
+			uint32_t q = 0;
+			while (q < kQuota && wc < nc) {
+				const uint32_t len = c_len[wc], m = min(kQuota - q, len - wo);
+				const uint32_t tag = ((wc - w) / kWaves) << 24;
+				if (q == 0) {
 #pragma unroll
-			for (uint32_t k = 0; k < kSegs; k++) {
-				while (wc < nc && __builtin_amdgcn_readfirstlane(c_len[wc]) == 0)
-					wc += kWaves;  // (empty calls)
-				if (t.q < kQuota && wc < nc) {
-					// (readfirstlane: the values are uniform; keep them in SGPRs)
-					const uint32_t len = __builtin_amdgcn_readfirstlane(c_len[wc]), m = min(kQuota - t.q, len - wo);
-					const uint64_t st = c_start[wc];
-					sb[k] = (((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(st >> 32)) << 32) |
-					         __builtin_amdgcn_readfirstlane((uint32_t)st)) + wo - t.q;
-					t.sm[k] = __builtin_amdgcn_readfirstlane(c_meta[wc]);
-					t.q += m;
-					wo += m;
-					if (wo == len) {
-						wc += kWaves;
-						wo = 0;
-					}
-					t.ns = k + 1;
-				} else {
-					sb[k] = k ? sb[k - 1] : 0;
-					t.sm[k] = k ? t.sm[k - 1] : 0;
+					for (uint32_t u = 0; u < kPer; u++)
+						loc[u] = tag | wo;  // clamped default: a valid address
 				}
-				t.se[k] = t.q;
-			}
-			if (t.ns == 1 && t.q == kQuota) {  // one call fills the tile: a scalar base, no selects
-				const uint32_t* src = sigs + sb[0];
 #pragma unroll
 				for (uint32_t u = 0; u < kPer; u++) {
-					ev[u] = __builtin_nontemporal_load(&src[u * 64 + lane]);
-					if (kEntry)
-						pv[kEntry ? u : 0] = (uint8_t)__builtin_nontemporal_load(&x.elem_prio[sb[0] + u * 64 + lane]);
+					const uint32_t i = u * 64 + lane;
+					loc[u] = i >= q && i < q + m ? tag | (wo + i - q) : loc[u];
 				}
-			} else if (t.q) {
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; u++) {
-					const uint32_t i = min(u * 64 + lane, t.q - 1);  // clamped: a valid address
-					uint64_t b0 = sb[0];
-#pragma unroll
-					for (uint32_t k = 1; k < kSegs; k++)
-						b0 = k < t.ns && i >= t.se[k - 1] ? sb[k] : b0;
-					ev[u] = __builtin_nontemporal_load(&sigs[b0 + i]);
-					if (kEntry)
-						pv[kEntry ? u : 0] = (uint8_t)__builtin_nontemporal_load(&x.elem_prio[b0 + i]);
+				q += m;
+				wo += m;
+				if (wo == len) {
+					wc += kWaves;
+					wo = 0;
 				}
 			}
+			if (q) {
+#pragma unroll
+				for (uint32_t u = 0; u < kPer; u++) {
+					const uint64_t at = c_start[w + (loc[u] >> 24) * kWaves] + (loc[u] & 0xFFFFFFu);
+					ev[u] = __builtin_nontemporal_load(&sigs[at]);
+					if (kEntry)
+						pv[kEntry ? u : 0] = (uint8_t)__builtin_nontemporal_load(&x.elem_prio[at]);
+				}
+			}
+			return q;
 		};
 		// write out the blocks that filled in this sub-round: 16 lanes per block,
 		// four blocks per lane group in flight
@@ -676,10 +647,9 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 				for (uint32_t t = 0; t < 4; t++) {
 					const bool ok = jb + t * kWaves * kG + w * kG + grp < nf, fits = wr[t] + kB <= cap;
 					spilled |= ok && !fits;  // the cell is full: the run is redone with counted cells
-					// (a chunk's cells span fewer than 2^32 records: a 32-bit offset)
-					uint32_t* d = ok && fits ? cell0 + (pp[t] * cap + wr[t]) : dummy;
-					if (!(SYZ_SCAT_DBG & 4))  // (experiment builds: timing without the block stores)
-						d[slot] = v[t];
+					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp[t] * cap + wr[t]
+					                         : cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
+					d[slot] = v[t];
 				}
 				__builtin_amdgcn_wave_barrier();
 				if (slot == 0) {  // (a group past the list updates the spare entry kAggMaxParts)
@@ -694,17 +664,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 			rnd++;
 		};
 		// a tile's records: packed record and partition, and the mask of those to place
-		auto pack = [&](const uint32_t (&ev)[kPer], const Tile& t, uint32_t (&rec)[kPer], uint32_t (&pt)[kPer]) -> uint32_t {
+		auto pack = [&](const uint32_t (&ev)[kPer], const uint32_t (&loc)[kPer], uint32_t n, uint32_t (&rec)[kPer],
+		                uint32_t (&pt)[kPer]) -> uint32_t {
 			uint32_t pend = 0;
-			const uint32_t n = t.q;
 #pragma unroll
 			for (uint32_t u = 0; u < kPer; u++) {
 				const uint32_t h = fmix32(ev[u]);
 				pt[u] = g.part(h);
-				uint32_t meta = t.sm[0];  // the record's call meta
-#pragma unroll
-				for (uint32_t k = 1; k < kSegs; k++)
-					meta = k < t.ns && u * 64 + lane >= t.se[k - 1] ? t.sm[k] : meta;
+				uint32_t meta = c_meta[w + (loc[u] >> 24) * kWaves];
 				const bool keep = !kEntry || x.nshards == 1 || owner_of(ev[u], x.nshards) == x.shard;
 				if (kEntry) {
 					const uint32_t lv = s_lvl[pv[kEntry ? u : 0]];
@@ -714,48 +681,48 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 				rec[u] = g.rec(h, meta);
 				pend |= (uint32_t)(u * 64 + lane < n && keep) << u;
 			}
-			return (dbg | SYZ_SCAT_DBG) & 2 ? 0u : pend;  // dbg & 2: timing only, records loaded and dropped
+			return dbg & 2 ? 0u : pend;  // dbg & 2: timing only, records loaded and dropped
 		};
 		// one placement pass: a slot in each record's partition block (all slot
 		// requests in flight together), or it waits for the block's flush; the
-		// blocks this wave filled go to the flush list with one LDS atomic.
-		// Returns the records left.
+		// blocks this lane filled go to the flush list.  Returns what is left.
 		auto place = [&](const uint32_t (&rec)[kPer], const uint32_t (&pt)[kPer], uint32_t pend) -> uint32_t {
-			uint32_t sl[kPer];
+			uint32_t sl[kPer], full = 0;
 #pragma unroll
 			for (uint32_t u = 0; u < kPer; u++)
 				sl[u] = (pend >> u) & 1 ? atomicAdd(&fillc[pt[u]], 1u) : kB;
-			uint32_t tot = 0;
 #pragma unroll
 			for (uint32_t u = 0; u < kPer; u++) {
 				if (sl[u] < kB) {
 					buf[pt[u] * kB + sl[u]] = rec[u];
 					pend &= ~(1u << u);
+					full |= (uint32_t)(sl[u] == kB - 1) << u;
 				}
-				tot += (uint32_t)__popcll(__ballot(sl[u] == kB - 1));
 			}
-			if (tot) {
+			while (__ballot(full != 0)) {
+				const bool has = full != 0;
+				const uint32_t cu = __builtin_ctz(full | (1u << kPer));
+				uint32_t pf = 0;
+#pragma unroll
+				for (uint32_t u = 0; u < kPer; u++)
+					pf = cu == u ? pt[u] : pf;
+				const uint64_t m = __ballot(has);
 				uint32_t base = 0;
 				if (lane == 0)
-					base = atomicAdd(&nfl[rnd & 1], tot);
-				base = __builtin_amdgcn_readfirstlane(base);
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; u++) {
-					const uint64_t fm = __ballot(sl[u] == kB - 1);
-					if (sl[u] == kB - 1)
-						flist[base + lane_rank(fm)] = (uint16_t)pt[u];
-					base += (uint32_t)__popcll(fm);
-				}
+					base = atomicAdd(&nfl[rnd & 1], (uint32_t)__popcll(m));
+				base = __shfl(base, 0, 64);
+				if (has)
+					flist[base + lane_rank(m)] = (uint16_t)pf;
+				full &= full - 1;
 			}
 			return pend;
 		};
-		uint32_t ev[kPer];
-		Tile t;
-		fetch(ev, t);
+		uint32_t ev[kPer], loc[kPer];
+		uint32_t n = fetch(ev, loc);
 		for (;;) {
 			uint32_t rec[kPer], pt[kPer];
-			uint32_t pend = pack(ev, t, rec, pt);
-			fetch(ev, t);  // the next tile's loads fly while this one is placed
+			uint32_t pend = pack(ev, loc, n, rec, pt);
+			n = fetch(ev, loc);  // the next tile's loads fly while this one is placed
 			for (;;) {
 				pend = place(rec, pt, pend);
 				const bool more = wg_or(pend != 0);
@@ -764,7 +731,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 					break;
 				__syncthreads();
 			}
-			if (!wg_or(t.q != 0))  // (its barrier also ends the last flush)
+			if (!wg_or(n != 0))  // (its barrier also ends the last flush)
 				break;
 		}
 		// the chunk's last partial block of every cell, and the cell counts
@@ -785,257 +752,15 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 		atomicOr(x.bad_level, 1u);
 }
 
-// The barrier-free scatter (round 5): the same capped cells as
-// k_agg_scatter_blk, written in the same whole kB-record blocks, without a
-// workgroup barrier inside a chunk.
-//  * Each wave walks its own calls of the chunk (local calls w, w + 16, ...),
-//    with the call's start, length and meta in scalar registers: a record's
-//    address is a scalar base plus the lane's offset and its meta is uniform
-//    (k_agg_scatter_blk looked both up in LDS per record, with 64-bit math).
-//    A tile of kPer records per lane holds at most two calls.
-//  * A record takes a ticket for a slot of its partition's block (one LDS
-//    atomic on tick[p]), writes itself there, and counts itself done (an
-//    atomic on done[p] after a release fence).  The lane whose done count
-//    completes the block is its last writer: every slot is written, so its
-//    wave flushes the block at once (kB lanes per block) and re-opens it
-//    (done, then tick back to 0).  A record whose ticket is past the block
-//    (the block is full and not yet flushed) tries again.
-//  * Progress: a full block is flushed by a lane that already holds its
-//    ticket and is not waiting for anything, so every retry ends.
-// Blocks only leave their waves through complete flushes, so the cells,
-// their counts and the spill rule are k_agg_scatter_blk's.
-template <bool kEntry, uint32_t kB>
-__global__ __launch_bounds__(kAggThreads) void k_agg_scatter_async(const uint32_t* __restrict__ sigs,
-                                                                   const uint64_t* __restrict__ call_start,
-                                                                   const uint32_t* __restrict__ call_len,
-                                                                   const uint8_t* __restrict__ call_prio, LevelMap lm,
-                                                                   uint64_t c0, uint64_t c1, AggGeom g, AggSrc x,
-                                                                   CapCells cc, uint32_t* recs, uint32_t dbg)
-{
-	constexpr uint32_t kWaves = kAggThreads / 64, kPer = kEntry ? SYZ_SCAT_PER_ENTRY : SYZ_SCAT_PER, kQuota = kPer * 64;
-	constexpr uint32_t kG = 64 / kB;  // blocks a wave flushes per store
-	static_assert(kB == 16 || kB == 32, "block of 64 or 128 B");
-	__shared__ uint32_t buf[kAggMaxParts * kBlk];  // per partition: the block being filled (P * kB <= this)
-	__shared__ uint32_t tick[kAggMaxParts];        // slots handed out in it (may overshoot kB)
-	__shared__ uint32_t done[kAggMaxParts];        // slots written
-	__shared__ uint32_t written[kAggMaxParts];     // records of the cell flushed so far
-	__shared__ uint32_t junk[kWaves][64];          // target of the writes and atomics a lane does not make
-	__shared__ uint8_t s_lvl[256];
-	const uint32_t P = 1u << g.pbits, ib = g.ibits;
-	const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id(), grp = lane / kB,
-	               slot = lane & (kB - 1);
-	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << ib) - 1) >> ib;  // work items
-	if (*cc.ovf)
-		return;  // the run is already void (an optimistic run's assumptions failed, or a cell spilled)
-	for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
-		s_lvl[i] = lm.lvl[i];
-	uint32_t* const jk = &junk[w][lane];
-	uint32_t* const dummy = cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
-	bool spilled = false, badlv = false;
-	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-		const uint64_t cbeg = ch << ib;
-		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
-		const uint32_t cap = cc.cap[ch];
-		const uint64_t cbase = cc.base[ch];
-		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-			tick[i] = 0;
-			done[i] = 0;
-			written[i] = 0;
-		}
-		__syncthreads();
-		// this wave's walk: local call wc (its start cs, length cl, meta cm), offset wo
-		uint32_t wc = w, cl = 0, cm = 0, wo = 0;
-		uint64_t cs = 0;
-		auto load_call = [&]() {  // the next non-empty call from wc on; cl = 0 past the last
-			cl = 0;
-			wo = 0;
-			for (; wc < nc; wc += kWaves) {
-				const uint64_t c = c0 + cbeg + wc;
-				cl = __builtin_amdgcn_readfirstlane(call_len[c]);
-				if (cl) {
-					cs = call_start[c];
-					cm = __builtin_amdgcn_readfirstlane(g.meta(kEntry ? 0 : s_lvl[call_prio[c]], cbeg + wc));
-					break;
-				}
-			}
-		};
-		load_call();
-		// a tile: records [0, m1) at b1 + i (meta1), [m1, n) at b2 + i (meta2)
-		struct Tile {
-			uint64_t b1, b2;
-			uint32_t m1, n, meta1, meta2;
-		};
-		auto next_tile = [&](Tile& t) -> bool {
-			if (!cl)
-				return false;
-			t.b1 = cs + wo;
-			t.meta1 = t.meta2 = cm;
-			const uint32_t r1 = cl - wo;
-			if (r1 >= kQuota) {
-				t.m1 = t.n = kQuota;
-				t.b2 = t.b1;
-				wo += kQuota;
-				if (wo == cl) {
-					wc += kWaves;
-					load_call();
-				}
-				return true;
-			}
-			t.m1 = t.n = r1;
-			t.b2 = t.b1;
-			wc += kWaves;
-			load_call();
-			if (cl) {
-				const uint32_t r2 = min(cl, kQuota - r1);
-				t.b2 = cs - r1;  // record i >= m1 is at b2 + i
-				t.meta2 = cm;
-				t.n = r1 + r2;
-				wo = r2;
-				if (wo == cl) {
-					wc += kWaves;
-					load_call();
-				}
-			}
-			return true;
-		};
-		uint32_t pv[kEntry ? kPer : 1];  // kEntry: the records' prios
-		auto fetch = [&](const Tile& t, uint32_t (&ev)[kPer]) {
-			if (t.n == kQuota && t.m1 == kQuota) {
-				const uint32_t* src = sigs + t.b1;
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; u++) {
-					ev[u] = __builtin_nontemporal_load(&src[u * 64 + lane]);
-					if (kEntry)
-						pv[kEntry ? u : 0] = (uint8_t)__builtin_nontemporal_load(&x.elem_prio[t.b1 + u * 64 + lane]);
-				}
-			} else {
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; u++) {
-					const uint32_t i = min(u * 64 + lane, t.n - 1);  // clamped: a valid address
-					const uint64_t at = (i < t.m1 ? t.b1 : t.b2) + i;
-					ev[u] = __builtin_nontemporal_load(&sigs[at]);
-					if (kEntry)
-						pv[kEntry ? u : 0] = (uint8_t)__builtin_nontemporal_load(&x.elem_prio[at]);
-				}
-			}
-		};
-		// flush the blocks whose last writers are the lanes of m (pu: their partitions)
-		auto flush = [&](uint64_t m, uint32_t pu) {
-			while (m) {
-				uint32_t pg = 0;
-				bool vg = false;
-#pragma unroll
-				for (uint32_t k = 0; k < kG; k++) {
-					if (m) {
-						const uint32_t l = (uint32_t)__builtin_ctzll(m);
-						m &= m - 1;
-						const uint32_t pp = __builtin_amdgcn_readlane(pu, l);
-						pg = grp == k ? pp : pg;
-						vg = vg || grp == k;
-					}
-				}
-				const uint32_t v = buf[pg * kB + slot];
-				const uint32_t wr = written[pg];
-				const bool fits = wr + kB <= cap;
-				spilled |= vg && !fits;  // the cell is full: the run is redone with counted cells
-				uint32_t* d = vg && fits ? recs + cbase + (uint64_t)pg * cap + wr : dummy;
-				d[slot] = v;
-				if (vg && slot == 0) {
-					written[pg] = wr + kB;
-					done[pg] = 0;
-					// re-open the block after its slots were read (the release waits for them)
-					__hip_atomic_store(&tick[pg], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-				}
-			}
-		};
-		Tile t;
-		uint32_t ev[kPer];
-		bool have = next_tile(t);
-		if (have)
-			fetch(t, ev);
-		while (have) {
-			uint32_t rec[kPer], pt[kPer];
-			bool pend[kPer];
-#pragma unroll
-			for (uint32_t u = 0; u < kPer; u++) {
-				const uint32_t i = u * 64 + lane;
-				const uint32_t h = fmix32(ev[u]);
-				pt[u] = g.part(h);
-				uint32_t meta = i < t.m1 ? t.meta1 : t.meta2;
-				const bool keep = !kEntry || x.nshards == 1 || owner_of(ev[u], x.nshards) == x.shard;
-				if (kEntry) {
-					const uint32_t lv = s_lvl[pv[kEntry ? u : 0]];
-					badlv |= i < t.n && keep && lv == 0xff;
-					meta |= (lv & 3) << g.cbits();
-				}
-				rec[u] = g.rec(h, meta);
-				pend[u] = i < t.n && keep && !(dbg & 2);  // dbg & 2: timing only, records loaded and dropped
-			}
-			have = next_tile(t);
-			if (have)
-				fetch(t, ev);  // the next tile's loads fly while this one is placed
-			for (;;) {
-				uint32_t tk[kPer];
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; u++)
-					tk[u] = atomicAdd(pend[u] ? &tick[pt[u]] : jk, 1u);
-				bool ok[kPer];
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; u++) {
-					ok[u] = pend[u] && tk[u] < kB;
-					*(ok[u] ? &buf[pt[u] * kB + tk[u]] : jk) = rec[u];
-				}
-				__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // the slots before the done counts
-				bool any = false;
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; u++) {
-					const uint32_t dn = atomicAdd(ok[u] ? &done[pt[u]] : jk, 1u);
-					flush(__ballot(ok[u] && dn == kB - 1), pt[u]);
-					pend[u] = pend[u] && !ok[u];
-					any |= pend[u];
-				}
-				if (!__ballot(any))
-					break;
-				__builtin_amdgcn_s_sleep(1);  // full blocks being flushed by other waves
-			}
-		}
-		__syncthreads();
-		// the chunk's last partial block of every cell, and the cell counts
-		for (uint32_t p = w * kG + grp; p < P; p += kWaves * kG) {
-			const uint32_t c = done[p], wr = written[p];
-			if (wr + c > cap)
-				spilled = true;
-			else if (slot < c)
-				recs[cbase + (uint64_t)p * cap + wr + slot] = buf[p * kB + slot];
-			if (slot == 0)
-				cc.cnt[(uint64_t)p * cc.nchunks + ch] = min(wr + c, cap);
-		}
-		__syncthreads();  // tick/done/written/buf are reset by the next chunk
-	}
-	if (spilled)
-		*cc.ovf = 1u;
-	if (kEntry && x.bad_level && __ballot(badlv) && lane == 0)
-		atomicOr(x.bad_level, 1u);
-}
-
 // The scatter's write-combining blocks fill the same 128 KB of LDS: 64 B per
 // partition at 2048 partitions, whole 128-B lines at <= 1024.
 #ifndef SYZ_SCAT_WIDE
 #define SYZ_SCAT_WIDE 1
 #endif
-#ifndef SYZ_SCAT_ASYNC
-#define SYZ_SCAT_ASYNC 0
-#endif
 template <bool kEntry, typename... A>
 static void scatter_blk(uint32_t grid, hipStream_t s, uint32_t pbits, A... a)
 {
-	const bool wide = SYZ_SCAT_WIDE && pbits < kAggMaxBits;
-	if (SYZ_SCAT_ASYNC) {
-		if (wide)
-			k_agg_scatter_async<kEntry, 32><<<grid, kAggThreads, 0, s>>>(a...);
-		else
-			k_agg_scatter_async<kEntry, 16><<<grid, kAggThreads, 0, s>>>(a...);
-	} else if (wide)
+	if (SYZ_SCAT_WIDE && pbits < kAggMaxBits)
 		k_agg_scatter_blk<kEntry, 32><<<grid, kAggThreads, 0, s>>>(a...);
 	else
 		k_agg_scatter_blk<kEntry, 16><<<grid, kAggThreads, 0, s>>>(a...);

@@ -17,8 +17,6 @@
 // is first[top level present] -- argmax (prio, -rank) again.  The atomic form
 // above remains the fallback for more than 4 distinct prios (the records
 // carry 2 level bits) or a context of >= 2^24 entries.
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <vector>
 
@@ -458,17 +456,15 @@ static int minimize_agg(syzsig_ctx* ctx, const uint64_t* d_off, const uint32_t* 
 static int minimize_order(syzsig_ctx* ctx, const uint64_t* d_off, uint64_t nctx, const uint32_t** order)
 {
 	hipStream_t st = ctx->stream;
-	void *dk, *dtmp = nullptr;
+	void* dk;
 	SYZ_TRY(ws_get(ctx, 13, nctx * 16 + 64, &dk));
 	uint32_t* dv = (uint32_t*)dk + nctx;
 	uint32_t* dk2 = dv + nctx;
 	uint32_t* dv2 = dk2 + nctx;
 	k_min_keys<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, nctx, (uint32_t*)dk, dv);
-	size_t tmp_bytes = 0;
-	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)dk, dk2, dv, dv2, (int)nctx, 0, 32, st));
-	SYZ_TRY(ws_get(ctx, 15, tmp_bytes + 64, &dtmp));
-	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, (uint32_t*)dk, dk2, dv, dv2, (int)nctx, 0, 32, st));
-	*order = dv2;
+	uint32_t *sk, *sv;
+	SYZ_TRY(radix_sort_pairs(ctx, (uint32_t*)dk, dv, dk2, dv2, (uint32_t)nctx, &sk, &sv, 15));
+	*order = sv;
 	return SYZSIG_OK;
 }
 
@@ -693,7 +689,7 @@ int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint
 	if (total && (!d_elems || !d_prios))
 		return fail(SYZSIG_EINVAL, "minimize: NULL entry arrays");
 	// 1. stable order by (Len desc, index asc)
-	void *dk, *dv, *dk2, *dv2, *drank, *dtmp = nullptr;
+	void *dk, *dv, *dk2, *dv2, *drank;
 	SYZ_TRY(ws_get(ctx, 13, nctx * 16 + 64, &dk));
 	dv = (uint32_t*)dk + nctx;
 	dk2 = (uint32_t*)dv + nctx;
@@ -702,13 +698,10 @@ int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[3], st));
 	k_min_keys<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, nctx, (uint32_t*)dk, (uint32_t*)dv);
-	size_t tmp_bytes = 0;
-	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)dk, (uint32_t*)dk2, (uint32_t*)dv,
-	                                           (uint32_t*)dv2, (int)nctx, 0, 32, st));
-	SYZ_TRY(ws_get(ctx, 15, tmp_bytes + 64, &dtmp));
-	SYZ_HIP(hipcub::DeviceRadixSort::SortPairs(dtmp, tmp_bytes, (uint32_t*)dk, (uint32_t*)dk2, (uint32_t*)dv,
-	                                           (uint32_t*)dv2, (int)nctx, 0, 32, st));
-	const uint32_t* order = (const uint32_t*)dv2;
+	uint32_t *sk, *sv;
+	SYZ_TRY(radix_sort_pairs(ctx, (uint32_t*)dk, (uint32_t*)dv, (uint32_t*)dk2, (uint32_t*)dv2, (uint32_t)nctx, &sk,
+	                         &sv, 15));
+	const uint32_t* order = sv;
 	bool used = false;
 	if (total && !(ctx->agg_dbg & SYZSIG_DEBUG_MIN_ATOMIC))
 		SYZ_TRY(minimize_agg(ctx, d_off, d_elems, d_prios, nctx, total, nshards, shard, hint_distinct, order, d_keep,
