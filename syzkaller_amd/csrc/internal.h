@@ -236,11 +236,11 @@ int rp_triage_records(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, const ui
 constexpr uint32_t kRpGroupCap = 2048;
 int rp_group(syzsig_ctx* ctx, const uint64_t* x, uint64_t n, uint64_t** keys, uint32_t** base, uint32_t* pbits,
              unsigned long long* ctr);
-// Stable LSD radix sort of n (u32 key, u32 value) pairs (sort.hip), ping-pong
-// between the input and tmp buffers; *keys_out / *vals_out = the sorted pairs.
-// Enqueues only; scratch workspace slot ws_slot.
+// Stable LSD radix sort of n (u32 key, u32 value) pairs, keys < 2^key_bits
+// (sort.hip), ping-pong between the input and tmp buffers; *keys_out /
+// *vals_out = the sorted pairs.  Enqueues only; scratch workspace slot ws_slot.
 int radix_sort_pairs(syzsig_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* keys_tmp, uint32_t* vals_tmp,
-                     uint32_t n, uint32_t** keys_out, uint32_t** vals_out, int ws_slot);
+                     uint32_t n, uint32_t key_bits, uint32_t** keys_out, uint32_t** vals_out, int ws_slot);
 // a set an owner step holds until syzsig_step_finish takes no other call
 inline int set_check_idle(const syzsig_set* s)
 {

@@ -24,13 +24,35 @@
 
 namespace syz {
 
-__global__ void k_min_keys(const uint64_t* __restrict__ off, uint64_t n, uint32_t* keys, uint32_t* idx)
+// the longest context (clamped to 2^32 - 1) into *mx (zeroed by the caller)
+__global__ __launch_bounds__(256) void k_min_maxlen(const uint64_t* __restrict__ off, uint64_t n, uint32_t* mx)
+{
+	uint32_t m = 0;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+		m = max(m, (uint32_t)min<uint64_t>(off[i + 1] - off[i], 0xFFFFFFFFull));
+	for (int o = 32; o > 0; o >>= 1)
+		m = max(m, (uint32_t)__shfl_xor(m, o, 64));
+	if (lane_id() == 0 && m)
+		atomicMax(mx, m);
+}
+
+// ascending key = Len desc: maxlen - len (< 2^bits(maxlen), the sort's passes)
+__global__ void k_min_keys(const uint64_t* __restrict__ off, uint64_t n, uint32_t maxlen, uint32_t* keys,
+                           uint32_t* idx)
 {
 	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-		uint64_t len = off[i + 1] - off[i];
-		keys[i] = 0xFFFFFFFFu - (uint32_t)min<uint64_t>(len, 0xFFFFFFFFull);  // ascending key = Len desc
+		const uint64_t len = off[i + 1] - off[i];
+		keys[i] = maxlen - (uint32_t)min<uint64_t>(len, maxlen);
 		idx[i] = (uint32_t)i;
 	}
+}
+
+static uint32_t bits_of(uint32_t x)
+{
+	uint32_t b = 0;
+	while (b < 32 && (x >> b))
+		b++;
+	return b;
 }
 
 __global__ void k_min_rank(const uint32_t* __restrict__ order, uint64_t n, uint32_t* rank_of)
@@ -461,9 +483,14 @@ static int minimize_order(syzsig_ctx* ctx, const uint64_t* d_off, uint64_t nctx,
 	uint32_t* dv = (uint32_t*)dk + nctx;
 	uint32_t* dk2 = dv + nctx;
 	uint32_t* dv2 = dk2 + nctx;
-	k_min_keys<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, nctx, (uint32_t*)dk, dv);
+	uint32_t maxlen = 0;
+	SYZ_HIP(hipMemsetAsync(dk2, 0, 4, st));
+	k_min_maxlen<<<grid_for(nctx, 256, 1024), 256, 0, st>>>(d_off, nctx, dk2);
+	SYZ_HIP(hipMemcpyAsync(&maxlen, dk2, 4, hipMemcpyDeviceToHost, st));
+	SYZ_HIP(hipStreamSynchronize(st));
+	k_min_keys<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, nctx, maxlen, (uint32_t*)dk, dv);
 	uint32_t *sk, *sv;
-	SYZ_TRY(radix_sort_pairs(ctx, (uint32_t*)dk, dv, dk2, dv2, (uint32_t)nctx, &sk, &sv, 15));
+	SYZ_TRY(radix_sort_pairs(ctx, (uint32_t*)dk, dv, dk2, dv2, (uint32_t)nctx, bits_of(maxlen), &sk, &sv, 15));
 	*order = sv;
 	return SYZSIG_OK;
 }
@@ -683,24 +710,29 @@ int syzsig_minimize_shard_dev(syzsig_ctx* ctx, const uint64_t* d_off, const uint
 	if (nctx >= 0xFFFFFFull)
 		return fail(SYZSIG_ERANGE, "minimize: more than 2^24-2 contexts");
 	hipStream_t st = ctx->stream;
-	uint64_t total = 0;
-	SYZ_HIP(hipMemcpyAsync(&total, d_off + nctx, 8, hipMemcpyDeviceToHost, st));
-	SYZ_HIP(hipStreamSynchronize(st));
-	if (total && (!d_elems || !d_prios))
-		return fail(SYZSIG_EINVAL, "minimize: NULL entry arrays");
-	// 1. stable order by (Len desc, index asc)
 	void *dk, *dv, *dk2, *dv2, *drank;
 	SYZ_TRY(ws_get(ctx, 13, nctx * 16 + 64, &dk));
 	dv = (uint32_t*)dk + nctx;
 	dk2 = (uint32_t*)dv + nctx;
 	dv2 = (uint32_t*)dk2 + nctx;
 	SYZ_TRY(ws_get(ctx, 14, nctx * 4 + 64, &drank));
+	// the entry count and the longest context (the order's sort passes), one sync
+	uint64_t total = 0;
+	uint32_t maxlen = 0;
+	SYZ_HIP(hipMemsetAsync(dk2, 0, 4, st));
+	k_min_maxlen<<<grid_for(nctx, 256, 1024), 256, 0, st>>>(d_off, nctx, (uint32_t*)dk2);
+	SYZ_HIP(hipMemcpyAsync(&maxlen, dk2, 4, hipMemcpyDeviceToHost, st));
+	SYZ_HIP(hipMemcpyAsync(&total, d_off + nctx, 8, hipMemcpyDeviceToHost, st));
+	SYZ_HIP(hipStreamSynchronize(st));
+	if (total && (!d_elems || !d_prios))
+		return fail(SYZSIG_EINVAL, "minimize: NULL entry arrays");
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[3], st));
-	k_min_keys<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, nctx, (uint32_t*)dk, (uint32_t*)dv);
+	// 1. stable order by (Len desc, index asc)
+	k_min_keys<<<grid_for(nctx, 256), 256, 0, st>>>(d_off, nctx, maxlen, (uint32_t*)dk, (uint32_t*)dv);
 	uint32_t *sk, *sv;
-	SYZ_TRY(radix_sort_pairs(ctx, (uint32_t*)dk, (uint32_t*)dv, (uint32_t*)dk2, (uint32_t*)dv2, (uint32_t)nctx, &sk,
-	                         &sv, 15));
+	SYZ_TRY(radix_sort_pairs(ctx, (uint32_t*)dk, (uint32_t*)dv, (uint32_t*)dk2, (uint32_t*)dv2, (uint32_t)nctx,
+	                         bits_of(maxlen), &sk, &sv, 15));
 	const uint32_t* order = sv;
 	bool used = false;
 	if (total && !(ctx->agg_dbg & SYZSIG_DEBUG_MIN_ATOMIC))

@@ -4,7 +4,7 @@
 // the greedy pass).  200k contexts at C3: microseconds, so it is written for
 // simplicity, not speed -- no library sort.
 //
-// Four passes of 8-bit digits.  Per pass: k_rs_hist counts each tile's digits
+// One pass per 8-bit digit of the keys' significant bits.  Per pass: k_rs_hist counts each tile's digits
 // (tiles of kRsTile keys, one wave each), k_rs_scan turns the digit-major
 // counts into every (digit, tile) run's place, and k_rs_scatter writes the
 // tile's keys in order: one wave walks its tile 64 keys at a time, a key's rank
@@ -35,30 +35,37 @@ __global__ __launch_bounds__(64) void k_rs_hist(const uint32_t* __restrict__ key
 		hist[(uint64_t)d * ntiles + t] = h[d];
 }
 
-// exclusive scan of m counts in place (one workgroup)
+// exclusive scan of m counts in place (one workgroup): 1024 counts per step,
+// coalesced, a block scan each, the running total carried
 __global__ __launch_bounds__(1024) void k_rs_scan(uint32_t* v, uint32_t m)
 {
-	__shared__ uint32_t part[1024];
-	const uint32_t per = (m + 1023) / 1024, a = threadIdx.x * per, z = min(m, a + per);
-	uint32_t s = 0;
-	for (uint32_t i = a; i < z; i++)
-		s += v[i];
-	part[threadIdx.x] = s;
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		uint32_t run = 0;
-		for (uint32_t k = 0; k < 1024; k++) {
-			const uint32_t x = part[k];
-			part[k] = run;
-			run += x;
+	__shared__ uint32_t wsum[16];
+	__shared__ uint32_t s_carry;
+	const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+	if (tid == 0)
+		s_carry = 0;
+	for (uint32_t b = 0; b < m; b += 1024) {
+		const uint32_t i = b + tid;
+		const uint32_t x = i < m ? v[i] : 0;
+		uint32_t inc = x;
+#pragma unroll
+		for (uint32_t d = 1; d < 64; d <<= 1) {
+			const uint32_t y = __shfl_up(inc, d, 64);
+			inc += lane >= d ? y : 0;
 		}
-	}
-	__syncthreads();
-	uint32_t run = part[threadIdx.x];
-	for (uint32_t i = a; i < z; i++) {
-		const uint32_t x = v[i];
-		v[i] = run;
-		run += x;
+		if (lane == 63)
+			wsum[w] = inc;
+		__syncthreads();
+		uint32_t pre = s_carry, tot = 0;
+		for (uint32_t k = 0; k < 16; k++) {
+			pre += k < w ? wsum[k] : 0;
+			tot += wsum[k];
+		}
+		if (i < m)
+			v[i] = pre + inc - x;
+		__syncthreads();  // wsum and s_carry are rewritten by the next step
+		if (tid == 0)
+			s_carry += tot;
 	}
 }
 
@@ -95,7 +102,7 @@ __global__ __launch_bounds__(64) void k_rs_scatter(const uint32_t* __restrict__ 
 }
 
 int radix_sort_pairs(syzsig_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* keys_tmp, uint32_t* vals_tmp,
-                     uint32_t n, uint32_t** keys_out, uint32_t** vals_out, int ws_slot)
+                     uint32_t n, uint32_t key_bits, uint32_t** keys_out, uint32_t** vals_out, int ws_slot)
 {
 	*keys_out = keys;
 	*vals_out = vals;
@@ -107,7 +114,7 @@ int radix_sort_pairs(syzsig_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* 
 	uint32_t* hist = (uint32_t*)wh;
 	const hipStream_t s = ctx->stream;
 	uint32_t *ki = keys, *vi = vals, *ko = keys_tmp, *vo = vals_tmp;
-	for (uint32_t shift = 0; shift < 32; shift += 8) {
+	for (uint32_t shift = 0; shift < std::min(key_bits, 32u); shift += 8) {  // (keys < 2^key_bits)
 		k_rs_hist<<<ntiles, 64, 0, s>>>(ki, n, shift, ntiles, hist);
 		k_rs_scan<<<1, 1024, 0, s>>>(hist, 256 * ntiles);
 		k_rs_scatter<<<ntiles, 64, 0, s>>>(ki, vi, n, shift, ntiles, hist, ko, vo);
@@ -115,7 +122,7 @@ int radix_sort_pairs(syzsig_ctx* ctx, uint32_t* keys, uint32_t* vals, uint32_t* 
 		std::swap(vi, vo);
 	}
 	SYZ_HIP(hipGetLastError());
-	*keys_out = ki;  // (after four passes: the input buffers)
+	*keys_out = ki;
 	*vals_out = vi;
 	return SYZSIG_OK;
 }

@@ -30,7 +30,7 @@ def _port():
     return p
 
 
-def worker(rank, world, port, outdir, want_bits, cap, gate=False):
+def worker(rank, world, port, outdir, want_bits, cap, gate=False, backend="gloo"):
     import torch
     import torch.distributed as dist
 
@@ -39,8 +39,12 @@ def worker(rank, world, port, outdir, want_bits, cap, gate=False):
     from syzkaller_amd.device import Device
     from syzkaller_amd.dist import GpuShardOps, ShardedTriage
 
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     torch.cuda.set_device(0)
+    if backend == "nccl":  # RCCL: its collectives run on RCCL's own streams
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     dev = Device(0)
     dev.L.syzsig_ctx_set_timing(dev.eng.h, 1)
     if gate:  # every owner's LDS records pass reports an overflow: the fix-up path
@@ -83,20 +87,24 @@ def worker(rank, world, port, outdir, want_bits, cap, gate=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,want_bits,cap,gate", [(2, True, None, False), (2, False, None, False),
-                                                       (2, False, 256, False), (4, True, None, False),
-                                                       (4, False, 256, False), (2, True, None, True)])
-def test_gpu_sharded_step_gloo(world, want_bits, cap, gate):
+@pytest.mark.parametrize("world,want_bits,cap,gate,backend", [
+    (2, True, None, False, "gloo"), (2, False, None, False, "gloo"), (2, False, 256, False, "gloo"),
+    (4, True, None, False, "gloo"), (4, False, 256, False, "gloo"), (2, True, None, True, "gloo"),
+    (1, False, None, False, "nccl"), (1, True, 256, True, "nccl")])
+def test_gpu_sharded_step_gloo(world, want_bits, cap, gate, backend):
     """The stream-ordered step (syzsig_step_*: staircase buckets, equal-split
     exchanges, the owners' LDS-partitioned replay, flags back) on the real
     kernels, 2 or 4 ranks on one GPU over gloo, two consecutive batches;
     cap=256 overflows the first step's buckets, which is redone with a larger
     cap; gate: every owner skips its LDS pass, so every step takes the owner
-    fix-up (per-record redo, a second flags exchange)."""
+    fix-up (per-record redo, a second flags exchange).  backend nccl: one rank
+    over RCCL (it refuses two ranks on one GPU) -- the exchanges run on RCCL's
+    own streams, so the library's ordering against them (its blocking stream
+    against torch's null stream, device.py) is what is checked."""
     from tests.test_gpu_triage import oracle_pairs
     from syzkaller_amd import synth
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(worker, args=(world, _port(), d, want_bits, cap, gate), nprocs=world,
+        mp.start_processes(worker, args=(world, _port(), d, want_bits, cap, gate, backend), nprocs=world,
                            start_method="spawn")
         res = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     if gate:
