@@ -60,7 +60,9 @@ void* syzsig_ctx_stream(syzsig_ctx* ctx);
 /* Record HIP events around the triage kernels (batch stats probe_ms/decide_ms). */
 int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable);
 /* With timing on: device time (ms, HIP events on the context stream) of the
- * kernels of the last syzsig_edge_derive_dev / syzsig_minimize_dev call. */
+ * kernels of the last syzsig_edge_derive_dev / syzsig_minimize_dev call, or the
+ * stream work of the last syzsig_manager_poll_batch call (uploads to its last
+ * kernel, including the host round trips between). */
 double syzsig_ctx_last_ms(syzsig_ctx* ctx);
 /* Measurement: a plain device copy of `bytes` (16-B aligned buffers and size)
  * on the context stream, 16 B per lane per step; *ms = its device time (HIP

@@ -1,4 +1,4 @@
-"""Run one of bench.py's extra lines alone (c5, c4, c1, gw, rw, pipe; then the walk: global | region), for
+"""Run one of bench.py's extra lines alone (c5, c4, c1, gw, rw, pipe, poll; then the walk: global | region), for
 profiling: the line's JSON object on stdout."""
 import json
 import os
@@ -23,6 +23,8 @@ elif which == "gw":
     out = bench.c2_walk_line(dev, pairs, 4096, 64, 4096, "global")
 elif which == "rw":
     out = bench.c2_walk_line(dev, pairs, 4096, 64, 4096, "region")
+elif which == "poll":
+    out = bench.poll_line(dev)
 elif which == "pipe":
     out = bench.pipeline_line(dev, pairs, 4096, 64, 4096, WALK)
 else:

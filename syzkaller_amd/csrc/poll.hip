@@ -76,6 +76,15 @@ __device__ __forceinline__ void poll_put(uint64_t* T, uint64_t C, uint64_t w)
 	}
 }
 
+// every entry's poll (poll_off as the caller gave it: entries from off[0] on)
+__global__ __launch_bounds__(256) void k_poll_recpoll(const uint64_t* __restrict__ off, uint32_t K, uint32_t* rec_poll)
+{
+	const uint64_t o0 = off[0];
+	for (uint32_t i = blockIdx.x; i < K; i += gridDim.x)
+		for (uint64_t r = off[i] + threadIdx.x; r < off[i + 1]; r += blockDim.x)
+			rec_poll[r - o0] = i;
+}
+
 // the entries for rp_group: e << 32 | entry index
 __global__ void k_poll_x(const uint32_t* __restrict__ elems, uint64_t n, uint64_t* x)
 {
@@ -208,12 +217,32 @@ __global__ void k_poll_pre(const uint64_t* __restrict__ slots, uint64_t nslots, 
 	}
 }
 
-__global__ void k_poll_count(const uint64_t* __restrict__ T, uint64_t C, unsigned int* tcount)
+// Per-target counts (k_poll_count) and inserts (k_poll_scatter) are summed
+// in LDS per workgroup when the targets fit (a batch has K + F of them, and
+// thousands of workgroups adding into a few hundred global counters serialise
+// on them), else with global atomics.
+constexpr uint32_t kPollLdsTargets = 8192;
+
+__global__ __launch_bounds__(256) void k_poll_count(const uint64_t* __restrict__ T, uint64_t C, unsigned int* tcount,
+                                                    uint32_t ntargets)
 {
+	__shared__ unsigned int lc[kPollLdsTargets];
+	const bool lds = ntargets <= kPollLdsTargets;
+	if (lds) {
+		for (uint32_t t = threadIdx.x; t < ntargets; t += blockDim.x)
+			lc[t] = 0;
+		__syncthreads();
+	}
 	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < C; i += (uint64_t)gridDim.x * blockDim.x) {
 		const uint64_t w = T[i];
 		if (w != kPollEmpty)
-			atomicAdd(&tcount[w >> 40], 1u);
+			atomicAdd(lds ? &lc[w >> 40] : &tcount[w >> 40], 1u);
+	}
+	if (lds) {
+		__syncthreads();
+		for (uint32_t t = threadIdx.x; t < ntargets; t += blockDim.x)
+			if (lc[t])
+				atomicAdd(&tcount[t], lc[t]);
 	}
 }
 
@@ -222,9 +251,17 @@ struct PollTarget {
 	uint64_t bmask;
 };
 
-__global__ void k_poll_scatter(const uint64_t* __restrict__ T, uint64_t C, const PollTarget* __restrict__ tg,
-                               unsigned int* tins, unsigned long long* ctr)
+__global__ __launch_bounds__(256) void k_poll_scatter(const uint64_t* __restrict__ T, uint64_t C,
+                                                      const PollTarget* __restrict__ tg, unsigned int* tins,
+                                                      uint32_t ntargets, unsigned long long* ctr)
 {
+	__shared__ unsigned int lc[kPollLdsTargets];
+	const bool lds = ntargets <= kPollLdsTargets;
+	if (lds) {
+		for (uint32_t t = threadIdx.x; t < ntargets; t += blockDim.x)
+			lc[t] = 0;
+		__syncthreads();
+	}
 	uint64_t ovf = 0;
 	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < C; i += (uint64_t)gridDim.x * blockDim.x) {
 		const uint64_t w = T[i];
@@ -233,8 +270,14 @@ __global__ void k_poll_scatter(const uint64_t* __restrict__ T, uint64_t C, const
 		const uint32_t t = (uint32_t)(w >> 40);
 		const int r = tbl_merge(tg[t].slots, tg[t].bmask, (uint32_t)(w >> 8), (int8_t)((uint8_t)w ^ 0x80u));
 		if (r == 1)
-			atomicAdd(&tins[t], 1u);
+			atomicAdd(lds ? &lc[t] : &tins[t], 1u);
 		ovf += r < 0;
+	}
+	if (lds) {
+		__syncthreads();
+		for (uint32_t t = threadIdx.x; t < ntargets; t += blockDim.x)
+			if (lc[t])
+				atomicAdd(&tins[t], lc[t]);
 	}
 	block_count(&ctr[kCntOverflow], ovf);
 }
@@ -325,16 +368,13 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 		return fail(SYZSIG_ERANGE, "manager_poll_batch: polls x fuzzers or entries x fuzzers too large for one batch");
 	const hipStream_t s = ctx->stream;
 	// next target of (poll i, fuzzer g): g's next poll after i, else K + g (its final newMaxSignal)
-	std::vector<uint32_t> next((uint64_t)K * F), rec_poll(n), last(F);
+	std::vector<uint32_t> next((uint64_t)K * F), last(F);
 	for (uint32_t g = 0; g < F; g++)
 		last[g] = K + g;
 	for (uint32_t i = K; i-- > 0;) {
 		std::copy(last.begin(), last.end(), next.begin() + (uint64_t)i * F);
 		last[poll_fuzzer[i]] = i;
 	}
-	for (uint32_t i = 0; i < K; i++)
-		for (uint64_t r = poll_off[i]; r < poll_off[i + 1]; r++)
-			rec_poll[r - poll_off[0]] = i;
 	// Nothing the caller can see changes until every set is made and sized:
 	// sets made here are freed again on an early return (PollFresh), and
 	// maxSignal, the fuzzers' sets and the replies are written only by the
@@ -351,15 +391,19 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 	void *de, *dp, *drp, *dx, *dev, *dnext;
 	SYZ_TRY(ws_get(ctx, 40, n * 4 + 64, &de));
 	SYZ_TRY(ws_get(ctx, 41, n + 64, &dp));
-	SYZ_TRY(ws_get(ctx, 42, n * 4 + 64, &drp));
+	SYZ_TRY(ws_get(ctx, 42, n * 4 + ((uint64_t)K + 1) * 8 + 64, &drp));
+	uint64_t* doff = (uint64_t*)((uint32_t*)drp + ((n + 1) & ~1ull));
 	SYZ_TRY(ws_get(ctx, 43, n * 8 + 64, &dx));
 	SYZ_TRY(ws_get(ctx, 44, n * 8 + ((uint64_t)K * F + K) * 4 + 64, &dev));
 	dnext = (uint64_t*)dev + n;
 	uint32_t* dpf = (uint32_t*)dnext + (uint64_t)K * F;
+	if (ctx->timing)  // (the call's stream work from its uploads to its last kernel: ctx last_ms)
+		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
 	if (n) {
 		SYZ_HIP(hipMemcpyAsync(de, elems + poll_off[0], n * 4, hipMemcpyHostToDevice, s));
 		SYZ_HIP(hipMemcpyAsync(dp, prios + poll_off[0], n, hipMemcpyHostToDevice, s));
-		SYZ_HIP(hipMemcpyAsync(drp, rec_poll.data(), n * 4, hipMemcpyHostToDevice, s));
+		SYZ_HIP(hipMemcpyAsync(doff, poll_off, ((uint64_t)K + 1) * 8, hipMemcpyHostToDevice, s));
+		k_poll_recpoll<<<std::min<uint32_t>(K, 65536), 256, 0, s>>>(doff, K, (uint32_t*)drp);
 	}
 	if ((uint64_t)K * F)
 		SYZ_HIP(hipMemcpyAsync(dnext, next.data(), (uint64_t)K * F * 4, hipMemcpyHostToDevice, s));
@@ -408,7 +452,7 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 		if (last[g] < K && syzsig_len(new_max[g]))
 			k_poll_pre<<<grid_for(new_max[g]->nslots(), 256), 256, 0, s>>>(new_max[g]->slots, new_max[g]->nslots(),
 			                                                               last[g], (uint64_t*)dT, C);
-	k_poll_count<<<grid_for(C, 256, 8192), 256, 0, s>>>((const uint64_t*)dT, C, tcount);
+	k_poll_count<<<grid_for(C, 256, 2048), 256, 0, s>>>((const uint64_t*)dT, C, tcount, K + F);
 	SYZ_HIP(hipGetLastError());
 	std::vector<unsigned int> hc((uint64_t)K + F);
 	SYZ_HIP(hipMemcpyAsync(hc.data(), tcount, ((uint64_t)K + F) * 4, hipMemcpyDeviceToHost, s));
@@ -440,12 +484,19 @@ extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signa
 	if (E)
 		k_poll_commit<<<grid_for(E, 256, 8192), 256, 0, s>>>((const uint64_t*)dev, E, ms->slots, ms->nbuckets - 1,
 		                                                     ctx->d_cnt);
-	k_poll_scatter<<<grid_for(C, 256, 8192), 256, 0, s>>>((const uint64_t*)dT, C, (const PollTarget*)dtg, tins,
+	k_poll_scatter<<<grid_for(C, 256, 2048), 256, 0, s>>>((const uint64_t*)dT, C, (const PollTarget*)dtg, tins, K + F,
 	                                                      ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
 	std::vector<unsigned int> hi((uint64_t)K + F);
 	SYZ_HIP(hipMemcpyAsync(hi.data(), tins, ((uint64_t)K + F) * 4, hipMemcpyDeviceToHost, s));
+	if (ctx->timing)
+		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
 	SYZ_TRY(counters_fetch(ctx));  // (synchronizes: hi and tg are consumed)
+	if (ctx->timing) {
+		float t = 0;
+		SYZ_HIP(hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]));
+		ctx->last_ms = t;
+	}
 	if (ctx->h_cnt[kCntOverflow])
 		return fail(SYZSIG_EIO, "manager_poll_batch: table overflow after reserve (internal error)");
 	fresh.sets.clear();  // everything made here is handed out now

@@ -251,17 +251,43 @@ __global__ void k_count_live(const uint64_t* __restrict__ slots, uint64_t nslots
 		counts[blockIdx.x] = part;
 }
 
-__global__ void k_scan_counts(unsigned long long* counts, uint32_t n, unsigned long long* total)
+// exclusive scan of the per-block counts in place, *total = their sum: one
+// workgroup, 1024 counts per step (a serial loop over them was a chain of
+// dependent global loads, ~17 us per Serialize of a small set)
+__global__ __launch_bounds__(1024) void k_scan_counts(unsigned long long* counts, uint32_t n,
+                                                      unsigned long long* total)
 {
-	if (threadIdx.x == 0 && blockIdx.x == 0) {
-		unsigned long long run = 0;
-		for (uint32_t i = 0; i < n; i++) {
-			unsigned long long c = counts[i];
-			counts[i] = run;
-			run += c;
+	__shared__ unsigned long long wsum[16];
+	__shared__ unsigned long long s_carry;
+	const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+	if (tid == 0)
+		s_carry = 0;
+	for (uint32_t b = 0; b < n; b += 1024) {
+		const uint32_t i = b + tid;
+		const unsigned long long x = i < n ? counts[i] : 0;
+		unsigned long long inc = x;
+#pragma unroll
+		for (uint32_t d = 1; d < 64; d <<= 1) {
+			const unsigned long long y = __shfl_up(inc, d, 64);
+			inc += lane >= d ? y : 0;
 		}
-		*total = run;
+		if (lane == 63)
+			wsum[w] = inc;
+		__syncthreads();
+		unsigned long long pre = s_carry, tot = 0;
+		for (uint32_t k = 0; k < 16; k++) {
+			pre += k < w ? wsum[k] : 0;
+			tot += wsum[k];
+		}
+		if (i < n)
+			counts[i] = pre + inc - x;
+		__syncthreads();  // wsum and s_carry are rewritten by the next step
+		if (tid == 0)
+			s_carry += tot;
 	}
+	__syncthreads();
+	if (tid == 0)
+		*total = s_carry;
 }
 
 __global__ void k_write_live(const uint64_t* __restrict__ slots, uint64_t nslots, uint64_t chunk,
@@ -625,7 +651,7 @@ int syzsig_serialize(syzsig_ctx* ctx, const syzsig_set* s, uint32_t* elems, int8
 	SYZ_TRY(ws_get(ctx, 2, m * 5 + 16, &d_out));
 	unsigned long long* counts = (unsigned long long*)d_counts;
 	k_count_live<<<nblk, 256, 0, ctx->stream>>>(s->slots, nslots, chunk, counts);
-	k_scan_counts<<<1, 64, 0, ctx->stream>>>(counts, nblk, counts + nblk);
+	k_scan_counts<<<1, 1024, 0, ctx->stream>>>(counts, nblk, counts + nblk);
 	uint32_t* de = (uint32_t*)d_out;
 	int8_t* dp = (int8_t*)(de + m);
 	k_write_live<<<nblk, 256, 0, ctx->stream>>>(s->slots, nslots, chunk, counts, de, dp, m);
