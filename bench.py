@@ -151,7 +151,7 @@ def achievable_bw(dev, nbytes=1 << 30, reps=5):
     t = float(np.median(ms))
     del src, dst
     return {"value": 2 * nbytes / (t * 1e-3) / 1e9, "unit": "GB/s", "ms": t, "bytes_copied": nbytes,
-            "kernel": "k_copy16 (16 B per lane, nontemporal loads and stores)", "check": ok}
+            "kernel": "k_copy16 (one 16-B element per lane, nontemporal loads and stores)", "check": ok}
 
 
 def with_achievable(roof, ach):

@@ -82,24 +82,17 @@ int counters_fetch(syzsig_ctx* ctx)
 }  // namespace syz
 
 namespace syz {
-// A plain device copy, 16 B per lane per step (the achievable-bandwidth
-// companion of the rooflines: SURVEY 8(d) "also measure achievable BW with a
-// device copy kernel"); four steps in flight per lane.
+// A plain device copy (the achievable-bandwidth companion of the rooflines:
+// SURVEY 8(d) "also measure achievable BW with a device copy kernel"): one
+// 16-B element per lane, nontemporal, one wave-pass over the buffer -- of the
+// forms measured (scripts/mb_copy.hip: 1-8 elements per lane, grid-stride or
+// not, plain or nontemporal) the fastest, 6.2-6.6 TB/s on 1 GiB.
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_copy16(const v4u* __restrict__ src, v4u* __restrict__ dst, uint64_t n)
 {
 	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-	uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-	for (; i + 3 * stride < n; i += 4 * stride) {
-		const v4u a = __builtin_nontemporal_load(&src[i]), b = __builtin_nontemporal_load(&src[i + stride]);
-		const v4u c = __builtin_nontemporal_load(&src[i + 2 * stride]), d = __builtin_nontemporal_load(&src[i + 3 * stride]);
-		__builtin_nontemporal_store(a, &dst[i]);
-		__builtin_nontemporal_store(b, &dst[i + stride]);
-		__builtin_nontemporal_store(c, &dst[i + 2 * stride]);
-		__builtin_nontemporal_store(d, &dst[i + 3 * stride]);
-	}
-	for (; i < n; i += stride)
-		dst[i] = src[i];
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+		__builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
 }
 }  // namespace syz
 
@@ -253,8 +246,8 @@ int syzsig_copy_bw_dev(syzsig_ctx* ctx, void* d_dst, const void* d_src, uint64_t
 	SYZ_HIP(hipEventCreate(&ev[0]));
 	SYZ_HIP(hipEventCreate(&ev[1]));
 	const uint64_t n = bytes / 16;
-	// one 16-B load and store per lane per step, 8 workgroups per CU
-	const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((n + 1023) / 1024, 1), 256 * 8);
+	// one 16-B element per lane, one pass (grid-stride only past 2^30 threads)
+	const uint32_t grid = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((n + 255) / 256, 1), 1u << 22);
 	int rc = SYZSIG_OK;
 	if (hipEventRecord(ev[0], ctx->stream) != hipSuccess)
 		rc = syz::fail(SYZSIG_EIO, "copy_bw: event record");
