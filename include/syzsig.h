@@ -86,12 +86,17 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
  * the owner side of a sharded step) reports every input as over its capacity,
  * so the per-record path and the step's owner fix-up run (tests).
  * SYZSIG_DEBUG_CAP_SPILL = capped cells of 64 records, so that dense runs
- * overflow them and take the redo with counted cells. */
+ * overflow them and take the redo with counted cells.
+ * SYZSIG_DEBUG_EDGE_MARKALL / SYZSIG_DEBUG_EDGE_PASSES = syzsig_edge_derive_dev
+ * runs the dedup rounds with one marking pass / with marking passes, instead
+ * of choosing from the previous launch's duplicate rate. */
 #define SYZSIG_DEBUG_FIN_DEFER 32u
 #define SYZSIG_DEBUG_MIN_ATOMIC 64u
 #define SYZSIG_DEBUG_EXACT_CELLS 128u
 #define SYZSIG_DEBUG_CAP_SPILL 256u
 #define SYZSIG_DEBUG_RECS_GATE 512u
+#define SYZSIG_DEBUG_EDGE_MARKALL 1024u
+#define SYZSIG_DEBUG_EDGE_PASSES 2048u
 int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
 
 /* ---- pkg/signal/signal.go ---- */

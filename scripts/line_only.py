@@ -1,4 +1,4 @@
-"""Run one of bench.py's extra lines alone (c5, c4, c1, gw, rw, pipe, poll; then the walk: global | region), for
+"""Run one of bench.py's extra lines alone (c5, c4, c1, gw, rw, pipe, poll, edge; then the walk: global | region), for
 profiling: the line's JSON object on stdout."""
 import json
 import os
@@ -25,6 +25,22 @@ elif which == "rw":
     out = bench.c2_walk_line(dev, pairs, 4096, 64, 4096, "region")
 elif which == "poll":
     out = bench.poll_line(dev)
+elif which == "edge":
+    import numpy as np
+    P, C, L = 4096, 64, 4096
+    cl = torch.full((P * C,), L, dtype=torch.int32)
+    pcs, cs, cl, _ = dev.synth_traces(bench.walk_cfg(WALK), 0, P, C, cl)
+    pidx = torch.arange(P + 1, dtype=torch.int32, device=dev.dev) * C
+    sigs = torch.empty(pcs.numel(), dtype=torch.int32, device=dev.dev)
+    cnt = torch.empty(P * C, dtype=torch.int32, device=dev.dev)
+    comp = torch.empty(P, dtype=torch.int32, device=dev.dev)
+    ms = []
+    for i in range(6):
+        dev.edge_derive(pcs, cs, cl, pidx, sigs, cnt, comp)
+        ms.append(dev.L.syzsig_ctx_last_ms(dev.eng.h))
+    out = {"walk": WALK, "edge_dev_ms": float(np.median(ms[1:])), "all": ms,
+           "signals": int(cnt.to(torch.int64).sum().item()),
+           "checksum": int(sigs.to(torch.int64).sum().item())}
 elif which == "pipe":
     out = bench.pipeline_line(dev, pairs, 4096, 64, 4096, WALK)
 else:

@@ -21,6 +21,8 @@ SYZSIG_DEBUG_MIN_ATOMIC = 64
 SYZSIG_DEBUG_EXACT_CELLS = 128
 SYZSIG_DEBUG_CAP_SPILL = 256
 SYZSIG_DEBUG_RECS_GATE = 512
+SYZSIG_DEBUG_EDGE_MARKALL = 1024
+SYZSIG_DEBUG_EDGE_PASSES = 2048
 
 
 class SyzsigError(RuntimeError):

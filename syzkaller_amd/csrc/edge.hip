@@ -22,9 +22,11 @@
 //      itself (conservative about which lane: the earliest pending lane is
 //      never blocked, so every round finalises at least one); a blocked lane
 //      marks too, and marking repeats until no new marks.  Writers mark in the
-//      first pass.  What a lane marks: every slot it can write, now or after a
-//      re-run -- h and its window's slots that are empty now -- and, when
-//      blocked, d (a later lane must not write what it will read again);
+//      first pass (in the mark-all mode every pending lane does, which is the
+//      passes' fixed point at once).  What a lane marks: every slot it can
+//      write, now or after a re-run -- h and its window's slots that are empty
+//      now -- and, when blocked, d (a later lane must not write what it will
+//      read again);
 //   3. unblocked lanes are final: writers store, everyone leaves the round.
 // Why that is exact: a lane's outcome depends on d only, as long as no slot
 // of its window becomes empty again.  An earlier write of a nonzero value !=
@@ -43,8 +45,13 @@
 //     window holding slot 0, so such a later lane waits for the zero write.
 // A final lane has no earlier pending writer that could touch what it read,
 // and duplicates change nothing, so its outcome is the sequential one.
-// Mostly duplicates (repeated edges) finish in few rounds (2.3 per 256-signal
-// chunk on the global walk, 2.5 on the region walk: host simulation).
+// The same invariant says that after any round the pending lanes, run in
+// trace order on the table as it stands, give the sequential outcome: once a
+// round leaves at most kEdgeSeqMax lanes pending (7 per 256-signal chunk on
+// average on the global walk), one wave runs them through plain dedup, one
+// signal per step, instead of further rounds and their barriers.
+// After the first round 7 of 256 lanes are pending on average on the global
+// walk (19.5 on the region walk; host simulation).
 // Rounds need workgroup barriers; they are LDS-only (lds_barrier), so the
 // trace loads in flight are never drained.  The trace is read kEdgeDepth
 // chunks ahead of the chunk being deduplicated, ping-ponging between two
@@ -55,11 +62,34 @@ namespace syz {
 
 constexpr uint32_t kBinShift = 3;  // 8-slot bins
 constexpr uint32_t kBins = kDedupSize >> kBinShift;
-constexpr uint32_t kEdgeDepthSignals = 4;  // trace signals in flight per lane per buffer
+#ifndef SYZ_EDGE_DEPTH
+#define SYZ_EDGE_DEPTH 4
+#endif
+// trace signals in flight per lane per buffer; every chunk of a buffer is a
+// copy of the chunk code (the instruction cache bounds how many fit)
+constexpr uint32_t kEdgeDepthSignals = SYZ_EDGE_DEPTH;
 #ifndef SYZ_EDGE_KS
 #define SYZ_EDGE_KS 1
 #endif
 constexpr uint32_t kEdgeKS = SYZ_EDGE_KS;  // signals per lane per chunk
+#ifndef SYZ_EDGE_SEQ
+#define SYZ_EDGE_SEQ 16
+#endif
+// a round that leaves at most this many lanes pending hands them to one wave,
+// which runs them through plain dedup in trace order (0: rounds only)
+constexpr uint32_t kEdgeSeqMax = SYZ_EDGE_SEQ;
+static_assert(kEdgeSeqMax <= 32, "the tail's masks are 32 bits");
+// Two marking modes, one kernel instantiation each (both exact; one code
+// path per kernel keeps it small and straight):
+//   passes   -- writers mark, blocked lanes mark in further passes until no
+//               new marks (one workgroup OR per pass);
+//   mark-all -- every pending lane marks in the one pass (its write slots and
+//               d: the passes' fixed point at once, extra marks only block
+//               more), no second workgroup OR per round.  On a thrashing table
+//               almost every lane is a writer and marks anyway, so it costs no
+//               blocking there; on mostly-duplicate traces it blocks more.
+// The host picks per launch from the previous launch's duplicate rate.
+constexpr uint32_t kEdgeMarkAllMaxDupPct = 5;  // mark-all below 5 % first-round duplicates
 
 // Geometry of one variant: W waves per program, KS signals per lane, chunks of
 // 64 * W * KS signals (lane l of wave w holds positions k * 64 W + 64 w + l,
@@ -89,7 +119,7 @@ __device__ __forceinline__ void lds_barrier()
 // this epoch's markers (older epochs compare lower): it was set by a position
 // before mine this epoch  <=>  stamp > my own v = epoch << kPosBits | (kPosMask - pos).
 
-template <uint32_t W, uint32_t KS>
+template <uint32_t W, uint32_t KS, bool kMarkAll>
 __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restrict__ pcs, uint64_t npc,
                                                            const uint64_t* __restrict__ call_start,
                                                            const uint32_t* __restrict__ call_len, uint64_t ncalls,
@@ -107,6 +137,11 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 	__shared__ uint32_t fm1[kDedupSize / 32], fm2[kDedupSize / 32];
 	__shared__ __align__(16) uint32_t s_any[2][kEdgeWaves];
 	__shared__ uint32_t s_carry[2][KS][kEdgeWaves];
+	// the tail (KS == 1): each wave's pending signals packed, and per wave the
+	// tail's emitted ones by rank
+	constexpr bool kSeq = KS == 1 && kEdgeSeqMax > 0;
+	__shared__ uint32_t s_sig[kSeq ? kLanes : 1];
+	__shared__ uint64_t s_pm[kEdgeWaves];
 	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, pos = threadIdx.x;  // pos: place in a sub-chunk
 	uint32_t seq = 0;
 	// Workgroup OR of a predicate (one barrier): every wave writes its own
@@ -139,6 +174,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 	};
 	uint64_t err = 0;
 	uint32_t epoch = 0;
+	uint64_t dups = 0;  // first-round duplicates of every chunk (uniform; the host's mode choice)
 	for (uint64_t p = blockIdx.x; p < nprog; p += gridDim.x) {
 		const uint64_t cb = prog_call[p], ce = prog_call[p + 1];
 		if (cb > ce || ce > ncalls) {
@@ -222,7 +258,13 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 				// publishes every wave's emit counts for the output below
 				bool wb1[KS];  // the window's second bin takes a mark
 				uint32_t pset[KS];  // window offsets the lane can write: 0 (h) and the empty slots
-				for (;;) {
+				bool first_round = true;
+				// one round; 0: no lane pending, 1: the tail finished the chunk (output
+				// written), 2: another round.  Instantiated per marking mode, so that
+				// each is straight code.
+				auto round = [&](auto ma_c) -> int {
+					constexpr bool ma = decltype(ma_c)::value;
+					bool dup[KS];
 					// 1. evaluate dedup() (executor.h:692-706) on the current table,
 					// branch-free: the first probe i with T[h+i] == sig (duplicate)
 					// or T[h+i] == 0 (insert there), else the forced overwrite at h
@@ -237,6 +279,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						}
 						const uint32_t first = __builtin_ctz(eqm | zm | 16u);
 						writer[k] = !((eqm >> first) & 1);
+						dup[k] = pending[k] && !writer[k];
 						wpos[k] = (sig[k] + (first & 3)) & (kDedupSize - 1);
 						// whatever it writes, now or after a re-run, goes to h or to a slot
 						// that is empty now (only slot 0 ever becomes empty again); a window
@@ -261,7 +304,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 					for (uint32_t k = 0; k < KS; k++) {
 						v[k] = (epoch << G::kPosBits) | (G::kPosMask - (k * kLanes + pos));
 						dbin[k] = wpos[k] >> kBinShift;
-						mark_win[k] = win_marked[k] = pending[k] && writer[k];
+						mark_win[k] = win_marked[k] = pending[k] && (ma || writer[k]);
 						blocked[k] = false;
 					}
 					for (;;) {
@@ -311,13 +354,19 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 							win_marked[k] = win_marked[k] || mark_win[k];
 							any_new |= mark_win[k];
 						}
-						if (!wg_any(any_new, 0))
+						if (ma || !wg_any(any_new, 0))
 							break;
 					}
 					// this round's slot marks are read: cleared for the next round (the
-					// commit's barrier orders this before the next round's marks)
-					for (uint32_t i = threadIdx.x; i < kDedupSize / 32; i += kLanes)
-						fm1[i] = fm2[i] = 0;
+					// commit's barrier orders this before the next round's marks; with
+					// one marking pass no barrier follows the tests, so the clear waits
+					// for the commit's barrier and needs one of its own before a next round)
+					auto clear_marks = [&]() {
+						for (uint32_t i = threadIdx.x; i < kDedupSize / 32; i += kLanes)
+							fm1[i] = fm2[i] = 0;
+					};
+					if (!ma)
+						clear_marks();
 					// 3. final lanes commit (visible after the next round's barrier)
 					bool any_pending = false;
 					uint32_t counts = 0;
@@ -331,9 +380,125 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						any_pending |= pending[k];
 						counts |= (uint32_t)__popcll(__ballot(emit[k])) << (8 * k);
 					}
-					if (!wg_any(any_pending, counts))
-						break;
-				}
+					if constexpr (kSeq) {
+						const uint64_t pm = __ballot(pending[0]);
+						if (pending[0])  // this wave's pending signals, packed in trace order
+							s_sig[64 * w + lane_rank(pm)] = sig[0];
+						const uint32_t ndup = first_round ? __popcll(__ballot(dup[0])) : 0;
+						const bool more = wg_any(any_pending, counts | (uint32_t)__popcll(pm) << 8 | ndup << 16);
+						if (first_round) {
+#pragma unroll
+							for (uint32_t i = 0; i < kEdgeWaves; i++)
+								dups += row[i] >> 17;
+						}
+						first_round = false;
+						if (ma)
+							clear_marks();  // (ordered before the next chunk's marks by its first barrier)
+						if (!more)
+							return 0;
+						uint32_t npend = 0;
+#pragma unroll
+						for (uint32_t i = 0; i < kEdgeWaves; i++)
+							npend += (row[i] >> 9) & 0xFF;
+						if (npend <= kEdgeSeqMax) {
+							// The tail in one wave, no barriers: lane j holds the j-th pending
+							// signal in trace order.  It waits only for earlier pending signals
+							// whose windows overlap its own -- every write lies in the writer's
+							// window, so a signal no earlier pending window overlaps reads
+							// nothing they can write, and writes nothing they read: its
+							// dedup() (executor.h:692-706) on the table as it stands is the
+							// sequential one.  Passes until none is left; the wave's LDS
+							// operations run in order, so a pass sees the previous one's stores.
+#ifdef SYZ_EDGE_TAIL_DROP  // timing only (results wrong): the tail skipped
+							if (w == 0 && lane < kEdgeWaves)
+								s_pm[lane] = 0;
+							if (false) {
+#else
+							if (w == 0) {
+#endif
+								uint32_t seg = 0, segbase = 0, acc = 0;
+#pragma unroll
+								for (uint32_t i = 0; i < kEdgeWaves; i++) {
+									const uint32_t c = (row[i] >> 9) & 0xFF;
+									if (lane >= acc) {
+										seg = i;
+										segbase = acc;
+									}
+									acc += c;
+								}
+								const bool item = lane < npend;
+								const uint32_t sg = item ? s_sig[64 * seg + lane - segbase] : 0;
+								const uint32_t h = sg & (kDedupSize - 1);
+								// earlier pending signals with an overlapping window (distance <= 3)
+								uint32_t ovm = 0;
+								for (uint32_t k = 0; k < npend; k++) {
+									const uint32_t hk = __builtin_amdgcn_readlane(h, k);
+									const uint32_t d = (h - hk + 3) & (kDedupSize - 1);
+									ovm |= k < lane && d <= 6 ? 1u << k : 0u;
+								}
+								uint32_t act = (uint32_t)__ballot(item), em = 0;
+								while (act) {
+									const bool go = item && ((act >> (lane & 31)) & 1) && !(ovm & act);
+									bool wr = false;
+									if (go) {
+										uint32_t first = 4, tf = 0;
+#pragma unroll
+										for (int q = 3; q >= 0; q--) {
+											const uint32_t t = table[(h + q) & (kDedupSize - 1)];
+											if (t == sg || t == 0) {
+												first = q;
+												tf = t;
+											}
+										}
+										wr = first == 4 || tf != sg;
+										if (wr)
+											table[(h + (first & 3)) & (kDedupSize - 1)] = sg;
+									}
+									em |= (uint32_t)__ballot(wr);
+									act &= ~(uint32_t)__ballot(go);
+								}
+								// the emitted ones, per source wave, by rank among its pending lanes
+								if (lane < kEdgeWaves) {
+									uint32_t c = 0, b = 0;
+#pragma unroll
+									for (uint32_t i = 0; i < kEdgeWaves; i++) {
+										const uint32_t x = (row[i] >> 9) & 0xFF;
+										b += i < lane ? x : 0;
+										c = i == lane ? x : c;
+									}
+									s_pm[lane] = c ? (em >> b) & (~0u >> (32 - c)) : 0;
+								}
+							}
+							lds_barrier();
+							const uint64_t tail = s_pm[w];
+							const bool mine = emit[0] || (pending[0] && ((tail >> lane_rank(pm)) & 1));
+							const uint64_t me = __ballot(mine);
+							uint32_t base = nsig, tot = 0;
+#pragma unroll
+							for (uint32_t i = 0; i < kEdgeWaves; i++) {
+								const uint32_t x = ((row[i] >> 1) & 0xFF) + __popcll(s_pm[i]);
+								base += i < w ? x : 0;
+								tot += x;
+							}
+							if (mine)
+								sigs[start + base + lane_rank(me)] = sig[0];
+							nsig += tot;
+							return 1;
+						}
+						if (ma)
+							lds_barrier();  // the clear before the next round's marks
+					} else {
+						if (!wg_any(any_pending, counts))
+							return 0;
+					}
+					return 2;
+				};
+				int st;
+				do
+					st = round(std::integral_constant<bool, kSeq && kMarkAll>{});
+				while (st == 2);
+				if (st == 1)
+					return true;
 				// write_output order == trace order: sub-chunks in order, then waves,
 				// then lanes
 #pragma unroll
@@ -394,6 +559,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 		lds_barrier();  // the table is re-zeroed for the next program
 	}
 	block_count(&cnt[kCntError], err);
+	block_count(&cnt[kCntAux], threadIdx.x == 0 ? dups : 0);
 }
 
 
@@ -417,21 +583,35 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 	const int grid = (int)std::min<uint64_t>(nprog, 256 * 4);
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
+	// the marking mode: forced by a debug flag, else mark-all while the last
+	// launch's first rounds saw few duplicates (they mark in one pass too)
+	const bool mark_all = ctx->agg_dbg & SYZSIG_DEBUG_EDGE_MARKALL   ? true
+	                      : ctx->agg_dbg & SYZSIG_DEBUG_EDGE_PASSES ? false
+	                                                                : ctx->edge_mark_all;
 #ifdef SYZ_EXPERIMENTS
 	// measured slower: 8 waves 25 ms, 2 waves 16.1, 1 wave 21.3 vs 4 waves 14.9 at C2
 	if (ctx->edge_waves == 8)
-		k_edge_dedup<8, kEdgeKS><<<grid, 512, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
-		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
+		k_edge_dedup<8, kEdgeKS, false><<<grid, 512, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls,
+		                                                          d_prog_call, nprog, d_sigs, d_sig_cnt, d_completed,
+		                                                          ctx->d_cnt);
 	else if (ctx->edge_waves == 2)
-		k_edge_dedup<2, kEdgeKS><<<grid, 128, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
-		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
+		k_edge_dedup<2, kEdgeKS, false><<<grid, 128, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls,
+		                                                          d_prog_call, nprog, d_sigs, d_sig_cnt, d_completed,
+		                                                          ctx->d_cnt);
 	else if (ctx->edge_waves == 1)
-		k_edge_dedup<1, kEdgeKS><<<grid, 64, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
-		                                              nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
+		k_edge_dedup<1, kEdgeKS, false><<<grid, 64, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls,
+		                                                         d_prog_call, nprog, d_sigs, d_sig_cnt, d_completed,
+		                                                         ctx->d_cnt);
 	else
 #endif
-		k_edge_dedup<4, kEdgeKS><<<grid, 256, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls, d_prog_call,
-		                                               nprog, d_sigs, d_sig_cnt, d_completed, ctx->d_cnt);
+	if (mark_all)
+		k_edge_dedup<4, kEdgeKS, true><<<grid, 256, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls,
+		                                                         d_prog_call, nprog, d_sigs, d_sig_cnt, d_completed,
+		                                                         ctx->d_cnt);
+	else
+		k_edge_dedup<4, kEdgeKS, false><<<grid, 256, 0, ctx->stream>>>(d_pcs, npc, d_call_start, d_call_len, ncalls,
+		                                                          d_prog_call, nprog, d_sigs, d_sig_cnt, d_completed,
+		                                                          ctx->d_cnt);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
@@ -443,5 +623,7 @@ extern "C" int syzsig_edge_derive_dev(syzsig_ctx* ctx, const uint64_t* d_pcs, ui
 	}
 	if (ctx->h_cnt[kCntError])
 		return fail(SYZSIG_EINVAL, "edge_derive: malformed program/call ranges or a call with >= 262144 PCs");
+	if (npc)
+		ctx->edge_mark_all = ctx->h_cnt[kCntAux] * 100 < (unsigned long long)kEdgeMarkAllMaxDupPct * npc;
 	return SYZSIG_OK;
 }

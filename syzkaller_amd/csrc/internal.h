@@ -72,7 +72,7 @@ struct Workspace {
 // the debug flags that change only the path taken, never a result
 constexpr uint32_t kDebugResultPreserving =
     SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL |
-    SYZSIG_DEBUG_RECS_GATE;
+    SYZSIG_DEBUG_RECS_GATE | SYZSIG_DEBUG_EDGE_MARKALL | SYZSIG_DEBUG_EDGE_PASSES;
 
 // capped cells of the aggregation path (agg.hip): default slack, in standard deviations
 constexpr float kCapSdDefault = 6.0f;
@@ -112,6 +112,7 @@ struct syzsig_ctx {
 	float cap_sd_entry = syz::kCapSdDefault;  // the same for Minimize's runs
 	bool agg_counted_once = false;        // the next agg_aggregate takes counted cells (a one-sync run spilled)
 	uint32_t edge_waves = 4;              // waves per program of k_edge_dedup (4 or 8; SYZSIG_EDGE_WAVES)
+	bool edge_mark_all = true;            // k_edge_dedup's marking mode for the next launch (edge.hip)
 	uint32_t agg_dbg = 0;                 // SYZSIG_DEBUG_* path flags; timing-only bits need -DSYZ_EXPERIMENTS
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	double last_ms = 0;                   // device time of the last timed entry point's kernels

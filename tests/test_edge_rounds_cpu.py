@@ -68,10 +68,25 @@ def write_slots(s, ps, h):
     return [(h + k) % M for k in range(4) if ps >> k & 1]
 
 
-def round_chunk(T, ch, binsh=3):
-    """One chunk through the rounds; returns (emitted flags, rounds)."""
+def round_chunk(T, ch, binsh=3, seq_max=0, mark_all=False):
+    """One chunk through the rounds; returns (emitted flags, rounds).  Once a
+    round leaves at most seq_max lanes pending, they go to edge.hip's tail
+    (SYZ_EDGE_SEQ): in passes, a pending signal whose window no earlier pending
+    window overlaps runs dedup() on the table as it stands.  That is exact
+    because every write lies in its writer's window, given the rounds'
+    invariant that the pending lanes, run in order on the table as it stands,
+    give the sequential outcome.  mark_all (SYZ_EDGE_MARKALL): every pending
+    lane marks in the first pass, so one pass is the fixed point."""
     n, pend, emit, rounds = len(ch), list(range(len(ch))), [False] * len(ch), 0
     while pend:
+        if rounds and len(pend) <= seq_max:
+            while pend:
+                go = [i for j, i in enumerate(pend)
+                      if all((ch[i] - ch[k] + 3) % M > 6 for k in pend[:j])]
+                for i in go:  # disjoint windows: any order
+                    emit[i] = seq_dedup(T, ch[i])
+                pend = [i for i in pend if i not in go]
+            break
         rounds += 1
         ev = {}
         for i in pend:
@@ -99,6 +114,8 @@ def round_chunk(T, ch, binsh=3):
             w, d, ps, h = ev[i]
             if w:
                 mark(i, write_slots(ch[i], ps, h))
+            elif mark_all:
+                mark(i, write_slots(ch[i], ps, h) + [d])
         while True:
             new = []
             for i in pend:
@@ -128,8 +145,12 @@ def _golden_names():
     return sorted(f[:-4] for f in os.listdir(HERE) if f.startswith("executor_") and f.endswith(".npz"))
 
 
+SEQ_MAX = [0, 24, 256]  # rounds only; the kernel's tail; one round then sequential
+
+
+@pytest.mark.parametrize("seq_max", SEQ_MAX)
 @pytest.mark.parametrize("name", _golden_names())
-def test_rounds_equal_sequential_dedup(name):
+def test_rounds_equal_sequential_dedup(name, seq_max):
     """Every program of every reference-executor fixture, chunk by chunk.
     A program aborted by cover_check is replayed over all its calls: the
     rounds are checked against sequential dedup, not against the abort."""
@@ -145,14 +166,15 @@ def test_rounds_equal_sequential_dedup(name):
                 prev = exec_hash(x & 0xFFFFFFFF)
             for c0 in range(0, len(sigs), 256):
                 ch = sigs[c0: c0 + 256]
-                got, _ = round_chunk(Tp, ch)
+                got, _ = round_chunk(Tp, ch, seq_max=seq_max)
                 want = [seq_dedup(Ts, s) for s in ch]
                 assert got == want, (name, p, c, c0)
                 assert Tp == Ts
 
 
+@pytest.mark.parametrize("seq_max", SEQ_MAX)
 @pytest.mark.parametrize("global_walk,region_log2", [(1, 8), (0, 8), (0, 12)])
-def test_rounds_equal_sequential_dedup_synthetic(global_walk, region_log2):
+def test_rounds_equal_sequential_dedup_synthetic(global_walk, region_log2, seq_max):
     """The bench's trace distributions (SURVEY 8(d)'s global walk: the table
     thrashes, almost every signal a forced overwrite; region walks: mostly
     duplicates), 16 calls of 4096 PCs of one program."""
@@ -168,7 +190,7 @@ def test_rounds_equal_sequential_dedup_synthetic(global_walk, region_log2):
             prev = exec_hash(x & 0xFFFFFFFF)
         for c0 in range(0, len(sigs), 256):
             ch = sigs[c0: c0 + 256]
-            got, _ = round_chunk(Tp, ch)
+            got, _ = round_chunk(Tp, ch, seq_max=seq_max)
             assert got == [seq_dedup(Ts, s) for s in ch], (c, c0)
             assert Tp == Ts
 
@@ -185,8 +207,9 @@ def _zero_stress_chunk(rng, n):
     return [int(vals[j]) for j in rng.choice(len(vals), n, p=p)]
 
 
+@pytest.mark.parametrize("seq_max", SEQ_MAX)
 @pytest.mark.parametrize("seed", range(8))
-def test_rounds_zero_writer_stress(seed):
+def test_rounds_zero_writer_stress(seed, seq_max):
     """Randomized: chunks seeded with zero signals over a table whose slots
     8188..4 start full, empty or mixed; every chunk's flags and the table
     after it equal sequential dedup (executor.h:693-706)."""
@@ -200,9 +223,46 @@ def test_rounds_zero_writer_stress(seed):
         Tp, Ts = list(T), list(T)
         for _ in range(3):
             ch = _zero_stress_chunk(rng, int(rng.integers(8, 257)))
-            got, _ = round_chunk(Tp, ch)
+            got, _ = round_chunk(Tp, ch, seq_max=seq_max)
             want = [seq_dedup(Ts, s) for s in ch]
             assert got == want, (seed, trial)
+            assert Tp == Ts, (seed, trial)
+
+
+@pytest.mark.parametrize("seq_max", [0, 16])
+@pytest.mark.parametrize("name", _golden_names())
+def test_rounds_mark_all_equal_sequential_dedup(name, seq_max):
+    """The one-pass marking variant (SYZ_EDGE_MARKALL) on every fixture."""
+    d = np.load(os.path.join(HERE, name + ".npz"))
+    pcs, cs, cl, pc = d["pcs"], d["call_start"], d["call_len"], d["prog_call"]
+    for p in range(pc.size - 1):
+        Tp, Ts = [0] * M, [0] * M
+        for c in range(int(pc[p]), int(pc[p + 1])):
+            trace = pcs[int(cs[c]): int(cs[c]) + int(cl[c])].tolist()
+            prev, sigs = 0, []
+            for x in trace:
+                sigs.append((x & 0xFFFFFFFF) ^ prev)
+                prev = exec_hash(x & 0xFFFFFFFF)
+            for c0 in range(0, len(sigs), 256):
+                ch = sigs[c0: c0 + 256]
+                got, _ = round_chunk(Tp, ch, seq_max=seq_max, mark_all=True)
+                assert got == [seq_dedup(Ts, s) for s in ch], (name, p, c, c0)
+                assert Tp == Ts
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_rounds_mark_all_zero_writer_stress(seed):
+    rng = np.random.default_rng(100 + seed)
+    for trial in range(40):
+        T = [0] * M
+        for sl in list(range(M - 6, M)) + list(range(0, 7)):
+            if trial % 3 == 0 or (trial % 3 == 2 and rng.random() < 0.6):
+                T[sl] = int(rng.integers(1, 5)) * M + sl
+        Tp, Ts = list(T), list(T)
+        for _ in range(3):
+            ch = _zero_stress_chunk(rng, int(rng.integers(8, 257)))
+            got, _ = round_chunk(Tp, ch, seq_max=16, mark_all=True)
+            assert got == [seq_dedup(Ts, s) for s in ch], (seed, trial)
             assert Tp == Ts, (seed, trial)
 
 

@@ -9,6 +9,19 @@ from tests.conftest import golden_names, load_golden
 
 pytestmark = pytest.mark.gpu
 
+# K2's two marking modes (edge.hip), forced; None = the library's own choice
+MODES = [None, "markall", "passes"]
+
+
+@pytest.fixture
+def mode(gpu, request):
+    from syzkaller_amd._lib import SYZSIG_DEBUG_EDGE_MARKALL, SYZSIG_DEBUG_EDGE_PASSES
+
+    m = request.param
+    gpu.eng.set_debug({None: 0, "markall": SYZSIG_DEBUG_EDGE_MARKALL, "passes": SYZSIG_DEBUG_EDGE_PASSES}[m])
+    yield m
+    gpu.eng.set_debug(0)
+
 
 def _run(gpu, pcs, call_start, call_len, prog_call):
     d = gpu.dev
@@ -28,16 +41,19 @@ def _check(fx_sigs, fx_cnt, fx_comp, call_start, sigs, cnt, comp):
         np.testing.assert_array_equal(sigs[s: s + n], fx_sigs[s: s + n], err_msg=f"call {c}")
 
 
+@pytest.mark.parametrize("mode", MODES, indirect=True)
 @pytest.mark.parametrize("name", golden_names())
-def test_edge_matches_reference_executor_goldens(gpu, name):
+def test_edge_matches_reference_executor_goldens(gpu, name, mode):
     fx = load_golden(name)
     out = _run(gpu, fx["pcs"], fx["call_start"], fx["call_len"], fx["prog_call"])
     _check(fx["exp_sigs"], fx["exp_cnt"], fx["exp_completed"], fx["call_start"], *out)
 
 
 @pytest.mark.parametrize("over,ragged", [({}, None), ({"region_log2": 12}, (0, 3000)),
-                                          ({"bad_pc_ppm": 20}, (0, 4000)), ({"skew": 1}, None)])
-def test_edge_c1_batch_vs_oracle(gpu, over, ragged):
+                                          ({"bad_pc_ppm": 20}, (0, 4000)), ({"skew": 1}, None),
+                                          ({"global_walk": 1}, None)])
+@pytest.mark.parametrize("mode", MODES[1:], indirect=True)
+def test_edge_c1_batch_vs_oracle(gpu, over, ragged, mode):
     """Config 1 shape: 64 programs x 32 calls x 2k PCs (ragged variants)."""
     from syzkaller_amd import synth
 

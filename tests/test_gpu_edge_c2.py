@@ -64,11 +64,18 @@ def _check_edge_slices(cfg, sigs, cnt, comp):
         np.testing.assert_array_equal(dev[live], es.reshape(-1, PCS)[live], err_msg=f"signals, programs {p0}+")
 
 
-def test_edge_c2_full_batch_vs_oracle(gpu):
+@pytest.mark.parametrize("mode", ["markall", "passes"])
+def test_edge_c2_full_batch_vs_oracle(gpu, mode):
+    """The region walk (mostly duplicates) under both of K2's marking modes."""
     from syzkaller_amd import synth
+    from syzkaller_amd._lib import SYZSIG_DEBUG_EDGE_MARKALL, SYZSIG_DEBUG_EDGE_PASSES
 
     cfg = synth.synth_default()
-    sigs, cs, cnt, comp, prio = _device_edge(gpu, cfg)
+    gpu.eng.set_debug(SYZSIG_DEBUG_EDGE_MARKALL if mode == "markall" else SYZSIG_DEBUG_EDGE_PASSES)
+    try:
+        sigs, cs, cnt, comp, prio = _device_edge(gpu, cfg)
+    finally:
+        gpu.eng.set_debug(0)
     _check_edge_slices(cfg, sigs, cnt, comp)
 
 
