@@ -136,6 +136,14 @@ int syzsig_from_raw(syzsig_ctx* ctx, const uint32_t* raw, uint64_t n, uint8_t pr
  * min(cap, Len) entries and sets *n_out = Len. */
 int syzsig_serialize(syzsig_ctx* ctx, const syzsig_set* s, uint32_t* elems, int8_t* prios,
                      uint64_t cap, uint64_t* n_out);
+/* Serialize of many sets at once (the manager serializes every Poll reply,
+ * manager.go:1049 r.MaxSignal = f.newMaxSignal.Serialize()): one round of
+ * kernels and one copy for all of them.  offs[0..nsets] = the sets' Len
+ * prefix sums (a NULL set is empty); set i's entries land in
+ * elems/prios[offs[i], offs[i+1]).  cap == 0 fills offs only (sizing); a cap
+ * below offs[nsets] is SYZSIG_ERANGE. */
+int syzsig_serialize_batch(syzsig_ctx* ctx, const syzsig_set* const* sets, uint64_t nsets, uint32_t* elems,
+                           int8_t* prios, uint64_t cap, uint64_t* offs);
 /* Deserialize, signal.go:59-71: SYZSIG_ECORRUPT if n_elems != n_prios; NULL
  * when empty; a later duplicate element overwrites an earlier one. */
 int syzsig_deserialize(syzsig_ctx* ctx, const uint32_t* elems, uint64_t n_elems, const int8_t* prios,

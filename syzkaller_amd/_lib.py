@@ -104,6 +104,7 @@ SIGNATURES = {
     "syzsig_capacity": (c_uint64, [_P]),
     "syzsig_from_raw": (c_int, [_P, _P, c_uint64, c_uint8, _PP]),
     "syzsig_serialize": (c_int, [_P, _P, _P, _P, c_uint64, POINTER(c_uint64)]),
+    "syzsig_serialize_batch": (c_int, [_P, _P, c_uint64, _P, _P, c_uint64, _P]),
     "syzsig_deserialize": (c_int, [_P, _P, c_uint64, _P, c_uint64, _PP]),
     "syzsig_deserialize_dev": (c_int, [_P, _P, _P, c_uint64, _PP]),
     "syzsig_diff": (c_int, [_P, _P, _P, _PP]),

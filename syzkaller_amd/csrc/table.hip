@@ -10,6 +10,8 @@
 
 #include "internal.h"
 
+#include <vector>
+
 namespace syz {
 
 // ---------------------------------------------------------------- kernels
@@ -305,6 +307,55 @@ __global__ void k_write_live(const uint64_t* __restrict__ slots, uint64_t nslots
 		if (live && pos + r < cap) {
 			elems[pos + r] = slot_key(s);
 			prios[pos + r] = slot_prio(s);
+		}
+		pos += tot;
+	}
+}
+
+// the batch Serialize: block b of the launch covers chunk (b - blk0) of the
+// set blk_set[b]; one scan over every block's count places each set's
+// entries right after the previous set's (their live counts are their Lens)
+struct SerDesc {
+	const uint64_t* slots;
+	uint64_t nslots, chunk;
+	uint32_t blk0, pad;
+};
+
+__global__ void k_count_live_multi(const SerDesc* __restrict__ d, const uint32_t* __restrict__ blk_set,
+                                   unsigned long long* counts)
+{
+	const SerDesc sd = d[blk_set[blockIdx.x]];
+	const uint64_t lo = (blockIdx.x - sd.blk0) * sd.chunk, hi = min(sd.nslots, lo + sd.chunk);
+	uint64_t c = 0;
+	for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+		c += slot_live(sd.slots[i]);
+	__shared__ unsigned long long part;
+	if (threadIdx.x == 0)
+		part = 0;
+	__syncthreads();
+	c = wave_sum_u64(c);
+	if (lane_id() == 0)
+		atomicAdd(&part, (unsigned long long)c);
+	__syncthreads();
+	if (threadIdx.x == 0)
+		counts[blockIdx.x] = part;
+}
+
+__global__ void k_write_live_multi(const SerDesc* __restrict__ d, const uint32_t* __restrict__ blk_set,
+                                   const unsigned long long* __restrict__ offs, uint32_t* elems, int8_t* prios)
+{
+	const SerDesc sd = d[blk_set[blockIdx.x]];
+	const uint64_t lo = (blockIdx.x - sd.blk0) * sd.chunk, hi = min(sd.nslots, lo + sd.chunk);
+	uint64_t pos = offs[blockIdx.x];
+	for (uint64_t base = lo; base < hi; base += blockDim.x) {
+		const uint64_t i = base + threadIdx.x;
+		const uint64_t sl = i < hi ? sd.slots[i] : 0;
+		const bool live = slot_live(sl);
+		uint32_t tot;
+		const uint32_t r = block_rank(live, &tot);
+		if (live) {
+			elems[pos + r] = slot_key(sl);
+			prios[pos + r] = slot_prio(sl);
 		}
 		pos += tot;
 	}
@@ -662,6 +713,59 @@ int syzsig_serialize(syzsig_ctx* ctx, const syzsig_set* s, uint32_t* elems, int8
 	}
 	SYZ_HIP(hipStreamSynchronize(ctx->stream));
 	*n_out = s->len;
+	return SYZSIG_OK;
+}
+
+int syzsig_serialize_batch(syzsig_ctx* ctx, const syzsig_set* const* sets, uint64_t nsets, uint32_t* elems,
+                           int8_t* prios, uint64_t cap, uint64_t* offs)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !offs || (nsets && !sets))
+		return fail(SYZSIG_EINVAL, "serialize_batch: NULL argument");
+	offs[0] = 0;
+	for (uint64_t i = 0; i < nsets; i++) {
+		SYZ_TRY(set_check_idle(sets[i]));
+		offs[i + 1] = offs[i] + (sets[i] ? sets[i]->len : 0);
+	}
+	const uint64_t total = offs[nsets];
+	if (cap == 0 || total == 0)
+		return SYZSIG_OK;  // the offsets only (sizing), or nothing to write
+	if (!elems || !prios)
+		return fail(SYZSIG_EINVAL, "serialize_batch: NULL output");
+	if (cap < total)
+		return fail(SYZSIG_ERANGE, "serialize_batch: cap below the sets' total Len (offs holds it)");
+	std::vector<SerDesc> desc;
+	std::vector<uint32_t> blk_set;
+	for (uint64_t i = 0; i < nsets; i++) {
+		const syzsig_set* st = sets[i];
+		if (!st || st->len == 0)
+			continue;
+		const uint64_t nslots = st->nslots();
+		const uint32_t nblk = (uint32_t)grid_for(nslots, 256);
+		desc.push_back(SerDesc{st->slots, nslots, (nslots + nblk - 1) / nblk, (uint32_t)blk_set.size(), 0});
+		blk_set.insert(blk_set.end(), nblk, (uint32_t)(desc.size() - 1));
+	}
+	const uint64_t nb = blk_set.size();
+	if (nb >= (1u << 31))
+		return fail(SYZSIG_ERANGE, "serialize_batch: too many sets");
+	void *d_desc, *d_blk, *d_counts, *d_out;
+	SYZ_TRY(ws_get(ctx, 0, desc.size() * sizeof(SerDesc), &d_desc));
+	SYZ_TRY(ws_get(ctx, 1, (nb + 1) * sizeof(unsigned long long), &d_counts));
+	SYZ_TRY(ws_get(ctx, 2, total * 5 + 16, &d_out));
+	SYZ_TRY(ws_get(ctx, 3, nb * sizeof(uint32_t), &d_blk));
+	SYZ_HIP(hipMemcpyAsync(d_desc, desc.data(), desc.size() * sizeof(SerDesc), hipMemcpyHostToDevice, ctx->stream));
+	SYZ_HIP(hipMemcpyAsync(d_blk, blk_set.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+	unsigned long long* counts = (unsigned long long*)d_counts;
+	k_count_live_multi<<<(uint32_t)nb, 256, 0, ctx->stream>>>((const SerDesc*)d_desc, (const uint32_t*)d_blk, counts);
+	k_scan_counts<<<1, 1024, 0, ctx->stream>>>(counts, (uint32_t)nb, counts + nb);
+	uint32_t* de = (uint32_t*)d_out;
+	int8_t* dp = (int8_t*)(de + total);
+	k_write_live_multi<<<(uint32_t)nb, 256, 0, ctx->stream>>>((const SerDesc*)d_desc, (const uint32_t*)d_blk, counts,
+	                                                        de, dp);
+	SYZ_HIP(hipGetLastError());
+	SYZ_HIP(hipMemcpyAsync(elems, de, total * 4, hipMemcpyDeviceToHost, ctx->stream));
+	SYZ_HIP(hipMemcpyAsync(prios, dp, total, hipMemcpyDeviceToHost, ctx->stream));
+	SYZ_HIP(hipStreamSynchronize(ctx->stream));  // (the host vectors above outlive the copies)
 	return SYZSIG_OK;
 }
 

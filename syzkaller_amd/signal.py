@@ -244,6 +244,27 @@ class Serial:
         return Signal(h, eng)
 
 
+def serialize_many(sets, eng=None):
+    """Serialize (signal.go:42-57) of every set in `sets` (Signal objects; a
+    nil one is empty) with one library call (syzsig_serialize_batch): the
+    manager serializes every Poll reply (manager.go:1049).  Returns a Serial
+    per set; their arrays are views of one buffer."""
+    n = len(sets)
+    if n == 0:
+        return []
+    eng = eng or next((x._e for x in sets if x is not None), None) or engine()
+    hs = (ctypes.c_void_p * n)(*[(x.handle.value or 0) if x is not None else 0 for x in sets])
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    check(eng.L.syzsig_serialize_batch(eng.h, hs, n, None, None, 0, _ptr(offs)))
+    tot = int(offs[-1])
+    if tot == 0:
+        return [Serial() for _ in range(n)]
+    elems = np.empty(tot, dtype=np.uint32)
+    prios = np.empty(tot, dtype=np.int8)
+    check(eng.L.syzsig_serialize_batch(eng.h, hs, n, _ptr(elems), _ptr(prios), tot, _ptr(offs)))
+    return [Serial(elems[a:b], prios[a:b]) for a, b in zip(offs[:-1].tolist(), offs[1:].tolist())]
+
+
 def FromRaw(raw, prio, eng=None):
     """signal.go:31-40"""
     eng = eng or engine()
@@ -381,8 +402,5 @@ def manager_poll(max_signal, new_max, polls, eng=None):
             max_signal._h = mh
         for g, s in enumerate(new_max):
             s._h = ctypes.c_void_p(nm[g]) if nm[g] else None
-    out = []
-    for i in range(K):
-        r = Signal(ctypes.c_void_p(rep[i]) if rep[i] else None, eng)
-        out.append(r.Serialize() if not r.is_nil() else Serial())
-    return out
+    reps = [Signal(ctypes.c_void_p(rep[i]) if rep[i] else None, eng) for i in range(K)]
+    return serialize_many(reps, eng)

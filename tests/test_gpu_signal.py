@@ -103,3 +103,40 @@ def test_gpu_deserialize_last_duplicate_wins(gpu):
     e = rng.integers(0, 1000, size=50000).astype(np.uint32)
     p = rng.integers(-128, 128, size=e.size).astype(np.int8)
     assert S.Serial(e, p).Deserialize(gpu.eng).to_dict() == O.deserialize(e, p).to_dict()
+
+
+def test_gpu_serialize_many_vs_serialize(gpu):
+    """syzsig_serialize_batch (the Poll replies' Serialize, manager.go:1049)
+    against one Serialize per set: nil, empty-after-Subtract, small and
+    multi-block sets in one call; set i's entries in [offs[i], offs[i+1])."""
+    import ctypes
+
+    from syzkaller_amd import signal as S
+    from syzkaller_amd._lib import SyzsigError
+
+    rng = np.random.default_rng(7)
+    sets = [None]
+    for n in (1, 5, 300, 70_000, 0, 2_000_000, 17):
+        e = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+        p = rng.integers(-128, 128, n).astype(np.int8)
+        sets.append(S.Serial(e, p).Deserialize(gpu.eng) if n else S.Signal.make(0, gpu.eng))
+    sets.append(None)
+    got = S.serialize_many(sets, gpu.eng)
+    assert len(got) == len(sets)
+    for s, g in zip(sets, got):
+        want = s.Serialize() if s is not None else S.Serial()
+        assert g.Elems.size == want.Elems.size
+        o1, o2 = np.argsort(g.Elems), np.argsort(want.Elems)
+        np.testing.assert_array_equal(g.Elems[o1], want.Elems[o2])
+        np.testing.assert_array_equal(g.Prios[o1], want.Prios[o2])
+    # a cap below the total is refused, with the offsets filled
+    hs = (ctypes.c_void_p * len(sets))(*[(x.handle.value or 0) if x is not None else 0 for x in sets])
+    offs = np.zeros(len(sets) + 1, np.uint64)
+    e = np.empty(10, np.uint32)
+    p = np.empty(10, np.int8)
+    rc = gpu.eng.L.syzsig_serialize_batch(gpu.eng.h, hs, len(sets), e.ctypes.data, p.ctypes.data, 10,
+                                          offs.ctypes.data)
+    assert rc != 0 and int(offs[-1]) == sum(g.Elems.size for g in got)
+    with pytest.raises(SyzsigError):
+        from syzkaller_amd._lib import check
+        check(rc)
