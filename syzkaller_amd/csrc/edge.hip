@@ -140,7 +140,8 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 	// the tail (KS == 1): each wave's pending signals packed, and per wave the
 	// tail's emitted ones by rank
 	constexpr bool kSeq = KS == 1 && kEdgeSeqMax > 0;
-	__shared__ uint32_t s_sig[kSeq ? kLanes : 1];
+	__shared__ __align__(16) uint32_t s_sig[kSeq ? kLanes : 1];
+	__shared__ uint32_t s_th[kSeq ? 32 : 1];  // the tail's window homes
 	__shared__ uint64_t s_pm[kEdgeWaves];
 	const uint32_t lane = lane_id(), w = threadIdx.x >> 6, pos = threadIdx.x;  // pos: place in a sub-chunk
 	uint32_t seq = 0;
@@ -429,12 +430,23 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 								const bool item = lane < npend;
 								const uint32_t sg = item ? s_sig[64 * seg + lane - segbase] : 0;
 								const uint32_t h = sg & (kDedupSize - 1);
-								// earlier pending signals with an overlapping window (distance <= 3)
+								// earlier pending signals with an overlapping window (distance <= 3):
+								// candidates from 32-slot buckets (s_sig is free once gathered: the
+								// wave's LDS operations run in order), then the exact distance
+								static_assert(kSeq ? kLanes == 256 && kEdgeSeqMax <= 32 : true, "tail buckets");
+								reinterpret_cast<uint4*>(s_sig)[lane] = make_uint4(0, 0, 0, 0);
+								const uint32_t bk = h >> 5;
+								if (item) {
+									atomicOr(&s_sig[bk], 1u << lane);
+									s_th[lane] = h;
+								}
+								uint32_t cand = s_sig[(bk + 255) & 255] | s_sig[bk] | s_sig[(bk + 1) & 255];
+								cand = item ? cand & ((1u << lane) - 1) : 0u;
 								uint32_t ovm = 0;
-								for (uint32_t k = 0; k < npend; k++) {
-									const uint32_t hk = __builtin_amdgcn_readlane(h, k);
-									const uint32_t d = (h - hk + 3) & (kDedupSize - 1);
-									ovm |= k < lane && d <= 6 ? 1u << k : 0u;
+								while (cand) {  // (rare: most tails have no two windows within 32 slots)
+									const uint32_t k = __builtin_ctz(cand);
+									cand &= cand - 1;
+									ovm |= ((h - s_th[k] + 3) & (kDedupSize - 1)) <= 6 ? 1u << k : 0u;
 								}
 								uint32_t act = (uint32_t)__ballot(item), em = 0;
 								while (act) {
