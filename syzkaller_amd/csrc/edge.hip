@@ -73,7 +73,7 @@ constexpr uint32_t kEdgeDepthSignals = SYZ_EDGE_DEPTH;
 #endif
 constexpr uint32_t kEdgeKS = SYZ_EDGE_KS;  // signals per lane per chunk
 #ifndef SYZ_EDGE_SEQ
-#define SYZ_EDGE_SEQ 16
+#define SYZ_EDGE_SEQ 32
 #endif
 // a round that leaves at most this many lanes pending hands them to one wave,
 // which runs them through plain dedup in trace order (0: rounds only)
