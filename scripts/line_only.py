@@ -27,6 +27,12 @@ elif which == "poll":
     out = bench.poll_line(dev)
 elif which == "edge":
     import numpy as np
+
+    from syzkaller_amd._lib import SYZSIG_DEBUG_EDGE_MARKALL, SYZSIG_DEBUG_EDGE_PASSES
+
+    mode = os.environ.get("EDGE_MODE", "")  # force K2's marking mode: markall | passes
+    if mode:
+        dev.eng.set_debug(SYZSIG_DEBUG_EDGE_MARKALL if mode == "markall" else SYZSIG_DEBUG_EDGE_PASSES)
     P, C, L = 4096, 64, 4096
     cl = torch.full((P * C,), L, dtype=torch.int32)
     pcs, cs, cl, _ = dev.synth_traces(bench.walk_cfg(WALK), 0, P, C, cl)
