@@ -8,7 +8,8 @@
 // signals (4 per CU: the table bounds residency, so the waves of a program
 // are what fills the SIMDs).  K1 is data-parallel: sig_i = (u32)pc_i ^
 // hash((u32)pc_{i-1}), the previous PC's hash taken from the lane below
-// (across waves through LDS, across chunks from a carry).  K2 is a sequential
+// (across waves through LDS, across chunks from a carry; for all the chunks of
+// a prefetch group under one barrier).  K2 is a sequential
 // state machine, parallelised exactly.  Signal i reads only its 4-slot window
 // {h, h+1, h+2, h+3} (h = sig % 8192) and writes at most one slot of it
 // (insert at the first empty slot, or the forced overwrite at h); a duplicate
@@ -75,6 +76,9 @@ constexpr uint32_t kEdgeKS = SYZ_EDGE_KS;  // signals per lane per chunk
 #ifndef SYZ_EDGE_SEQ
 #define SYZ_EDGE_SEQ 32
 #endif
+#ifndef SYZ_EDGE_GROUP_K1
+#define SYZ_EDGE_GROUP_K1 1
+#endif
 // a round that leaves at most this many lanes pending hands them to one wave,
 // which runs them through plain dedup in trace order (0: rounds only)
 constexpr uint32_t kEdgeSeqMax = SYZ_EDGE_SEQ;
@@ -136,7 +140,11 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 	// marked at least twice (2 KB: four programs still fit a CU's LDS)
 	__shared__ uint32_t fm1[kDedupSize / 32], fm2[kDedupSize / 32];
 	__shared__ __align__(16) uint32_t s_any[2][kEdgeWaves];
-	__shared__ uint32_t s_carry[2][KS][kEdgeWaves];
+	// K1 for a whole prefetch group of kDepth chunks at once (KS == 1): one
+	// barrier exchanges the waves' boundary hashes and cover_check verdicts of
+	// all of them, instead of one per chunk
+	constexpr bool kGroupK1 = KS == 1 && SYZ_EDGE_GROUP_K1;
+	__shared__ uint32_t s_carry[kGroupK1 ? kDepth : 2][KS][kEdgeWaves];
 	// the tail (KS == 1): each wave's pending signals packed, and per wave the
 	// tail's emitted ones by rank
 	constexpr bool kSeq = KS == 1 && kEdgeSeqMax > 0;
@@ -222,12 +230,16 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						buf[u][k] = pcs[min<uint64_t>(start + (uint64_t)(g + u) * kEdgeChunk + k * kLanes + pos, last)];
 			};
 			// chunk q of the call; false once the program aborts
-			auto chunk = [&](const uint64_t (&pcv)[KS], uint32_t q) -> bool {
+			auto chunk = [&](const uint64_t (&pcv)[KS], uint32_t sgv, uint32_t q) -> bool {
 				uint32_t sig[KS], b0[KS], b1[KS], v[KS], wpos[KS];
 				bool pending[KS], emit[KS], writer[KS], blocked[KS];
 				bool bad = false;
+				if constexpr (kGroupK1) {  // (its K1 ran for the whole group: `run`)
+					pending[0] = q * kEdgeChunk + pos < len;
+					sig[0] = sgv;
+				}
 #pragma unroll
-				for (uint32_t k = 0; k < KS; k++) {
+				for (uint32_t k = 0; k < (kGroupK1 ? 0 : KS); k++) {
 					const uint32_t j = q * kEdgeChunk + k * kLanes + pos;
 					pending[k] = j < len;
 					const uint64_t pc = pending[k] ? pcv[k] : 0;
@@ -240,20 +252,23 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						s_carry[q & 1][k][w] = h;
 					b0[k] = (uint32_t)pc;  // (the PC's low half, until the previous hash is known)
 				}
-				if (wg_any(bad, 0))
+				if (!kGroupK1 && wg_any(bad, 0))
 					return false;
 #pragma unroll
 				for (uint32_t k = 0; k < KS; k++) {
-					uint32_t up = sig[k];
-					if (lane == 0)
-						up = w > 0 ? s_carry[q & 1][k][w - 1] : k > 0 ? s_carry[q & 1][k - 1][kEdgeWaves - 1] : carry;
-					sig[k] = b0[k] ^ up;
+					if constexpr (!kGroupK1) {
+						uint32_t up = sig[k];
+						if (lane == 0)
+							up = w > 0 ? s_carry[q & 1][k][w - 1] : k > 0 ? s_carry[q & 1][k - 1][kEdgeWaves - 1] : carry;
+						sig[k] = b0[k] ^ up;
+					}
 					const uint32_t home = sig[k] & (kDedupSize - 1);
 					b0[k] = home >> kBinShift;
 					b1[k] = ((home + 3) & (kDedupSize - 1)) >> kBinShift;
 					emit[k] = false;
 				}
-				carry = s_carry[q & 1][KS - 1][kEdgeWaves - 1];
+				if constexpr (!kGroupK1)
+					carry = s_carry[q & 1][KS - 1][kEdgeWaves - 1];
 				// rounds until no lane is pending (a chunk always has a valid lane, so
 				// the first round needs no test); the test after the last round also
 				// publishes every wave's emit counts for the output below
@@ -530,9 +545,36 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 				return true;
 			};
 			auto run = [&](const uint64_t (&buf)[kDepth][KS], uint32_t g) -> bool {
+				uint32_t sgv[kDepth] = {};
+				if constexpr (kGroupK1) {
+					// sig_i = (u32)pc_i ^ hash((u32)pc_{i-1}) for the group's chunks; a
+					// cover_check failure anywhere in them aborts the call before any
+					// of them runs (the call publishes nothing either way)
+					uint32_t lo[kDepth], badm = 0;
+#pragma unroll
+					for (uint32_t u = 0; u < kDepth; u++) {
+						const bool pend = (g + u) * kEdgeChunk + pos < len;
+						const uint64_t pc = pend ? buf[u][0] : 0;
+						badm |= __ballot(pend && !cover_check(pc)) ? 1u << u : 0u;
+						const uint32_t h = exec_hash((uint32_t)pc);
+						sgv[u] = __shfl_up(h, 1, 64);
+						if (lane == 63)
+							s_carry[u][0][w] = h;
+						lo[u] = (uint32_t)pc;
+					}
+					if (wg_any(badm != 0, 0))
+						return false;
+#pragma unroll
+					for (uint32_t u = 0; u < kDepth; u++) {
+						if (lane == 0)
+							sgv[u] = w > 0 ? s_carry[u][0][w - 1] : u > 0 ? s_carry[u - 1][0][kEdgeWaves - 1] : carry;
+						sgv[u] ^= lo[u];
+					}
+					carry = s_carry[kDepth - 1][0][kEdgeWaves - 1];
+				}
 #pragma unroll
 				for (uint32_t u = 0; u < kDepth; u++)
-					if (g + u < nch && !chunk(buf[u], g + u))
+					if (g + u < nch && !chunk(buf[u], sgv[u], g + u))
 						return false;
 				return true;
 			};
