@@ -544,59 +544,66 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 				}
 				return true;
 			};
-			auto run = [&](const uint64_t (&buf)[kDepth][KS], uint32_t g) -> bool {
-				uint32_t sgv[kDepth] = {};
-				if constexpr (kGroupK1) {
-					// sig_i = (u32)pc_i ^ hash((u32)pc_{i-1}) for the group's chunks; a
-					// cover_check failure anywhere in them aborts the call before any
-					// of them runs (the call publishes nothing either way)
-					uint32_t lo[kDepth], badm = 0;
+			// K1 of a prefetch group (kGroupK1): sig_i = (u32)pc_i ^ hash((u32)pc_{i-1})
+			// for its chunks; a cover_check failure anywhere in them aborts the call
+			// before any of them runs (the call publishes nothing either way)
+			auto k1 = [&](const uint64_t (&buf)[kDepth][KS], uint32_t g, uint32_t (&sgv)[kDepth]) -> bool {
+				uint32_t lo[kDepth], badm = 0;
 #pragma unroll
-					for (uint32_t u = 0; u < kDepth; u++) {
-						const bool pend = (g + u) * kEdgeChunk + pos < len;
-						const uint64_t pc = pend ? buf[u][0] : 0;
-						badm |= __ballot(pend && !cover_check(pc)) ? 1u << u : 0u;
-						const uint32_t h = exec_hash((uint32_t)pc);
-						sgv[u] = __shfl_up(h, 1, 64);
-						if (lane == 63)
-							s_carry[u][0][w] = h;
-						lo[u] = (uint32_t)pc;
-					}
-					if (wg_any(badm != 0, 0))
-						return false;
-#pragma unroll
-					for (uint32_t u = 0; u < kDepth; u++) {
-						if (lane == 0)
-							sgv[u] = w > 0 ? s_carry[u][0][w - 1] : u > 0 ? s_carry[u - 1][0][kEdgeWaves - 1] : carry;
-						sgv[u] ^= lo[u];
-					}
-					carry = s_carry[kDepth - 1][0][kEdgeWaves - 1];
+				for (uint32_t u = 0; u < kDepth; u++) {
+					const bool pend = (g + u) * kEdgeChunk + pos < len;
+					const uint64_t pc = pend ? buf[u][0] : 0;
+					badm |= __ballot(pend && !cover_check(pc)) ? 1u << u : 0u;
+					const uint32_t h = exec_hash((uint32_t)pc);
+					sgv[u] = __shfl_up(h, 1, 64);
+					if (lane == 63)
+						s_carry[u][0][w] = h;
+					lo[u] = (uint32_t)pc;
 				}
+				if (wg_any(badm != 0, 0))
+					return false;
 #pragma unroll
-				for (uint32_t u = 0; u < kDepth; u++)
-					if (g + u < nch && !chunk(buf[u], sgv[u], g + u))
-						return false;
+				for (uint32_t u = 0; u < kDepth; u++) {
+					if (lane == 0)
+						sgv[u] = w > 0 ? s_carry[u][0][w - 1] : u > 0 ? s_carry[u - 1][0][kEdgeWaves - 1] : carry;
+					sgv[u] ^= lo[u];
+				}
+				carry = s_carry[kDepth - 1][0][kEdgeWaves - 1];
 				return true;
 			};
-			uint64_t ba[kDepth][KS], bb[kDepth][KS];
-			fetch(ba, 0);
-			for (uint32_t g = 0;;) {
-				fetch(bb, g + kDepth);
-				if (!run(ba, g)) {
-					aborted = true;
-					break;
+			{
+				auto run = [&](const uint64_t (&buf)[kDepth][KS], uint32_t g) -> bool {
+					uint32_t sgv[kDepth] = {};
+					if constexpr (kGroupK1) {
+						if (!k1(buf, g, sgv))
+							return false;
+					}
+#pragma unroll
+					for (uint32_t u = 0; u < kDepth; u++)
+						if (g + u < nch && !chunk(buf[u], sgv[u], g + u))
+							return false;
+					return true;
+				};
+				uint64_t ba[kDepth][KS], bb[kDepth][KS];
+				fetch(ba, 0);
+				for (uint32_t g = 0;;) {
+					fetch(bb, g + kDepth);
+					if (!run(ba, g)) {
+						aborted = true;
+						break;
+					}
+					g += kDepth;
+					if (g >= nch)
+						break;
+					fetch(ba, g + kDepth);
+					if (!run(bb, g)) {
+						aborted = true;
+						break;
+					}
+					g += kDepth;
+					if (g >= nch)
+						break;
 				}
-				g += kDepth;
-				if (g >= nch)
-					break;
-				fetch(ba, g + kDepth);
-				if (!run(bb, g)) {
-					aborted = true;
-					break;
-				}
-				g += kDepth;
-				if (g >= nch)
-					break;
 			}
 			if (aborted) {
 				done = c - cb;
