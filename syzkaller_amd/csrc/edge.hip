@@ -328,8 +328,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						for (uint32_t k = 0; k < KS; k++) {
 							if (mark_win[k]) {
 								atomicMax(&stamp[b0[k]], v[k]);
-								if (wb1[k])
-									atomicMax(&stamp[b1[k]], v[k]);
+								atomicMax(&stamp[wb1[k] ? b1[k] : b0[k]], v[k]);  // (twice on b0: the same max)
 								// the slots themselves, counted up to two (a blocked lane also its
 								// decision slot: a later lane must not write what it will read again)
 								const uint32_t hs = sig[k] & (kDedupSize - 1), off = hs & 31;
@@ -337,8 +336,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 								const uint32_t wa = hs >> 5, wbw = (wa + 1) & (kDedupSize / 32 - 1);
 								const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
 								const uint32_t oa = atomicOr(&fm1[wa], lo);
-								if (oa & lo)
-									atomicOr(&fm2[wa], oa & lo);
+								atomicOr(&fm2[wa], oa & lo);  // (0: nothing; no branch)
 								if (hi) {
 									const uint32_t ob = atomicOr(&fm1[wbw], hi);
 									if (ob & hi)
