@@ -69,6 +69,12 @@ double syzsig_ctx_last_ms(syzsig_ctx* ctx);
  * events).  The achievable-bandwidth companion of the bench's rooflines
  * (SURVEY.md 8(d)); not part of pkg/signal.  Synchronises. */
 int syzsig_copy_bw_dev(syzsig_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes, double* ms);
+/* Page-locked host memory (hipHostMalloc): host arrays handed to the library
+ * from it are uploaded by DMA without a staging copy (the manager's Poll
+ * batch builds its Serials there).  *out = NULL for 0 bytes; free with
+ * syzsig_host_free (NULL is a no-op). */
+int syzsig_host_alloc(syzsig_ctx* ctx, uint64_t bytes, void** out);
+int syzsig_host_free(syzsig_ctx* ctx, void* p);
 /* Large-batch triage path selection (tests and tuning; results never depend on it):
  * mode 0 = per-call probe path only, 1 = aggregation path for runs of >= 2^20
  * records (default), 2 = aggregation path always; parts = fixed partition

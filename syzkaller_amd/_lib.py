@@ -91,6 +91,8 @@ SIGNATURES = {
     "syzsig_ctx_set_debug": (c_int, [_P, ctypes.c_uint32]),
     "syzsig_ctx_last_ms": (ctypes.c_double, [_P]),
     "syzsig_copy_bw_dev": (c_int, [_P, _P, _P, c_uint64, POINTER(ctypes.c_double)]),
+    "syzsig_host_alloc": (c_int, [_P, c_uint64, POINTER(_P)]),
+    "syzsig_host_free": (c_int, [_P, _P]),
     "syzsig_set_make": (c_int, [_P, c_uint64, _PP]),
     "syzsig_set_free": (None, [_P]),
     "syzsig_set_clone": (c_int, [_P, _P, _PP]),

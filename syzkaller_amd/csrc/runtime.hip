@@ -265,6 +265,29 @@ int syzsig_copy_bw_dev(syzsig_ctx* ctx, void* d_dst, const void* d_src, uint64_t
 	return rc;
 }
 
+int syzsig_host_alloc(syzsig_ctx* ctx, uint64_t bytes, void** out)
+{
+	SYZ_LOCK(ctx);
+	if (!ctx || !out)
+		return syz::fail(SYZSIG_EINVAL, "host_alloc: NULL argument");
+	*out = nullptr;
+	if (bytes == 0)
+		return SYZSIG_OK;
+	if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+		*out = nullptr;
+		return syz::fail(SYZSIG_ENOMEM, "host_alloc: hipHostMalloc failed");
+	}
+	return SYZSIG_OK;
+}
+
+int syzsig_host_free(syzsig_ctx* ctx, void* p)
+{
+	SYZ_LOCK(ctx);
+	if (p && hipHostFree(p) != hipSuccess)
+		return syz::fail(SYZSIG_EIO, "host_free: hipHostFree failed");
+	return SYZSIG_OK;
+}
+
 int syzsig_ctx_set_timing(syzsig_ctx* ctx, int enable)
 {
 	SYZ_LOCK(ctx);

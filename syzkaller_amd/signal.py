@@ -33,6 +33,24 @@ class Engine:
         check(self.L.syzsig_ctx_create(int(device), ctypes.byref(h)))
         self.h = h
         self.device = int(device)
+        self._pin, self._pin_bytes = None, 0  # page-locked staging (syzsig_host_alloc)
+
+    def staging(self, nbytes):
+        """A page-locked host buffer of at least nbytes (uint8 numpy view),
+        reused across calls: arrays built in it upload by DMA.  Its contents
+        are the caller's until the next staging() call."""
+        if nbytes > self._pin_bytes:
+            self._free_staging()
+            want = max(int(nbytes), 2 * self._pin_bytes, 1 << 20)
+            p = ctypes.c_void_p()
+            check(self.L.syzsig_host_alloc(self.h, want, ctypes.byref(p)))
+            self._pin, self._pin_bytes = p, want
+        return np.ctypeslib.as_array(ctypes.cast(self._pin, ctypes.POINTER(ctypes.c_uint8)), shape=(self._pin_bytes,))
+
+    def _free_staging(self):
+        if self._pin is not None and self.h:
+            self.L.syzsig_host_free(self.h, self._pin)
+        self._pin, self._pin_bytes = None, 0
 
     def set_stream(self, stream_handle):
         check(self.L.syzsig_ctx_set_stream(self.h, ctypes.c_void_p(stream_handle)))
@@ -47,6 +65,7 @@ class Engine:
 
     def close(self):
         if self.h:
+            self._free_staging()
             self.L.syzsig_ctx_destroy(self.h)
             self.h = None
 
@@ -387,8 +406,16 @@ def manager_poll(max_signal, new_max, polls, eng=None):
             raise _lib.CorruptedSerial(_lib.SYZSIG_ECORRUPT, "corrupted Serial")  # signal.go:60-62
     off = np.zeros(K + 1, dtype=np.uint64)
     np.cumsum(lens, out=off[1:])
-    elems = np.concatenate([np.asarray(s.Elems, np.uint32) for _, s in polls]) if off[-1] else np.empty(0, np.uint32)
-    prios = np.concatenate([np.asarray(s.Prios, np.int8) for _, s in polls]) if off[-1] else np.empty(0, np.int8)
+    # the Serials back to back in page-locked memory (the upload is a DMA)
+    n = int(off[-1])
+    if n:
+        buf = eng.staging(5 * n + 64)
+        elems = buf[: 4 * n].view(np.uint32)
+        prios = buf[4 * n: 5 * n].view(np.int8)
+        np.concatenate([np.asarray(s.Elems, np.uint32) for _, s in polls], out=elems)
+        np.concatenate([np.asarray(s.Prios, np.int8) for _, s in polls], out=prios)
+    else:
+        elems, prios = np.empty(0, np.uint32), np.empty(0, np.int8)
     nm = (ctypes.c_void_p * max(F, 1))(*[s.handle.value or 0 for s in new_max])
     rep = (ctypes.c_void_p * max(K, 1))()
     mh = ctypes.c_void_p(max_signal.handle.value or 0)
