@@ -423,7 +423,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 							// dedup() (executor.h:692-706) on the table as it stands is the
 							// sequential one.  Passes until none is left; the wave's LDS
 							// operations run in order, so a pass sees the previous one's stores.
-#ifdef SYZ_EDGE_TAIL_DROP  // timing only (results wrong): the tail skipped
+#if defined(SYZ_EXPERIMENTS) && defined(SYZ_EDGE_TAIL_DROP)  // timing only (results wrong): the tail skipped
 							if (w == 0 && lane < kEdgeWaves)
 								s_pm[lane] = 0;
 							if (false) {
