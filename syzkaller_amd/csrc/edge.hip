@@ -147,7 +147,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 	__shared__ uint32_t s_carry[kGroupK1 ? kDepth : 2][KS][kEdgeWaves];
 	// the tail (KS == 1): each wave's pending signals packed, and per wave the
 	// tail's emitted ones by rank
-	constexpr bool kSeq = KS == 1 && kEdgeSeqMax > 0;
+	constexpr bool kSeq = KS == 1 && W == 4 && kEdgeSeqMax > 0;  // (the tail assumes 256 lanes)
 	__shared__ __align__(16) uint32_t s_sig[kSeq ? kLanes : 1];
 	__shared__ uint32_t s_th[kSeq ? 32 : 1];  // the tail's window homes
 	__shared__ uint64_t s_pm[kEdgeWaves];
