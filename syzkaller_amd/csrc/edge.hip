@@ -328,7 +328,8 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						for (uint32_t k = 0; k < KS; k++) {
 							if (mark_win[k]) {
 								atomicMax(&stamp[b0[k]], v[k]);
-								atomicMax(&stamp[wb1[k] ? b1[k] : b0[k]], v[k]);  // (twice on b0: the same max)
+								if (wb1[k])  // (rare on a full table: a branch, not a second atomic)
+									atomicMax(&stamp[b1[k]], v[k]);
 								// the slots themselves, counted up to two (a blocked lane also its
 								// decision slot: a later lane must not write what it will read again)
 								const uint32_t hs = sig[k] & (kDedupSize - 1), off = hs & 31;
@@ -362,7 +363,8 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 							// one; the earliest pending lane is never blocked)
 							const uint32_t fb = 1u << (wpos[k] & 31);
 							const bool mine = win_marked[k];  // (its marks include its decision slot)
-							const uint32_t fw = mine ? fm2[wpos[k] >> 5] : fm1[wpos[k] >> 5];
+							// (mark-all: every pending lane marked its decision slot)
+							const uint32_t fw = ma || mine ? fm2[wpos[k] >> 5] : fm1[wpos[k] >> 5];
 							blocked[k] = pending[k] && stamp[dbin[k]] > v[k] && (fw & fb);
 							mark_win[k] = blocked[k] && !win_marked[k];
 							win_marked[k] = win_marked[k] || mark_win[k];
