@@ -134,7 +134,15 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 	using G = EdgeGeom<W, KS>;
 	constexpr uint32_t kEdgeWaves = W, kLanes = G::kLanes, kEdgeChunk = G::kChunk, kEpochMax = G::kEpochMax;
 	constexpr uint32_t kDepth = G::kDepth;
-	__shared__ uint32_t table[kDedupSize];
+	// (+ a mirror of slots 0..2 past the end: a window reads h..h+3 without
+	// wrapping, two ds_read2 instead of four reads; every store goes through
+	// tstore)
+	__shared__ __align__(16) uint32_t table[kDedupSize + 4];
+	auto tstore = [&](uint32_t slot, uint32_t val) {
+		table[slot] = val;
+		if (slot < 3)
+			table[kDedupSize + slot] = val;
+	};
 	__shared__ uint32_t stamp[kBins];
 	// per-slot marks of the current round: fm1 = marked at least once, fm2 =
 	// marked at least twice (2 KB: four programs still fit a CU's LDS)
@@ -191,7 +199,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 			continue;
 		}
 		// fresh table per program (common_linux.h:1995-2030: fork zeroes it)
-		for (uint32_t i = threadIdx.x; i < kDedupSize / 4; i += kLanes)
+		for (uint32_t i = threadIdx.x; i < kDedupSize / 4 + 1; i += kLanes)
 			reinterpret_cast<uint4*>(table)[i] = make_uint4(0, 0, 0, 0);
 		for (uint32_t i = threadIdx.x; i < kBins; i += kLanes)
 			stamp[i] = 0;
@@ -289,7 +297,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						uint32_t eqm = 0, zm = 0;
 #pragma unroll
 						for (uint32_t i = 0; i < 4; i++) {
-							const uint32_t t = table[(sig[k] + i) & (kDedupSize - 1)];
+							const uint32_t t = table[(sig[k] & (kDedupSize - 1)) + i];
 							eqm |= (uint32_t)(t == sig[k]) << i;
 							zm |= (uint32_t)(t == 0) << i;
 						}
@@ -390,7 +398,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 					for (uint32_t k = 0; k < KS; k++) {
 						const bool fin_w = pending[k] && !blocked[k] && writer[k];
 						if (fin_w)
-							table[wpos[k]] = sig[k];
+							tstore(wpos[k], sig[k]);
 						emit[k] = emit[k] || fin_w;
 						pending[k] = pending[k] && blocked[k];
 						any_pending |= pending[k];
@@ -471,7 +479,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 										uint32_t first = 4, tf = 0;
 #pragma unroll
 										for (int q = 3; q >= 0; q--) {
-											const uint32_t t = table[(h + q) & (kDedupSize - 1)];
+											const uint32_t t = table[h + q];
 											if (t == sg || t == 0) {
 												first = q;
 												tf = t;
@@ -479,7 +487,7 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 										}
 										wr = first == 4 || tf != sg;
 										if (wr)
-											table[(h + (first & 3)) & (kDedupSize - 1)] = sg;
+											tstore((h + (first & 3)) & (kDedupSize - 1), sg);
 									}
 									em |= (uint32_t)__ballot(wr);
 									act &= ~(uint32_t)__ballot(go);
