@@ -95,7 +95,11 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
  * overflow them and take the redo with counted cells.
  * SYZSIG_DEBUG_EDGE_MARKALL / SYZSIG_DEBUG_EDGE_PASSES = syzsig_edge_derive_dev
  * runs the dedup rounds with one marking pass / with marking passes, instead
- * of choosing from the previous launch's duplicate rate. */
+ * of choosing from the previous launch's duplicate rate.
+ * Fault injection (an error, never a wrong result):
+ * SYZSIG_DEBUG_POLL_FAIL = the sequential Poll loop (syzsig_manager_poll_batch's
+ * exact fallback) fails with SYZSIG_EIO before its last poll, so tests can
+ * check that a failed batch leaves every set as it was. */
 #define SYZSIG_DEBUG_FIN_DEFER 32u
 #define SYZSIG_DEBUG_MIN_ATOMIC 64u
 #define SYZSIG_DEBUG_EXACT_CELLS 128u
@@ -103,6 +107,7 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
 #define SYZSIG_DEBUG_RECS_GATE 512u
 #define SYZSIG_DEBUG_EDGE_MARKALL 1024u
 #define SYZSIG_DEBUG_EDGE_PASSES 2048u
+#define SYZSIG_DEBUG_POLL_FAIL 4096u
 int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
 
 /* ---- pkg/signal/signal.go ---- */

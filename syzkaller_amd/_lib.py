@@ -23,6 +23,7 @@ SYZSIG_DEBUG_CAP_SPILL = 256
 SYZSIG_DEBUG_RECS_GATE = 512
 SYZSIG_DEBUG_EDGE_MARKALL = 1024
 SYZSIG_DEBUG_EDGE_PASSES = 2048
+SYZSIG_DEBUG_POLL_FAIL = 4096
 
 
 class SyzsigError(RuntimeError):

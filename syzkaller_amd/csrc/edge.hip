@@ -417,9 +417,18 @@ __global__ __launch_bounds__(64 * W) void k_edge_dedup(const uint64_t* __restric
 						}
 						first_round = false;
 						if (ma)
-							clear_marks();  // (ordered before the next chunk's marks by its first barrier)
-						if (!more)
+							clear_marks();
+						if (!more) {
+							// The clear must land before any wave marks again.  The next
+							// chunk of the same prefetch group starts marking without a
+							// barrier of its own (K1 ran for the whole group), so a fast
+							// wave could otherwise OR its marks into words a slow wave is
+							// still zeroing.  (Rare on the global walk: a chunk leaves no
+							// lane pending after its first round.)
+							if (ma)
+								lds_barrier();
 							return 0;
+						}
 						uint32_t npend = 0;
 #pragma unroll
 						for (uint32_t i = 0; i < kEdgeWaves; i++)

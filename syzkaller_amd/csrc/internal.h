@@ -73,6 +73,8 @@ struct Workspace {
 constexpr uint32_t kDebugResultPreserving =
     SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL |
     SYZSIG_DEBUG_RECS_GATE | SYZSIG_DEBUG_EDGE_MARKALL | SYZSIG_DEBUG_EDGE_PASSES;
+// ... and those a product build accepts: the above plus fault injection
+constexpr uint32_t kDebugAccepted = kDebugResultPreserving | SYZSIG_DEBUG_POLL_FAIL;
 
 // capped cells of the aggregation path (agg.hip): default slack, in standard deviations
 constexpr float kCapSdDefault = 6.0f;

@@ -29,6 +29,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <chrono>
+
 #include "internal.h"
 
 namespace syz {
@@ -294,40 +296,6 @@ static uint64_t pow2_ge(uint64_t x)
 
 using namespace syz;
 
-// The reference loop itself (manager.go:1027-1052), one poll after the other
-// over the set ops: the exact path for a batch whose entries crowd one element
-// partition past kRpGroupCap (a hot element polled thousands of times).
-static int poll_sequential(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_max, const uint32_t* poll_fuzzer,
-                           const uint64_t* poll_off, const uint32_t* elems, const int8_t* prios, uint32_t npolls,
-                           uint32_t nfuzzers, syzsig_set** replies)
-{
-	for (uint32_t i = 0; i < npolls; i++) {
-		const uint32_t f = poll_fuzzer[i];
-		const uint64_t a = poll_off[i], z = poll_off[i + 1];
-		syzsig_set *d = nullptr, *nm = nullptr;
-		SYZ_TRY(syzsig_deserialize(ctx, elems + a, z - a, prios + a, z - a, &d));
-		const int rc = syzsig_diff(ctx, *max_signal, d, &nm);
-		syzsig_set_free(d);
-		SYZ_TRY(rc);
-		if (!syzsig_empty(nm)) {
-			int r = syzsig_merge(ctx, max_signal, nm);
-			for (uint32_t g = 0; g < nfuzzers && r == SYZSIG_OK; g++)
-				if (g != f)
-					r = syzsig_merge(ctx, &new_max[g], nm);
-			if (r != SYZSIG_OK) {
-				syzsig_set_free(nm);
-				return r;
-			}
-		}
-		syzsig_set_free(nm);
-		if (!syzsig_empty(new_max[f])) {
-			replies[i] = new_max[f];
-			new_max[f] = nullptr;
-		}
-	}
-	return SYZSIG_OK;
-}
-
 // Sets this call made, freed again if it fails before the commit.
 struct PollFresh {
 	std::vector<syzsig_set*> sets;
@@ -337,6 +305,79 @@ struct PollFresh {
 			syzsig_set_free(x);
 	}
 };
+
+// The reference loop itself (manager.go:1027-1052), one poll after the other
+// over the set ops: the exact path for a batch whose entries crowd one element
+// partition past kRpGroupCap (a hot element polled thousands of times).
+// All or nothing, like the batched path: the loop runs on clones of
+// maxSignal and of every fuzzer's newMaxSignal, and only a loop that ran to
+// the end swaps them in and hands out the replies; on any error the clones
+// and the replies made so far are freed and the caller's sets are untouched.
+static int poll_sequential(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_max, const uint32_t* poll_fuzzer,
+                           const uint64_t* poll_off, const uint32_t* elems, const int8_t* prios, uint32_t npolls,
+                           uint32_t nfuzzers, syzsig_set** replies)
+{
+	// (the set ops below record the context's own events: this path's
+	// last_ms is host wall time over the loop, the stream drained at its end)
+	const auto t0 = std::chrono::steady_clock::now();
+	PollFresh work;  // clones and replies, freed unless the loop completes
+	syzsig_set* ms = nullptr;
+	SYZ_TRY(syzsig_set_clone(ctx, *max_signal, &ms));
+	if (ms)
+		work.sets.push_back(ms);
+	std::vector<syzsig_set*> nm(nfuzzers, nullptr), rep(npolls, nullptr);
+	for (uint32_t g = 0; g < nfuzzers; g++) {
+		SYZ_TRY(syzsig_set_clone(ctx, new_max[g], &nm[g]));
+		if (nm[g])
+			work.sets.push_back(nm[g]);
+	}
+	for (uint32_t i = 0; i < npolls; i++) {
+		if ((ctx->agg_dbg & SYZSIG_DEBUG_POLL_FAIL) && i + 1 == npolls && i > 0)
+			return fail(SYZSIG_EIO, "manager_poll_batch: injected failure (SYZSIG_DEBUG_POLL_FAIL)");
+		const uint32_t f = poll_fuzzer[i];
+		const uint64_t a = poll_off[i], z = poll_off[i + 1];
+		syzsig_set* d = nullptr;
+		SYZ_TRY(syzsig_deserialize(ctx, elems + a, z - a, prios + a, z - a, &d));
+		PollFresh nw;  // newMax of this poll, freed at the end of the iteration
+		nw.sets.push_back(nullptr);
+		const int rc = syzsig_diff(ctx, ms, d, &nw.sets[0]);
+		syzsig_set_free(d);
+		SYZ_TRY(rc);
+		if (!syzsig_empty(nw.sets[0])) {
+			syzsig_set* const ms0 = ms;
+			SYZ_TRY(syzsig_merge(ctx, &ms, nw.sets[0]));
+			if (!ms0)
+				work.sets.push_back(ms);  // Merge allocated a nil maxSignal
+			for (uint32_t g = 0; g < nfuzzers; g++) {
+				if (g == f)
+					continue;
+				syzsig_set* const n0 = nm[g];
+				SYZ_TRY(syzsig_merge(ctx, &nm[g], nw.sets[0]));
+				if (!n0)
+					work.sets.push_back(nm[g]);
+			}
+		}
+		if (!syzsig_empty(nm[f])) {  // the reply takes the fuzzer's set (the clone is in work.sets)
+			rep[i] = nm[f];
+			nm[f] = nullptr;
+		}
+	}
+	// commit: nothing below fails
+	work.sets.clear();
+	syzsig_set_free(*max_signal);
+	*max_signal = ms;
+	for (uint32_t g = 0; g < nfuzzers; g++) {
+		syzsig_set_free(new_max[g]);
+		new_max[g] = nm[g];
+	}
+	for (uint32_t i = 0; i < npolls; i++)
+		replies[i] = rep[i];
+	if (ctx->timing) {
+		SYZ_HIP(hipStreamSynchronize(ctx->stream));
+		ctx->last_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+	}
+	return SYZSIG_OK;
+}
 
 extern "C" int syzsig_manager_poll_batch(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set** new_max,
                                          uint32_t nfuzzers, const uint32_t* poll_fuzzer, const uint64_t* poll_off,

@@ -145,7 +145,7 @@ int syzsig_ctx_create(int device, syzsig_ctx** out)
 		// timing-only bits (skipped merges, dropped records) exist only in an
 		// experiment build (make exp EXPFLAGS=-DSYZ_EXPERIMENTS): a stray variable
 		// can select the result-preserving debug paths and nothing else
-		c->agg_dbg &= syz::kDebugResultPreserving;
+		c->agg_dbg &= syz::kDebugAccepted;
 #endif
 	}
 #ifdef SYZ_EXPERIMENTS
@@ -225,7 +225,7 @@ int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags)
 	SYZ_LOCK(ctx);
 	if (!ctx)
 		return syz::fail(SYZSIG_EINVAL, "ctx_set_debug: ctx is NULL");
-	ctx->agg_dbg = flags & syz::kDebugResultPreserving;
+	ctx->agg_dbg = flags & syz::kDebugAccepted;
 	return SYZSIG_OK;
 }
 

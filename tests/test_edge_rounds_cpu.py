@@ -276,3 +276,65 @@ def test_rounds_zero_writer_verdict_case():
     got, _ = round_chunk(Tp, sigs)
     assert got == [seq_dedup(Ts, s) for s in sigs] == [True] * 7
     assert Tp == Ts
+
+
+def clear_race_trace(nprog, nchunks=16, seed=0):
+    """Programs of one call whose 256-signal chunks alternate between a chunk
+    that every lane finishes in its first round with nothing left pending
+    (homes 32 apart: disjoint windows, no shared marks) and a chunk of
+    colliding pairs (lanes 2j and 2j+1 share a home: the second is blocked).
+    In edge.hip's mark-all mode the first kind leaves its round through the
+    `!more` path, and the next chunk of the same prefetch group marks with no
+    K1 barrier in front of it: the ADVICE round-5 race of the mark clear.
+    Returns (pcs, call_start, call_len, prog_call) in the golden layout."""
+    rng = np.random.default_rng(seed)
+    n = nchunks * 256
+
+    def vhash(a):  # exec_hash over a uint64 array of u32 values
+        a = (a ^ 61) ^ (a >> 16)
+        a = (a + (a << 3)) & 0xFFFFFFFF
+        a ^= a >> 4
+        a = (a * 0x27D4EB2D) & 0xFFFFFFFF
+        return a ^ (a >> 15)
+
+    pcs = np.zeros((nprog, n), np.uint64)
+    prev = np.zeros(nprog, np.uint64)
+    for q in range(nchunks):
+        base = rng.integers(0, M, nprog).astype(np.uint64)
+        for i in range(256):
+            home = (base + 32 * (i if q % 2 == 0 else i // 2)) % M
+            lo = np.zeros(nprog, np.uint64)
+            todo = np.ones(nprog, bool)
+            while todo.any():  # a signal with this home whose PC passes cover_check
+                k = int(todo.sum())
+                sig = (rng.integers(1, 1 << 19, k).astype(np.uint64) << 13) | home[todo]
+                cand = sig ^ prev[todo]
+                ok = (cand >= 0x80000000) & (cand < 0xFF000000)
+                idx = np.flatnonzero(todo)[ok]
+                lo[idx] = cand[ok]
+                todo[idx] = False
+            pcs[:, q * 256 + i] = np.uint64(0xFFFFFFFF00000000) | lo
+            prev = vhash(lo)
+    pcs = pcs.reshape(-1)
+    cs = np.arange(nprog, dtype=np.uint64) * n
+    cl = np.full(nprog, n, np.uint32)
+    return pcs, cs, cl, np.arange(nprog + 1, dtype=np.uint32)
+
+
+def test_clear_race_trace_shape():
+    """The trace clear_race_trace builds does what its GPU test needs: in the
+    mark-all mode, even chunks end after one round with no lane pending, odd
+    chunks leave lanes pending; and the rounds still equal sequential dedup."""
+    pcs, cs, cl, pc = clear_race_trace(2, nchunks=6, seed=3)
+    for p in range(2):
+        Tp, Ts = [0] * M, [0] * M
+        trace = pcs[int(cs[p]): int(cs[p]) + int(cl[p])].tolist()
+        prev, sigs = 0, []
+        for x in trace:
+            sigs.append((x & 0xFFFFFFFF) ^ prev)
+            prev = exec_hash(x & 0xFFFFFFFF)
+        for q, c0 in enumerate(range(0, len(sigs), 256)):
+            ch = sigs[c0: c0 + 256]
+            got, rounds = round_chunk(Tp, ch, seq_max=0, mark_all=True)
+            assert got == [seq_dedup(Ts, s) for s in ch]
+            assert (rounds == 1) == (q % 2 == 0), (p, q, rounds)

@@ -90,3 +90,21 @@ def test_edge_rejects_oversized_call(gpu):
     pcs = np.full(n, 0xFFFFFFFF81000000, np.uint64)
     with pytest.raises(SyzsigError):
         _run(gpu, pcs, np.array([0], np.uint64), np.array([n], np.uint32), np.array([0, 1], np.uint32))
+
+
+@pytest.mark.parametrize("mode", ["markall"], indirect=True)
+def test_edge_markall_clear_after_one_round_chunks(gpu, mode):
+    """in the mark-all mode a chunk that leaves no lane
+    pending after its first round clears its slot marks and returns with no
+    barrier behind the clear, while the next chunk of the same prefetch group
+    marks with no K1 barrier in front of it.  The trace alternates such chunks
+    with chunks of colliding pairs (whose lost marks would let a blocked lane
+    write), over 1024 programs so many waves interleave; bit-exact against the
+    oracle (which the CPU test pins to the round restatement's shape)."""
+    from tests.test_edge_rounds_cpu import clear_race_trace
+
+    pcs, cs, cl, pidx = clear_race_trace(1024, nchunks=16, seed=11)
+    exp = O.exec_batch(pcs, cs, cl, pidx)
+    for _ in range(3):
+        out = _run(gpu, pcs, cs, cl, pidx)
+        _check(*exp, cs, *out)

@@ -98,3 +98,36 @@ def test_poll_batch_sequential_path_vs_oracle(gpu, case):
     assert ms.to_dict() == oms.to_dict()
     for g in range(F):
         assert (nm[g].to_dict() if not nm[g].is_nil() else {}) == onm[g].to_dict(), f"fuzzer {g}"
+
+
+def test_poll_batch_sequential_failure_leaves_sets(gpu):
+    """the sequential fallback is all or nothing like
+    the batched path -- a failure before its last poll (injected,
+    SYZSIG_DEBUG_POLL_FAIL) leaves maxSignal and every fuzzer's newMaxSignal
+    as they were (nil ones nil), and hands out no reply."""
+    from syzkaller_amd import signal as S
+    from syzkaller_amd._lib import SYZSIG_DEBUG_POLL_FAIL, SYZSIG_DEBUG_RECS_GATE, SyzsigError
+
+    rng = np.random.default_rng(5)
+    F, U, K = 4, 3000, 12
+    m0 = _serial(rng, 800, U, dup=False)
+    pre = [None if g % 2 == 0 else _serial(rng, 40, U, dup=False) for g in range(F)]
+    polls = [(int(rng.integers(0, F)), S.Serial(*_serial(rng, 200, U))) for _ in range(K)]
+    ms = S.Serial(*m0).Deserialize(gpu.eng)
+    nm = [S.Serial(*p).Deserialize(gpu.eng) if p is not None else S.Signal(None, gpu.eng) for p in pre]
+    before = (ms.to_dict(), [None if s.is_nil() else s.to_dict() for s in nm])
+    gpu.eng.set_debug(SYZSIG_DEBUG_RECS_GATE | SYZSIG_DEBUG_POLL_FAIL)
+    try:
+        with pytest.raises(SyzsigError):
+            S.manager_poll(ms, nm, polls, gpu.eng)
+    finally:
+        gpu.eng.set_debug(0)
+    assert (ms.to_dict(), [None if s.is_nil() else s.to_dict() for s in nm]) == before
+    # and the same batch then goes through, against the oracle
+    replies = S.manager_poll(ms, nm, polls, gpu.eng)
+    oms = O.deserialize(*m0)
+    onm = [O.deserialize(*p) if p is not None else O.OSig() for p in pre]
+    for i, (f, ser) in enumerate(polls):
+        re, rp = O.poll(oms, onm, f, (np.asarray(ser.Elems), np.asarray(ser.Prios)))
+        assert dict(zip(replies[i].Elems.tolist(), replies[i].Prios.tolist())) == dict(zip(re.tolist(), rp.tolist()))
+    assert ms.to_dict() == oms.to_dict()
