@@ -223,7 +223,37 @@ def cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, calls_per_prog, target_s, t
     return out
 
 
-def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
+def minimize_cpu(off, elems, prios, target_s):
+    """Minimize's CPU leg: the oracle (plain-C restatement of
+    pkg/signal/signal.go:138-166: sort by Len desc, then the per-element
+    strictly-greater replacement over a Go-map-like hash) on one core, over
+    the first S contexts of the same corpus (a smaller corpus of the same
+    length and element distribution), S calibrated to ~target_s."""
+    from oracle import oracle as O
+
+    h_off = off.cpu().numpy().view(np.uint64)
+    n = h_off.size - 1
+
+    def run(k):
+        z = int(h_off[k])
+        e = elems[:z].cpu().numpy().view(np.uint32)
+        p = prios[:z].cpu().numpy().view(np.int8)
+        t = time.perf_counter()
+        O.minimize(h_off[: k + 1], e, p)
+        return z, time.perf_counter() - t
+
+    k = min(n, 2000)
+    z, dt = run(k)
+    est = max(1, min(n, int(k * target_s / max(dt, 1e-3))))
+    if est > k:
+        k = est
+        z, dt = run(k)
+    return {"value": z / dt, "unit": "entries/s", "cores": 1, "kind": "port", "ms": dt * 1e3,
+            "sample": f"first {k} of the {n} contexts ({z} entries), oracle/oracle.c orc_minimize single thread, "
+                      f"{dt:.2f} s"}
+
+
+def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3, cpu_s=0.0):
     """BASELINE config 3: signal.Minimize (pkg/signal/signal.go:138-166) over a
     synthetic n-context corpus (geometric lengths, mean `mean`, elements from a
     2^22 universe, distinct inside a context, prio 0..3), resident in HBM;
@@ -247,6 +277,7 @@ def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
         keep, cnt = dev.minimize(off, elems, prios, hint_distinct=U)
         ms.append(dev.L.syzsig_ctx_last_ms(dev.eng.h))
     t = float(np.median(ms))
+    cpu = minimize_cpu(off, elems, prios, cpu_s) if cpu_s > 0 else None
     byts = MIN_BYTES_PER_ENTRY * N + MIN_BYTES_PER_DISTINCT * distinct
     cfg = {"workload": f"BASELINE config 3: Minimize over a {n}-program synthetic corpus, 1 GPU",
            "contexts": n, "entries": N, "distinct": distinct, "mean_len": mean, "survivors": cnt}
@@ -254,7 +285,7 @@ def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
     achieved = byts / (t * 1e-3) / 1e9
     return {"metric": "signal.Minimize corpus entries/sec", "value": N / (t * 1e-3), "unit": "entries/s",
             "higher_is_better": True, "ms": t, "dtype": "u32",
-            "config": cfg,
+            "config": cfg, "cpu": cpu,
             "roofline": {"bound": "hbm", "kernel": MIN_KERNELS,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
@@ -266,7 +297,29 @@ def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3):
 POLL_BYTES_PER_ENTRY = 5.0  # Poll: a polled (elem u32, prio i8) entry (SURVEY 8(d)'s Minimize-style figure)
 
 
-def poll_line(dev, F=16, K=256, per=16384, fresh=0.05, m0=10_000_000, reps=3, seed=1027):
+def poll_cpu(e0, p0, polls, F, target_s):
+    """Poll's CPU leg: the reference loop (manager.go:1027-1052) restated over
+    the oracle's sets (oracle.poll: Diff into maxSignal, Merge, fan-out into
+    every other fuzzer's newMaxSignal, the reply) on one core, poll after poll
+    over the first polls of the same batch against the same maxSignal."""
+    from oracle import oracle as O
+
+    oms = O.deserialize(e0, p0)
+    onm = [O.OSig() for _ in range(F)]
+    t0, k, n = time.perf_counter(), 0, 0
+    for f, ser in polls:
+        O.poll(oms, onm, f, (np.asarray(ser.Elems), np.asarray(ser.Prios)))
+        k += 1
+        n += int(np.asarray(ser.Elems).size)
+        if time.perf_counter() - t0 > target_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "entries/s", "cores": 1, "kind": "port", "ms": dt * 1e3,
+            "sample": f"first {k} of the {len(polls)} polls ({n} entries) against the same {e0.size}-element "
+                      f"maxSignal, oracle.poll single thread (manager.go:1027-1052), {dt:.2f} s"}
+
+
+def poll_line(dev, F=16, K=256, per=16384, fresh=0.05, m0=10_000_000, reps=3, seed=1027, cpu_s=0.0):
     """syz-manager's Poll (manager.go:1027-1052) over a
     batch of K polls from F fuzzers, each carrying a Serial of `per` entries,
     against a 10M-element maxSignal (random u32, prio 0..3): a steady-state
@@ -305,11 +358,12 @@ def poll_line(dev, F=16, K=256, per=16384, fresh=0.05, m0=10_000_000, reps=3, se
         nrep = sum(int(np.asarray(x.Elems).size) for x in replies)
         del ms, nm, replies
     wall, dms = float(np.median(walls)), float(np.median(devs))
+    cpu = poll_cpu(e0, p0, polls, F, cpu_s) if cpu_s > 0 else None
     n = K * per
     achieved = POLL_BYTES_PER_ENTRY * n / (dms * 1e-3) / 1e9
     return {"metric": "manager Poll: polled entries/sec (Diff into maxSignal, Merge, fan-out)",
             "value": n / wall, "unit": "entries/s", "higher_is_better": True, "ms": wall * 1e3, "dtype": "u32",
-            "library_stream_ms": dms,
+            "library_stream_ms": dms, "cpu": cpu,
             "config": {"workload": f"{K} polls from {F} fuzzers x {per} entries ({fresh:.0%} new, the rest already in "
                                    f"maxSignal) vs a {m0}-element maxSignal, one batch (host Serials: upload and "
                                    "replies' Serialize included)",
@@ -337,7 +391,8 @@ def chain_ms(st):
     return st["part_ms"] + st["probe_ms"] + st["decide_ms"]
 
 
-def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m0=10_000_000, walk="global"):
+def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m0=10_000_000, walk="global",
+            cpu_s=0.0, cpu_threads=16):
     """BASELINE config 5 (sustained streaming triage, skewed PC distribution)
     at one rank's share of an 8-GPU node: batches of `programs` x `calls` x
     `pcs`, each triaged against the maxSignal/newSignal state the previous
@@ -365,6 +420,10 @@ def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m
         total += nrec
     m0e, m0p = dev.synth_m0(cfg, KNOWN_SYS[walk], m0)
     pristine = dev.deserialize(m0e, m0p)
+    # CPU leg: the first programs of batch 1 against the same M0 (the oracle's
+    # sequential checkNewSignal on one core, and `cpu_threads` Procs under one
+    # rwlock as fuzzer.go:494-511 runs them)
+    cpu = cpu_baseline(dev, *keep[0][:4], m0e, m0p, calls, cpu_s, cpu_threads) if cpu_s > 0 else None
     del m0e, m0p
     walls, chains, sts = [], [], []
     for r in range(reps + 1):
@@ -388,7 +447,7 @@ def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m
                                      expect_ms=chain / nbatches)
     return {"metric": "signal elems triaged/sec (Diff+Merge), streaming skewed batches",
             "value": total / wall, "unit": "elems/s", "higher_is_better": True,
-            "ms_per_batch": wall * 1e3 / nbatches, "dtype": "u32",
+            "ms_per_batch": wall * 1e3 / nbatches, "dtype": "u32", "cpu": cpu,
             "config": {"workload": wl,
                        "records": total, "batches": nbatches,
                        "retries": [x["retries"] for x in sts], "runs": [x["runs"] for x in sts],
@@ -722,6 +781,80 @@ def ingest_stage(dev, sigs, cs, cnt, prio, comp, P, C, reps=5):
     return float(np.median(ms)), ok
 
 
+def dist_parity(dev, sharded, batch, pool0, pairs, reset, ns, m0e, m0p, rank, world, P, C, backend, nprog=8):
+    """Parity evidence from the sharded run itself (outside the timed region):
+    one more step of batch 0 from M0 on every rank, then
+      * rank 0's first `nprog` programs -- the head of the rank-major serial
+        order, so their checkNewSignal result depends on M0 and their own
+        records only -- against the oracle (plain-C sequential checkNewSignal,
+        syz-fuzzer/fuzzer.go:494-511) over M0 restricted to their elements,
+        gathered from every rank's shard: call_new and the DiffRaw pairs;
+      * the newSignal shards: their union (the shards are disjoint by owner)
+        holds exactly the elements the owners changed.
+    The oracle is the checker here, never the thing measured."""
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+
+    cdev = dev.dev if backend == "nccl" else torch.device("cpu")
+    reset()
+    ns.clear()
+    _, cnew, st = sharded.step(batch, pool0[3], rank * P * C)
+    torch.cuda.synchronize()
+    tot = torch.tensor([ns.Len(), st["changed"], st["new_pairs"], int(cnew.to(torch.int64).sum().item())],
+                       dtype=torch.int64, device=cdev)
+    dist.all_reduce(tot)
+    ns_union, changed, npairs_all, cnew_all = (int(x) for x in tot.tolist())
+    sigs, cs, cnt, prio = pool0[:4]
+    npre = nprog * C
+    keys = None
+    if rank == 0:
+        end = int(cs[npre - 1].item()) + int(cnt[npre - 1].item())
+        hs = sigs[:end].cpu().numpy().view(np.uint32)
+        hcs, hcnt = cs[:npre].cpu().numpy().view(np.uint64), cnt[:npre].cpu().numpy().view(np.uint32)
+        hprio = prio[:npre].cpu().numpy().view(np.uint8)
+        keys = np.unique(np.concatenate([hs[int(a): int(a) + int(n)] for a, n in zip(hcs, hcnt)]))
+        nk = torch.tensor([keys.size], dtype=torch.int64, device=cdev)
+    else:
+        nk = torch.zeros(1, dtype=torch.int64, device=cdev)
+    dist.broadcast(nk, 0)
+    kt = torch.from_numpy(keys.view(np.int32)).to(cdev) if rank == 0 else \
+        torch.empty(int(nk.item()), dtype=torch.int32, device=cdev)
+    dist.broadcast(kt, 0)
+    mask = torch.isin(m0e, kt.to(m0e.device))
+    fe, fp = m0e[mask], m0p[mask].to(torch.int32)  # (int32 for the gather; prios are int8 values)
+    n_here = torch.tensor([fe.numel()], dtype=torch.int64, device=cdev)
+    ns_all = [torch.zeros_like(n_here) for _ in range(world)]
+    dist.all_gather(ns_all, n_here)
+    width = max(1, max(int(x.item()) for x in ns_all))
+    pad_e = torch.zeros(width, dtype=torch.int32, device=cdev)
+    pad_p = torch.zeros(width, dtype=torch.int32, device=cdev)
+    pad_e[: fe.numel()] = fe.to(cdev)
+    pad_p[: fp.numel()] = fp.to(cdev)
+    ge = [torch.zeros_like(pad_e) for _ in range(world)]
+    gp = [torch.zeros_like(pad_p) for _ in range(world)]
+    dist.all_gather(ge, pad_e)
+    dist.all_gather(gp, pad_p)
+    out = {"world_size": world, "backend": backend, "checked_programs": nprog,
+           "newsignal_union": ns_union, "owners_changed": changed, "union_ok": ns_union == changed,
+           "new_pairs_all_ranks": npairs_all, "calls_with_new_all_ranks": cnew_all}
+    if rank == 0:
+        e = np.concatenate([g[: int(n.item())].cpu().numpy().view(np.uint32) for g, n in zip(ge, ns_all)])
+        pr = np.concatenate([g[: int(n.item())].cpu().numpy().astype(np.int8) for g, n in zip(gp, ns_all)])
+        _, _, obits, ocnew = O.triage_batch(e, pr, hs, hcs, hcnt, hprio)
+        r = np.nonzero(np.unpackbits(obits.view(np.uint8), bitorder="little"))[0].astype(np.uint64)
+        call = np.searchsorted(hcs.astype(np.uint64) + hcnt.astype(np.uint64), r, side="right").astype(np.uint64)
+        opairs = np.unique((call << np.uint64(32)) | hs[r].astype(np.uint64))
+        gpairs = pairs[: st["new_pairs"]].cpu().numpy().view(np.uint64)
+        gpairs = np.unique(gpairs[gpairs < (np.uint64(npre) << np.uint64(32))])
+        cnew_ok = bool(np.array_equal(cnew[:npre].cpu().numpy().view(np.uint8), ocnew))
+        pairs_ok = bool(np.array_equal(gpairs, opairs))
+        out.update({"m0_keys_gathered": int(e.size), "prefix_records": int(hcnt.sum()),
+                    "call_new_ok": cnew_ok, "pairs_ok": pairs_ok, "pairs_checked": int(opairs.size),
+                    "ok": cnew_ok and pairs_ok and ns_union == changed})
+    return out
+
+
 def progress(rank, msg):
     """One line per setup phase on stderr (a silent multi-minute setup looks hung)."""
     print(f"[bench rank {rank}] {msg} (t={time.perf_counter() - T0:.1f}s)", file=sys.stderr, flush=True)
@@ -884,6 +1017,8 @@ def main():
         tr = torch.tensor([total_rec], dtype=torch.int64, device=dev.dev)
         dist.all_reduce(tr)
         total_rec = int(tr.item())
+    parity = dist_parity(dev, sharded, batches[0], pool[0], pairs, reset, ns, m0e, m0p, rank, world, P, C,
+                         a.dist_backend) if distributed else None
     ingest_ms, ingest_ok = ingest_stage(dev, sigs, cs, cnt, prio, comp, P, C) if not distributed else (None, None)
     ms_per_step = dt / a.steps * 1e3
     value = total_rec / dt
@@ -926,7 +1061,7 @@ def main():
                        "pcs_per_gpu": npc, "skew": a.skew, "walk": a.walk, "batches": NB,
                        "table_slots": ms.capacity(),
                        "parallelism": f"shard{world}" if distributed else "single",
-                       **({"dist_backend": a.dist_backend} if distributed else {})},
+                       **({"dist_backend": a.dist_backend, "world_size": world} if distributed else {})},
             "roofline": {"bound": "hbm",
                          "kernel": K3_KERNELS if not distributed else K3_DIST_KERNELS,
                          "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -962,9 +1097,10 @@ def main():
                          "traffic_note": e_note,
                          "bytes_per_unit": EDGE_BYTES_PER_PC, "units_per_launch": npc, "avg_launch_ms": e_ms}}}
     if rank == 0 and world == 1 and not a.no_min:
-        out["lines"]["minimize"] = minimize_line(dev, a.min_contexts)
+        out["lines"]["minimize"] = minimize_line(dev, a.min_contexts, cpu_s=0 if a.no_cpu else a.cpu_seconds / 3)
     if rank == 0 and world == 1 and not a.no_c5:
-        out["lines"]["c5"] = c5_line(dev, pairs)
+        out["lines"]["c5"] = c5_line(dev, pairs, cpu_s=0 if a.no_cpu else a.cpu_seconds / 3,
+                                     cpu_threads=a.cpu_threads)
         # rounds 1-4's C5 input (power-skewed region walks), kept comparable
         out["lines"]["c5_region_power"] = c5_line(dev, pairs, walk="region")
     if rank == 0 and world == 1 and not a.no_pipe:
@@ -975,13 +1111,15 @@ def main():
     if rank == 0 and world == 1 and not a.no_c1:
         out["lines"]["c1"] = c1_line(dev)
     if rank == 0 and world == 1 and not a.no_poll:
-        out["lines"]["poll"] = poll_line(dev)
+        out["lines"]["poll"] = poll_line(dev, cpu_s=0 if a.no_cpu else a.cpu_seconds / 3)
     if rank == 0 and world == 1 and not a.no_c4:
         out["lines"]["c4_rank"] = c4_rank_line(dev, sigs, cs, cnt, prio, P, C, L, a.walk)
     if rank == 0 and world == 1 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(dev, sigs, cs, cnt, prio, m0e, m0p, C, a.cpu_seconds, a.cpu_threads)
     elif rank == 0:
         out["cpu_baseline"] = None
+    if rank == 0 and distributed:
+        out["parity"] = parity
     if rank == 0:
         out["achievable_bw"] = ach
         with_achievable(out["roofline"], ach)

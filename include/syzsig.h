@@ -384,52 +384,26 @@ int syzsig_ingest_exec_output_dev(syzsig_ctx* ctx, const uint32_t* d_out, uint64
 
 /* ---- hash-sharded maxSignal across GPUs (one process per GPU) ----
  * The batch is split by program range over G GPUs (serial order = GPU-major);
- * every record is routed to the GPU owning its element
- * (owner = syz::owner_of(elem, G)), packed as
+ * each element is owned by the GPU owner = syz::owner_of(elem, G).  Records
+ * travel packed as
  *   elem << 32 | level << 24 | serial      (serial < 2^24, level < 4)
  * where serial is its call's position in the batch's global serial order and
  * level the rank of its call's prio in `levels` (ascending int8, <= 4 entries,
- * the union of the prios of all GPUs' calls).
+ * the union of the prios of all GPUs' calls).  A source sends only each
+ * element's staircase -- for every level, the element's first local record at
+ * that level if no earlier local record has a higher level, <= 4 records per
+ * distinct element: records off the staircase can never be new nor raise
+ * maxSignal, so the owner's triage of the staircases is checkNewSignal's exact
+ * result.  The exchange is the stream-ordered step below; the owner side is
+ * records mode:
  *
- * partition: d_send (b->nrec entries) receives the records grouped by owner,
- * owner g's group at [send_off[g], send_off[g] + send_counts[g]) with
- * send_off the exclusive prefix sum (host arrays, nshards entries each);
- * d_send_pos[r] = where record r went. */
-int syzsig_shard_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
-                               const int8_t* levels, uint32_t nlevels, uint32_t nshards,
-                               uint64_t* d_send, uint32_t* d_send_pos, uint64_t* send_counts);
-/* Owner side: triage received records against the local shard of maxSignal;
- * d_new_flags[i] = 1 iff received record i is new (checkNewSignal's DiffRaw
+ * syzsig_triage_records_dev: triage records against the local shard of
+ * maxSignal; d_new_flags[i] = 1 iff record i is new (checkNewSignal's DiffRaw
  * result for its call).  Serial order comes from the records' serial fields;
  * records with one serial are one call's, so they carry one level. */
 int syzsig_triage_records_dev(syzsig_ctx* ctx, syzsig_set* shard, syzsig_set** new_signal,
                               const uint64_t* d_recs, uint64_t nrec, const int8_t* levels,
                               uint32_t nlevels, uint8_t* d_new_flags, syzsig_batch_stats* stats);
-/* Source side: d_back_flags (send order, returned by the owners) -> b->new_bits
- * and b->call_new (both zeroed here first). */
-int syzsig_shard_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, const uint32_t* d_send_pos,
-                                 const uint8_t* d_back_flags);
-
-/* Aggregated routing (the large-batch form of the two calls above).  The
- * source aggregates its records per element and sends only each element's
- * staircase -- for every level, the element's first record at that level if
- * no earlier local record has a higher level -- at most 4 records per
- * distinct element, packed and grouped by owner as above (records-mode triage
- * on the owners is unchanged).  Records that are off the staircase can never
- * be new nor raise maxSignal, so the result is the same as routing every
- * record.  d_send needs room for the batch's record count (an upper bound);
- * send_counts[g] = records for owner g, packed at their exclusive prefix sum.
- * stats: records, distinct, parts and timings of the local aggregation;
- * candidates = staircase records sent. */
-int syzsig_shard_agg_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
-                                   const int8_t* levels, uint32_t nlevels, uint32_t nshards, uint64_t* d_send,
-                                   uint64_t send_cap, uint64_t* send_counts, syzsig_batch_stats* stats);
-/* Source side of the aggregated routing: the owners' flags for d_send[0 .. n_send)
- * -> b->call_new, b->new_bits (if set), b->new_pairs (if set; stats->new_pairs
- * = the total).  serial_base as given to the partition call. */
-int syzsig_shard_agg_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
-                                     const uint64_t* d_send, uint64_t n_send, const uint8_t* d_back_flags,
-                                     syzsig_batch_stats* stats);
 
 /* ---- the stream-ordered sharded step (one process per GPU) ----
  * The three calls below only enqueue work on the context's stream and return;
@@ -440,8 +414,7 @@ int syzsig_shard_agg_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uin
  *   word 0      header: records for g (the true count, even past cap)
  *               | SYZSIG_STEP_HDR_VOID (the source's run is void)
  *               | SYZSIG_STEP_HDR_OVF  (more than cap records for g)
- *   words 1..   the staircase records (elem << 32 | level << 24 | serial), as
- *               syzsig_shard_agg_partition_dev packs them.
+ *   words 1..   the staircase records (elem << 32 | level << 24 | serial).
  * An equal-split all-to-all of the buckets gives each owner every source's
  * bucket for it (d_recv, same layout, bucket s from source s); the owner's
  * flags go back the same way, one byte per word (d_flags / d_back, nshards *

@@ -131,14 +131,8 @@ SIGNATURES = {
     "syzsig_edge_derive_dev": (c_int, [_P, _P, c_uint64, _P, _P, c_uint64, _P, c_uint64, _P, _P, _P]),
     "syzsig_ingest_exec_output_dev": (c_int, [_P, _P, c_uint64, _P, c_uint64, _P, c_uint64, _P, _P, _P, _P, _P, _P,
                                               _P, _P, _P, POINTER(c_uint64)]),
-    "syzsig_shard_partition_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint32, c_uint32, _P, _P, _P]),
     "syzsig_triage_records_dev": (c_int, [_P, _P, _PP, _P, c_uint64, _P, c_uint32, _P,
                                           POINTER(BatchStats)]),
-    "syzsig_shard_unpartition_dev": (c_int, [_P, POINTER(Batch), _P, _P]),
-    "syzsig_shard_agg_partition_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint32, c_uint32, _P, c_uint64,
-                                               _P, POINTER(BatchStats)]),
-    "syzsig_shard_agg_unpartition_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint64, _P,
-                                                 POINTER(BatchStats)]),
     "syzsig_step_send_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint32, c_uint32, c_uint64, _P, c_int]),
     "syzsig_step_own_dev": (c_int, [_P, _P, _P, _P, c_uint32, c_uint64, _P, c_uint32, _P, c_int]),
     "syzsig_step_back_dev": (c_int, [_P, POINTER(Batch), c_uint64, _P, c_uint32, c_uint64, _P]),

@@ -527,25 +527,29 @@ constexpr uint32_t kDummyLines = 2048;  // CapCells::dummy lines
 // Work items of 2^ibits calls own their cells (items = chunks for a triage
 // batch).  kEntry (Minimize): the level comes from each record's own prio
 // (x.elem_prio), and only the records whose element shard x.shard owns are kept.
-template <bool kEntry, uint32_t kB>
-__global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t* __restrict__ sigs,
+// kMaxP: the partitions the LDS is sized for; kWpe: waves per SIMD the
+// registers are sized for (4: one workgroup per CU, 8: two, each with half
+// the LDS: 1024 partitions of 64-B blocks).
+template <bool kEntry, uint32_t kB, uint32_t kMaxP = kAggMaxParts, uint32_t kWpe = 4, uint32_t kT = kAggThreads>
+__global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __restrict__ sigs,
                                                                  const uint64_t* __restrict__ call_start,
                                                                  const uint32_t* __restrict__ call_len,
                                                                  const uint8_t* __restrict__ call_prio, LevelMap lm,
                                                                  uint64_t c0, uint64_t c1, AggGeom g, AggSrc x,
                                                                  CapCells cc, uint32_t* recs, uint32_t dbg)
 {
-	constexpr uint32_t kWaves = kAggThreads / 64, kPer = kEntry ? SYZ_SCAT_PER_ENTRY : SYZ_SCAT_PER, kQuota = kPer * 64;
+	constexpr uint32_t kWaves = kT / 64, kPer = kEntry ? SYZ_SCAT_PER_ENTRY : SYZ_SCAT_PER, kQuota = kPer * 64;
 	constexpr uint32_t kG = 64 / kB;  // blocks a wave writes per store (kB lanes each)
 	static_assert(kB == 16 || kB == 32, "block of 64 or 128 B");
-	__shared__ uint32_t buf[kAggMaxParts * kBlk];  // per partition: the block being filled (P * kB <= this)
-	__shared__ uint32_t fillc[kAggMaxParts + 1];   // slots handed out in it (may overshoot kB)
-	__shared__ uint32_t written[kAggMaxParts + 1]; // records of the cell written so far (+ a spare)
-	__shared__ uint16_t flist[kAggMaxParts];       // partitions whose block filled this sub-round
-	__shared__ uint32_t nfl[2];                    // their count, by sub-round parity
-	__shared__ uint64_t c_start[kScatChunkMax];    // the chunk's calls
-	__shared__ uint32_t c_len[kScatChunkMax];
-	__shared__ uint16_t c_meta[kScatChunkMax];
+	constexpr uint32_t kChunkMax = kMaxP / 4;        // calls per chunk (cbits = pbits - 2)
+	__shared__ uint32_t buf[kMaxP * (kMaxP == kAggMaxParts ? kBlk : kB)];  // per partition: the block being filled
+	__shared__ uint32_t fillc[kMaxP + 1];   // slots handed out in it (may overshoot kB)
+	__shared__ uint32_t written[kMaxP + 1]; // records of the cell written so far (+ a spare)
+	__shared__ uint16_t flist[kMaxP];       // partitions whose block filled this sub-round
+	__shared__ uint32_t nfl[2];             // their count, by sub-round parity
+	__shared__ uint64_t c_start[kChunkMax]; // the chunk's calls
+	__shared__ uint32_t c_len[kChunkMax];
+	__shared__ uint16_t c_meta[kChunkMax];
 	__shared__ uint8_t s_lvl[kEntry ? 256 : 1];
 	__shared__ uint32_t s_or[2][kWaves];
 	const uint32_t P = 1u << g.pbits, cb = g.cbits(), ib = g.ibits;
@@ -652,10 +656,10 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 					d[slot] = v[t];
 				}
 				__builtin_amdgcn_wave_barrier();
-				if (slot == 0) {  // (a group past the list updates the spare entry kAggMaxParts)
+				if (slot == 0) {  // (a group past the list updates the spare entry kMaxP)
 #pragma unroll
 					for (uint32_t t = 0; t < 4; t++) {
-						const uint32_t q = jb + t * kWaves * kG + w * kG + grp < nf ? pp[t] : kAggMaxParts;
+						const uint32_t q = jb + t * kWaves * kG + w * kG + grp < nf ? pp[t] : kMaxP;
 						written[q] = wr[t] + kB;
 						fillc[q] = 0;
 					}
@@ -757,10 +761,17 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_scatter_blk(const uint32_t*
 #ifndef SYZ_SCAT_WIDE
 #define SYZ_SCAT_WIDE 1
 #endif
+#ifndef SYZ_SCAT_2WG  // <= 1024 partitions: 64-B blocks, two workgroups per CU (experiment)
+#define SYZ_SCAT_2WG 0
+#endif
 template <bool kEntry, typename... A>
 static void scatter_blk(uint32_t grid, hipStream_t s, uint32_t pbits, A... a)
 {
-	if (SYZ_SCAT_WIDE && pbits < kAggMaxBits)
+	if (SYZ_SCAT_2WG == 2 && pbits < kAggMaxBits)  // two 512-thread workgroups per CU
+		k_agg_scatter_blk<kEntry, 16, kAggMaxParts / 2, 4, 512><<<grid, 512, 0, s>>>(a...);
+	else if (SYZ_SCAT_2WG && pbits < kAggMaxBits)
+		k_agg_scatter_blk<kEntry, 16, kAggMaxParts / 2, 8><<<grid, kAggThreads, 0, s>>>(a...);
+	else if (SYZ_SCAT_WIDE && pbits < kAggMaxBits)
 		k_agg_scatter_blk<kEntry, 32><<<grid, kAggThreads, 0, s>>>(a...);
 	else
 		k_agg_scatter_blk<kEntry, 16><<<grid, kAggThreads, 0, s>>>(a...);
@@ -2801,101 +2812,8 @@ __device__ __forceinline__ uint32_t stair_levels(uint4 f4, uint32_t nlev)
 	return m;
 }
 
-// staircase records per owner (block histogram, one atomic per owner per block)
-__global__ __launch_bounds__(256) void k_stair_count(const uint32_t* __restrict__ dist_e,
-                                                     const uint4* __restrict__ dist_f,
-                                                     const uint32_t* __restrict__ cnt, uint32_t nregions,
-                                                     uint32_t nlev, uint32_t nshards, unsigned long long* counts)
-{
-	__shared__ uint32_t h[kMaxShardsAgg];
-	if (threadIdx.x < kMaxShardsAgg)
-		h[threadIdx.x] = 0;
-	__syncthreads();
-	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
-		const uint32_t n = cnt[r] == kAggOverflow ? 0 : cnt[r];
-		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-			const uint64_t o = (uint64_t)r * kAggRegion + i;
-			const uint32_t m = stair_levels(dist_f[o], nlev);
-			if (m)
-				atomicAdd(&h[owner_of(dist_e[o], nshards)], (uint32_t)__popc(m));
-		}
-	}
-	__syncthreads();
-	if (threadIdx.x < nshards && h[threadIdx.x])
-		atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
-}
 
-// staircase records -> send[], grouped by owner (cursor[g] = next free slot of g)
-__global__ __launch_bounds__(256) void k_stair_scatter(const uint32_t* __restrict__ dist_e,
-                                                       const uint4* __restrict__ dist_f,
-                                                       const uint32_t* __restrict__ cnt, uint32_t nregions,
-                                                       uint32_t nlev, uint32_t nshards, uint64_t serial_base,
-                                                       unsigned long long* cursor, uint64_t* send)
-{
-	__shared__ uint32_t h[kMaxShardsAgg];
-	__shared__ unsigned long long base[kMaxShardsAgg];
-	for (uint32_t r = blockIdx.x; r < nregions; r += gridDim.x) {
-		if (threadIdx.x < kMaxShardsAgg)
-			h[threadIdx.x] = 0;
-		__syncthreads();
-		const uint32_t n = cnt[r] == kAggOverflow ? 0 : cnt[r];
-		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-			const uint64_t o = (uint64_t)r * kAggRegion + i;
-			const uint32_t m = stair_levels(dist_f[o], nlev);
-			if (m)
-				atomicAdd(&h[owner_of(dist_e[o], nshards)], (uint32_t)__popc(m));
-		}
-		__syncthreads();
-		if (threadIdx.x < nshards) {
-			base[threadIdx.x] = h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)h[threadIdx.x]) : 0;
-			h[threadIdx.x] = 0;
-		}
-		__syncthreads();
-		for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-			const uint64_t o = (uint64_t)r * kAggRegion + i;
-			const uint4 f4 = dist_f[o];
-			const uint32_t m = stair_levels(f4, nlev);
-			if (!m)
-				continue;
-			const uint32_t e = dist_e[o], g = owner_of(e, nshards);
-			const uint32_t f[4] = {f4.x, f4.y, f4.z, f4.w};
-			uint64_t pos = base[g] + atomicAdd(&h[g], (uint32_t)__popc(m));
-#pragma unroll
-			for (uint32_t l = 0; l < 4; l++)
-				if ((m >> l) & 1)
-					send[pos++] = ((uint64_t)e << 32) | ((uint64_t)l << 24) | ((serial_base + f[l]) & kSerialMask);
-		}
-		__syncthreads();
-	}
-}
 
-// The owners' flags back at the source: a flagged staircase record (e, serial)
-// is the pair (call = serial - serial_base, e) of that call's DiffRaw result.
-__global__ __launch_bounds__(256) void k_stair_back(const uint64_t* __restrict__ send,
-                                                    const uint8_t* __restrict__ back, uint64_t n,
-                                                    uint64_t serial_base, uint8_t* call_new, uint64_t* pairs,
-                                                    unsigned long long* npairs)
-{
-	const uint32_t lane = lane_id();
-	for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < n; i0 += (uint64_t)gridDim.x * blockDim.x) {
-		const uint64_t i = i0 + threadIdx.x;
-		const bool on = i < n && back[i];
-		uint64_t v = 0;
-		if (on) {
-			const uint64_t r = send[i];
-			const uint64_t c = (r & kSerialMask) - serial_base;
-			call_new[c] = 1;
-			v = (c << 32) | (r >> 32);
-		}
-		const uint64_t m = __ballot(on);
-		unsigned long long wb = 0;
-		if (lane == 0 && m)
-			wb = atomicAdd(npairs, (unsigned long long)__popcll(m));
-		wb = __shfl(wb, 0, 64);
-		if (on)
-			pairs[wb + lane_rank(m)] = v;
-	}
-}
 
 // ---- the stream-ordered step's source side (syzsig_step_send_dev / _back_dev)
 // Staircase records into fixed buckets: owner g's at send[g * (cap + 1) + 1 ...],
@@ -3177,105 +3095,6 @@ int syzsig_step_back_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial
 	}
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev_step[5], s));
-	return SYZSIG_OK;
-}
-
-int syzsig_shard_agg_partition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
-                                   const int8_t* levels, uint32_t nlevels, uint32_t nshards, uint64_t* d_send,
-                                   uint64_t send_cap, uint64_t* send_counts, syzsig_batch_stats* stats)
-{
-	SYZ_LOCK(ctx);
-	if (!ctx || !b || !send_counts || (b->nrec && !b->sigs) || (send_cap && !d_send) ||
-	    (b->ncalls && (!b->call_start || !b->call_len || !b->call_prio)))
-		return fail(SYZSIG_EINVAL, "shard_agg_partition: NULL argument");
-	if (nshards == 0 || nshards > kMaxShardsAgg)
-		return fail(SYZSIG_EINVAL, "shard_agg_partition: nshards must be 1..64");
-	if (b->nrec >= (1ull << 32))
-		return fail(SYZSIG_ERANGE, "shard_agg_partition: >= 2^32 records per GPU");
-	if (serial_base + b->ncalls > kSerialMask + 1ull)
-		return fail(SYZSIG_ERANGE, "shard_agg_partition: batch serial order exceeds 2^24 calls");
-	LevelMap lm;
-	SYZ_TRY(level_map_from_levels(levels, nlevels, &lm));
-	for (uint32_t i = 0; i < nshards; i++)
-		send_counts[i] = 0;
-	syzsig_batch_stats st;
-	memset(&st, 0, sizeof(st));
-	if (b->ncalls) {
-		uint64_t total = 0;
-		uint32_t mask[8];
-		SYZ_TRY(batch_total_records(ctx, b, &total, mask));
-		for (int p = 0; p < 256; p++)
-			if (((mask[p >> 5] >> (p & 31)) & 1) && lm.lvl[p] == 0xff)
-				return fail(SYZSIG_EINVAL, "shard_agg_partition: a call's prio is not among `levels`");
-		st.records = total;
-		if (total) {
-			AggOut a;
-			SYZ_TRY(agg_aggregate(ctx, b, 0, b->ncalls, lm, total, &st, &a));
-			const hipStream_t s = ctx->stream;
-			void* dcur;
-			SYZ_TRY(ws_get(ctx, 6, 2 * kMaxShardsAgg * 8, &dcur));
-			unsigned long long* counts = (unsigned long long*)dcur;
-			unsigned long long* cursor = counts + kMaxShardsAgg;
-			SYZ_HIP(hipMemsetAsync(counts, 0, kMaxShardsAgg * 8, s));
-			const int grid = (int)std::min<uint32_t>(a.nregions, 2048);
-			k_stair_count<<<grid, 256, 0, s>>>(a.dist_e, a.dist_f, a.cnt, a.nregions, lm.n, nshards, counts);
-			SYZ_HIP(hipGetLastError());
-			unsigned long long h[kMaxShardsAgg];
-			SYZ_HIP(hipMemcpyAsync(h, counts, nshards * 8, hipMemcpyDeviceToHost, s));
-			SYZ_HIP(hipStreamSynchronize(s));
-			unsigned long long off[kMaxShardsAgg], run = 0;
-			for (uint32_t i = 0; i < nshards; i++) {
-				off[i] = run;
-				run += h[i];
-				send_counts[i] = h[i];
-			}
-			st.candidates = run;
-			if (run > send_cap)
-				return fail(SYZSIG_ERANGE, "shard_agg_partition: send buffer too small (records suffice)");
-			SYZ_HIP(hipMemcpyAsync(cursor, off, nshards * 8, hipMemcpyHostToDevice, s));
-			k_stair_scatter<<<grid, 256, 0, s>>>(a.dist_e, a.dist_f, a.cnt, a.nregions, lm.n, nshards, serial_base,
-			                                     cursor, d_send);
-			SYZ_HIP(hipGetLastError());
-			SYZ_HIP(hipStreamSynchronize(s));
-		}
-	}
-	if (stats)
-		*stats = st;
-	return SYZSIG_OK;
-}
-
-int syzsig_shard_agg_unpartition_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial_base,
-                                     const uint64_t* d_send, uint64_t n_send, const uint8_t* d_back_flags,
-                                     syzsig_batch_stats* stats)
-{
-	SYZ_LOCK(ctx);
-	if (!ctx || !b || (n_send && (!d_send || !d_back_flags)) || (b->ncalls && !b->call_new) ||
-	    (b->new_pairs_cap && !b->new_pairs))
-		return fail(SYZSIG_EINVAL, "shard_agg_unpartition: NULL argument");
-	const hipStream_t s = ctx->stream;
-	if (b->new_bits)
-		SYZ_HIP(hipMemsetAsync(b->new_bits, 0, ((b->nrec + 31) / 32) * 4, s));
-	if (b->ncalls)
-		SYZ_HIP(hipMemsetAsync(b->call_new, 0, b->ncalls, s));
-	uint64_t np = 0;
-	if (n_send && b->ncalls) {
-		void* pr;
-		SYZ_TRY(ws_get(ctx, 15, n_send * 8 + 64, &pr));
-		SYZ_TRY(counters_reset(ctx));
-		k_stair_back<<<grid_for(n_send, 256, 8192), 256, 0, s>>>(d_send, d_back_flags, n_send, serial_base,
-		                                                          b->call_new, (uint64_t*)pr, &ctx->d_cnt[kCntAux2]);
-		SYZ_HIP(hipGetLastError());
-		SYZ_TRY(counters_fetch(ctx));
-		np = ctx->h_cnt[kCntAux2];
-		SYZ_TRY(agg_mark_bits(ctx, b, 0, b->ncalls, (const uint64_t*)pr, 0, np));
-		if (b->new_pairs && np)
-			SYZ_HIP(hipMemcpyAsync(b->new_pairs, pr, std::min(np, b->new_pairs_cap) * 8, hipMemcpyDeviceToDevice, s));
-	}
-	SYZ_HIP(hipStreamSynchronize(s));
-	if (stats) {
-		memset(stats, 0, sizeof(*stats));
-		stats->new_pairs = np;
-	}
 	return SYZSIG_OK;
 }
 

@@ -239,14 +239,7 @@ class Device:
                                                  _p(keep), ctypes.byref(cnt)))
         return keep, int(cnt.value)
 
-    # ---------------------------------------------------------------- sharding
-    def shard_partition(self, b, serial_base, levels, nshards, send, send_pos):
-        lv = (ctypes.c_int8 * len(levels))(*levels)
-        counts = (ctypes.c_uint64 * nshards)()
-        check(self.L.syzsig_shard_partition_dev(self.eng.h, ctypes.byref(b), int(serial_base), lv, len(levels),
-                                                int(nshards), _p(send), _p(send_pos), counts))
-        return [int(c) for c in counts]
-
+    # ---------------------------------------------------------------- sharding (records mode: the owner side)
     def triage_records(self, shard, new_signal, recs, levels, new_flags):
         self._check_dev(recs, new_flags)
         lv = (ctypes.c_int8 * len(levels))(*levels)
@@ -256,28 +249,6 @@ class Device:
                                                lv, len(levels), _p(new_flags), ctypes.byref(st)))
         if nh.value and new_signal.is_nil():
             new_signal._h = nh
-        return st.as_dict()
-
-    def shard_unpartition(self, b, send_pos, back_flags):
-        check(self.L.syzsig_shard_unpartition_dev(self.eng.h, ctypes.byref(b), _p(send_pos), _p(back_flags)))
-
-    def shard_agg_partition(self, b, serial_base, levels, nshards, send):
-        """Aggregated routing: each distinct element's staircase records, grouped
-        by owner, into send (int64, >= b.nrec entries).  -> (counts, stats)."""
-        self._check_dev(send)
-        lv = (ctypes.c_int8 * len(levels))(*levels)
-        counts = (ctypes.c_uint64 * nshards)()
-        st = BatchStats()
-        check(self.L.syzsig_shard_agg_partition_dev(self.eng.h, ctypes.byref(b), int(serial_base), lv, len(levels),
-                                                    int(nshards), _p(send), send.numel(), counts, ctypes.byref(st)))
-        return [int(c) for c in counts], st.as_dict()
-
-    def shard_agg_unpartition(self, b, serial_base, send, back_flags):
-        """The owners' flags for send -> b's call_new / new_bits / new_pairs."""
-        self._check_dev(send, back_flags)
-        st = BatchStats()
-        check(self.L.syzsig_shard_agg_unpartition_dev(self.eng.h, ctypes.byref(b), int(serial_base), _p(send),
-                                                      send.numel(), _p(back_flags), ctypes.byref(st)))
         return st.as_dict()
 
     # ---------------------------------------------------------------- the stream-ordered sharded step

@@ -7,12 +7,11 @@
       ~400M entries), against orc_minimize; plus a distinct-length corpus where
       the reference's unstable sort.Slice order cannot matter.
   C4  a 1B-element maxSignal: hash-sharded into 8 shard tables on one GPU, one
-      C2 batch split into 8 source program ranges routed through the staircase
-      exchange (shard_agg_partition -> owners' records-mode triage ->
-      shard_agg_unpartition), against the same batch on the unsharded 1B table;
-      plus the oracle on a program prefix (M0 restricted to the prefix's keys).
-      The same through the stream-ordered step API (syzsig_step_*) that
-      `bench.py --gpus 8` runs, on the global walk's 1.07e9-record batch.
+      C2 batch (the global walk's 1.07e9 records) split into 8 source program
+      ranges routed through the stream-ordered step API (syzsig_step_*) that
+      `bench.py --gpus 8` runs, against the same batch on the unsharded 1B
+      table; plus the oracle on a program prefix (M0 restricted to the
+      prefix's keys).
   C5  streaming, skewed: two consecutive batches of 8192 programs x 64 x 1k
       (one rank's share of 64k programs per batch on 8 GPUs; SURVEY 8(d)'s
       global walks from Zipf(1.1) entries, and rounds 1-4's power-skewed
@@ -146,85 +145,6 @@ def _owner_split(gpu, m0e, m0p, G, chunk=1 << 27):
             parts[g].append((e[m], p[m]))
         del own
     return [(torch.cat([x[0] for x in q]), torch.cat([x[1] for x in q])) for q in parts]
-
-
-def test_c4_sharded_1b_vs_unsharded(gpu):
-    from syzkaller_amd import signal as S
-    from syzkaller_amd import synth
-
-    G, NM0 = 8, 1_000_000_000
-    cfg = synth.synth_default()
-    P, C, L = 4096, 64, 4096
-    sigs, cs, cnt, prio = device_batch(gpu, cfg, 0, P, C, L)
-    m0e, m0p = gpu.synth_m0(cfg, 2048, NM0)
-    # unsharded: the whole batch against the 1B table
-    ms = gpu.deserialize(m0e, m0p)
-    assert ms.capacity() == 1 << 31
-    ns = S.Signal(None, gpu.eng)
-    pairs = torch.full((16 << 20,), -1, dtype=torch.int64, device=gpu.dev)
-    _, cnew, st = gpu.triage(ms, ns, sigs, cs, cnt, prio, new_pairs=pairs, want_bits=False)
-    ref_pairs = np.sort(_u(pairs[: st["new_pairs"]], np.uint64))
-    ref_cnew = cnew.clone()
-    # sharded: 8 owner tables, 8 source program ranges
-    split = _owner_split(gpu, m0e, m0p, G)
-    shards = [gpu.deserialize(e, p) for e, p in split]
-    del split
-    news = [S.Signal(None, gpu.eng) for _ in range(G)]
-    levels = sorted(set(int(x) for x in prio.cpu().numpy().astype(np.int8)))
-    ncalls = P * C
-    bounds = [ncalls * s // G for s in range(G + 1)]
-    src = []
-    for s in range(G):
-        a, z = bounds[s], bounds[s + 1]
-        sp = torch.full((16 << 20,), -1, dtype=torch.int64, device=gpu.dev)
-        b, _, scnew = gpu.batch(sigs, cs[a:z].contiguous(), cnt[a:z].contiguous(), prio[a:z].contiguous(),
-                                new_pairs=sp, want_bits=False)
-        send = torch.empty(int(cnt[a:z].to(torch.int64).sum()), dtype=torch.int64, device=gpu.dev)
-        counts, _ = gpu.shard_agg_partition(b, a, levels, G, send)
-        off = np.concatenate([[0], np.cumsum(counts)])
-        src.append((b, scnew, sp, send[: off[-1]], off))
-    flags = []
-    for g in range(G):
-        recv = torch.cat([x[3][x[4][g]: x[4][g + 1]] for x in src])
-        f = torch.zeros(recv.numel(), dtype=torch.uint8, device=gpu.dev)
-        if recv.numel():
-            gpu.triage_records(shards[g], news[g], recv, levels, f)
-        flags.append(f)
-    got_pairs = []
-    for s, (b, scnew, sp, send, off) in enumerate(src):
-        lens = [int(off[g + 1] - off[g]) for g in range(G)]
-        starts = [sum(int(x[4][g + 1] - x[4][g]) for x in src[:s]) for g in range(G)]
-        back = torch.cat([flags[g][starts[g]: starts[g] + lens[g]] for g in range(G)])
-        st2 = gpu.shard_agg_unpartition(b, bounds[s], send, back)
-        assert torch.equal(scnew, ref_cnew[bounds[s]: bounds[s + 1]])
-        got_pairs.append(_u(sp[: st2["new_pairs"]], np.uint64) + (np.uint64(bounds[s]) << np.uint64(32)))
-    np.testing.assert_array_equal(np.sort(np.concatenate(got_pairs)), ref_pairs)
-    # the union of the shards == the unsharded M_final (and newSignal): equal
-    # lengths and an empty Diff both ways (Diff is pinned against the oracle in
-    # test_gpu_signal.py)
-    assert sum(s.Len() for s in shards) == ms.Len()
-    U = S.Signal(None, gpu.eng)
-    for s in shards:
-        U.Merge(s)
-    assert U.Len() == ms.Len()
-    assert ms.Diff(U).is_nil() and U.Diff(ms).is_nil()
-    NU = S.Signal(None, gpu.eng)
-    for s in news:
-        NU.Merge(s)
-    assert NU.Len() == ns.Len() and ns.Diff(NU).is_nil() and NU.Diff(ns).is_nil()
-    del U, NU, shards
-    # oracle on a program prefix: M0 restricted to the prefix's elements gives
-    # the same checkNewSignal result for those calls as the whole 1B M0
-    npre = 16 * C
-    end = int(cs[npre - 1]) + int(cnt[npre - 1])
-    hs, hcs, hcnt, hprio = (_u(sigs[:end], np.uint32), _u(cs[:npre], np.uint64), _u(cnt[:npre], np.uint32),
-                            _u(prio[:npre], np.uint8))
-    keys = np.unique(np.concatenate([hs[int(a): int(a) + int(n)] for a, n in zip(hcs, hcnt)]))
-    fe, fp = O.filter_keys(_u(m0e, np.uint32), _u(m0p, np.int8), keys)
-    _, _, obits, ocnew = O.triage_batch(fe, fp, hs, hcs, hcnt, hprio)
-    np.testing.assert_array_equal(_u(ref_cnew[:npre], np.uint8), ocnew)
-    op = pairs_from_bits(hs, hcs, hcnt, obits)
-    np.testing.assert_array_equal(ref_pairs[ref_pairs < (np.uint64(npre) << np.uint64(32))], op)
 
 
 @pytest.mark.parametrize("walk", ["global", "region"])

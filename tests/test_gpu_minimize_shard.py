@@ -91,61 +91,16 @@ def test_minimize_host_api(gpu):
 
 
 @pytest.mark.parametrize("nshards", [2, 3, 8])
-def test_shard_routing_equals_unsharded(gpu, nshards):
-    """Hash-partition maxSignal into G tables on one GPU, route records with
-    partition -> triage_records (per shard) -> unpartition, and compare with
-    plain triage of the whole batch against the unsharded maxSignal."""
-    from syzkaller_amd import signal as S
-    from syzkaller_amd import synth
-    from syzkaller_amd._lib import Batch  # noqa: F401
-    from tests.test_gpu_triage import dev_batch
-
-    cfg = synth.synth_default(skew=1)
-    nprog, cpp = 48, 32
-    cl = synth.call_lengths(nprog, cpp, 0, ragged=(0, 3000), seed=nshards)
-    ds, dcs, dcnt, dprio = dev_batch(gpu, cfg, nprog, cpp, cl)
-    m0e, m0p = synth.m0(cfg, 1024, 80000)
-    # unsharded reference run
-    ms = S.Serial(m0e, m0p).Deserialize(gpu.eng)
-    ns = S.Signal(None, gpu.eng)
-    bits, cnew, _ = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
-    # sharded: shard g holds the M0 elements it owns
-    owner = np.array([_owner(int(x), nshards) for x in m0e], np.uint32)
-    shards = [S.Serial(m0e[owner == g], m0p[owner == g]).Deserialize(gpu.eng) for g in range(nshards)]
-    news = [S.Signal(None, gpu.eng) for _ in range(nshards)]
-    levels = sorted(set(int(x) for x in dprio.cpu().numpy().astype(np.int8)))
-    b, sbits, scnew = gpu.batch(ds, dcs, dcnt, dprio)
-    send = torch.empty(ds.numel(), dtype=torch.int64, device=gpu.dev)
-    send_pos = torch.empty(ds.numel(), dtype=torch.int32, device=gpu.dev)
-    counts = gpu.shard_partition(b, 0, levels, nshards, send, send_pos)
-    flags = torch.zeros(ds.numel(), dtype=torch.uint8, device=gpu.dev)
-    off = 0
-    for g in range(nshards):
-        seg = send[off: off + counts[g]]
-        f = flags[off: off + counts[g]]
-        gpu.triage_records(shards[g], news[g], seg, levels, f)
-        off += counts[g]
-    gpu.shard_unpartition(b, send_pos, flags)
-    torch.cuda.synchronize()
-    assert torch.equal(scnew, cnew)
-    assert torch.equal(sbits, bits)
-    merged = {}
-    for g in range(nshards):
-        merged.update(shards[g].to_dict())
-    assert merged == ms.to_dict()
-    nmerged = {}
-    for g in range(nshards):
-        nmerged.update(news[g].to_dict() if not news[g].is_nil() else {})
-    assert nmerged == ns.to_dict()
-
-
-@pytest.mark.parametrize("nshards", [2, 3, 8])
-def test_shard_agg_routing_equals_unsharded(gpu, nshards):
-    """The aggregated routing on one GPU: G sources (program ranges of one
-    batch) each send their staircase records (agg.hip) to G owner shards; the
-    owners triage in records mode, flags come back, and the union of the
-    sources' call flags / record bits / pairs and of the shards equals plain
-    triage of the whole batch against the unsharded maxSignal."""
+@pytest.mark.parametrize("bits", [False, True])
+def test_step_routing_equals_unsharded(gpu, nshards, bits):
+    """The sharded step's device API on one GPU (what dist.ShardedTriage
+    drives, the all-to-alls replaced by tensor copies): G sources (program
+    ranges of one batch) each send their staircase records into fixed buckets
+    (syzsig_step_send_dev), the G owner shards triage what they receive
+    (syzsig_step_own_dev), the flags come back (syzsig_step_back_dev); the
+    sources' call flags, record bits (when asked for) and pairs, the union of
+    the shards and of the newSignal shards equal plain triage of the whole
+    batch against the unsharded maxSignal, and the pairs equal the oracle's."""
     from syzkaller_amd import signal as S
     from syzkaller_amd import synth
     from tests.test_gpu_triage import dev_batch, oracle_pairs
@@ -157,48 +112,55 @@ def test_shard_agg_routing_equals_unsharded(gpu, nshards):
     m0e, m0p = synth.m0(cfg, 1024, 80000)
     ms = S.Serial(m0e, m0p).Deserialize(gpu.eng)
     ns = S.Signal(None, gpu.eng)
-    bits, cnew, _ = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
+    ref_bits, cnew, _ = gpu.triage(ms, ns, ds, dcs, dcnt, dprio)
     owner = np.array([_owner(int(x), nshards) for x in m0e], np.uint32)
     shards = [S.Serial(m0e[owner == g], m0p[owner == g]).Deserialize(gpu.eng) for g in range(nshards)]
-    news = [S.Signal(None, gpu.eng) for _ in range(nshards)]
+    news = [S.Signal.make(1 << 12, gpu.eng) for _ in range(nshards)]
     levels = sorted(set(int(x) for x in dprio.cpu().numpy().astype(np.int8)))
     ncalls = nprog * cpp
     bounds = [ncalls * s // nshards for s in range(nshards + 1)]
+    cap = int(dcnt.to(torch.int64).sum()) + 64  # generous: no step is void
+    W = cap + 1
     src = []
     for s in range(nshards):
         a, z = bounds[s], bounds[s + 1]
         pairs = torch.full((int(dcnt[a:z].sum()) + 1,), -1, dtype=torch.int64, device=gpu.dev)
         b, sbits, scnew = gpu.batch(ds, dcs[a:z].contiguous(), dcnt[a:z].contiguous(), dprio[a:z].contiguous(),
-                                    new_pairs=pairs)
-        send = torch.empty(ds.numel(), dtype=torch.int64, device=gpu.dev)
-        counts, st = gpu.shard_agg_partition(b, a, levels, nshards, send)
-        assert st["candidates"] == sum(counts) <= st["records"]
-        off = np.concatenate([[0], np.cumsum(counts)])
-        src.append((b, sbits, scnew, pairs, send[: off[-1]], off))
-    # owners: records of every source, in source order
+                                    new_pairs=pairs, want_bits=bits)
+        send = torch.empty(nshards * W, dtype=torch.int64, device=gpu.dev)
+        gpu.step_send(b, a, levels, nshards, cap, send)
+        st = gpu.step_finish()
+        assert not st["global_void"] and not st["src_void"] and st["max_out"] <= cap, st
+        src.append((b, sbits, scnew, pairs, send))
     flags = []
-    for g in range(nshards):
-        recv = torch.cat([x[4][x[5][g]: x[5][g + 1]] for x in src])
-        f = torch.zeros(recv.numel(), dtype=torch.uint8, device=gpu.dev)
-        if recv.numel():
-            gpu.triage_records(shards[g], news[g], recv, levels, f)
+    for g in range(nshards):  # owner g's bucket s is source s's bucket g
+        recv = torch.cat([x[4][g * W: (g + 1) * W] for x in src])
+        f = torch.empty(nshards * W, dtype=torch.uint8, device=gpu.dev)
+        gpu.step_own(shards[g], news[g], recv, nshards, cap, levels, f)
+        ost = gpu.step_finish()
+        assert not ost["global_void"] and not ost["owners_void"], ost
         flags.append(f)
-    got_bits = torch.zeros_like(bits)
-    got_pairs = []
-    for s, (b, sbits, scnew, pairs, send, off) in enumerate(src):
-        lens = [int(off[g + 1] - off[g]) for g in range(nshards)]
-        starts = [sum(int(x[5][g + 1] - x[5][g]) for x in src[:s]) for g in range(nshards)]
-        back = torch.cat([flags[g][starts[g]: starts[g] + lens[g]] for g in range(nshards)])
-        st = gpu.shard_agg_unpartition(b, bounds[s], send, back)
-        got_bits |= sbits
+    got_bits = torch.zeros_like(ref_bits)
+    got_pairs, before = [], 0
+    for s, (b, sbits, scnew, pairs, send) in enumerate(src):
+        back = torch.cat([flags[g][s * W: (s + 1) * W] for g in range(nshards)])
+        gpu.step_back(b, bounds[s], send, nshards, cap, back)
+        bst = gpu.step_finish()
+        assert not bst["global_void"] and not bst["owners_void"], bst
         assert torch.equal(scnew, cnew[bounds[s]: bounds[s + 1]])
-        p = pairs[: st["new_pairs"]].cpu().numpy().view(np.uint64)
+        if bits:
+            got_bits |= sbits
+        # (one context plays every source: the pairs counter keeps running
+        # over the step_back calls, so source s's pairs are [before, after))
+        p = pairs[before: bst["new_pairs"]].cpu().numpy().view(np.uint64)
         got_pairs.append(p + (np.uint64(bounds[s]) << np.uint64(32)))
+        before = bst["new_pairs"]
     torch.cuda.synchronize()
-    assert torch.equal(got_bits, bits)
+    if bits:
+        assert torch.equal(got_bits, ref_bits)
     hs, hcs, hc = ds.cpu().numpy().view(np.uint32), dcs.cpu().numpy().view(np.uint64), dcnt.cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(np.sort(np.concatenate(got_pairs)),
-                                  oracle_pairs(hs, hcs, hc, bits.cpu().numpy().view(np.uint32)))
+                                  oracle_pairs(hs, hcs, hc, ref_bits.cpu().numpy().view(np.uint32)))
     merged = {}
     for g in range(nshards):
         merged.update(shards[g].to_dict())
