@@ -362,10 +362,17 @@ static int poll_sequential(syzsig_ctx* ctx, syzsig_set** max_signal, syzsig_set*
 			nm[f] = nullptr;
 		}
 	}
-	// commit: nothing below fails
+	// commit: nothing below fails.  maxSignal keeps its handle (callers hold
+	// it: the batched path merges in place too), so the clone's contents move
+	// into it; the fuzzers' newMaxSignal handles are replaced, as the batched
+	// path replaces a polled fuzzer's.
 	work.sets.clear();
-	syzsig_set_free(*max_signal);
-	*max_signal = ms;
+	if (*max_signal) {
+		std::swap(**max_signal, *ms);
+		syzsig_set_free(ms);  // (the old storage)
+	} else {
+		*max_signal = ms;  // nil, or allocated by a Merge
+	}
 	for (uint32_t g = 0; g < nfuzzers; g++) {
 		syzsig_set_free(new_max[g]);
 		new_max[g] = nm[g];

@@ -124,7 +124,9 @@ def test_step_routing_equals_unsharded(gpu, nshards, bits):
     src = []
     for s in range(nshards):
         a, z = bounds[s], bounds[s + 1]
-        pairs = torch.full((int(dcnt[a:z].sum()) + 1,), -1, dtype=torch.int64, device=gpu.dev)
+        # (room for the whole batch's pairs: the pairs counter keeps running
+        # over the sources' step_back calls, see below)
+        pairs = torch.full((int(dcnt.to(torch.int64).sum()) + 1,), -1, dtype=torch.int64, device=gpu.dev)
         b, sbits, scnew = gpu.batch(ds, dcs[a:z].contiguous(), dcnt[a:z].contiguous(), dprio[a:z].contiguous(),
                                     new_pairs=pairs, want_bits=bits)
         send = torch.empty(nshards * W, dtype=torch.int64, device=gpu.dev)
