@@ -21,11 +21,12 @@ if [ -n "${TESTS:-}" ]; then
 fi
 A="--steps 10 --warmup 3 --no-cpu --no-min --no-c5 --no-c4 --no-c1 --no-gw --no-pipe --no-poll"
 for rep in 1 2; do
-	for v in ${VARIANTS:-base p1024 w2b w2}; do
+	for v in ${VARIANTS:-base s3a s3b p1024 w2b}; do
 		case $v in
 		base) E="" ;;
 		p1024) E="SYZSIG_AGG_PARTS=1024" ;;
-		*) E="SYZSIG_AGG_PARTS=1024 SYZSIG_LIB=exp/libsyzsig_$v.so" ;;
+		w2|w2b) E="SYZSIG_AGG_PARTS=1024 SYZSIG_LIB=exp/libsyzsig_$v.so" ;;
+		*) E="SYZSIG_LIB=exp/libsyzsig_$v.so" ;;
 		esac
 		step "k3_${v}_$rep" 240 env $E python -u bench.py $A || exit $?
 	done

@@ -86,6 +86,9 @@ constexpr uint32_t kAggGroup = SYZ_AGG_GROUP;  // cells per wave work item of k_
 #define SYZ_AGG_D 2
 #endif
 constexpr uint32_t kAggU = SYZ_AGG_U, kAggD = SYZ_AGG_D;
+#ifndef SYZ_AGG_OVF_EACH  // k_agg tests its overflow flag after every batch (1) or per group of cells (0)
+#define SYZ_AGG_OVF_EACH 1
+#endif
 
 // Partition geometry of one run (see the header).
 struct AggGeom {
@@ -756,6 +759,288 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 		atomicOr(x.bad_level, 1u);
 }
 
+// The lean scatter of triage runs (round 6): the same capped cells and 64-B
+// write-combining blocks, with the per-record bookkeeping of the loads taken
+// out.  A wave walks whole calls (calls w, w + kWaves, .. of its chunk) in
+// tiles of up to kK * 64 records of ONE call: the tile's start, level and
+// serial are wave-uniform scalars (s_load of the call, no LDS call table),
+// so a record costs its load, fmix32, one ds_add_rtn and one ds_write.
+// kSlices = 2: two workgroups per CU (kT = 512 threads each, half the LDS),
+// each placing the records of one half of the partitions of the same chunk
+// (both read every record of the chunk; the pair is scheduled on one XCD,
+// 8 work items apart, so the second read is an L2 hit).
+template <uint32_t kSlices, uint32_t kT, uint32_t kK, uint32_t kWpe, uint32_t kC>
+__global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__ sigs,
+                                                    const uint64_t* __restrict__ call_start,
+                                                    const uint32_t* __restrict__ call_len,
+                                                    const uint8_t* __restrict__ call_prio, LevelMap lm, uint64_t c0,
+                                                    uint64_t c1, AggGeom g, CapCells cc, uint32_t* recs)
+{
+	constexpr uint32_t kWaves = kT / 64, kB = kBlk, kG = 64 / kB, kTile = kK * 64;
+	constexpr uint32_t kMaxP = kAggMaxParts / kSlices;
+	static_assert(kK <= 31 && kC <= 8, "pending masks are 32-bit");
+	__shared__ uint32_t buf[kMaxP * kB];      // per partition: the block being filled
+	__shared__ uint32_t fillc[kMaxP + 1];     // slots handed out in it (may overshoot kB)
+	__shared__ uint32_t written[kMaxP + 1];   // records of the cell written so far (+ a spare)
+	__shared__ uint16_t flist[kMaxP];         // partitions whose block filled this sub-round
+	__shared__ uint32_t nfl[2];               // their count, by sub-round parity
+	__shared__ uint32_t s_or[2][kWaves];
+	__shared__ uint8_t s_lvl[256];            // prio -> level (an LDS read: lgkmcnt, not vmcnt)
+	const uint32_t Pl = (1u << g.pbits) / kSlices, lpbits = g.pbits - (kSlices == 2 ? 1 : 0);
+	// (w through readfirstlane: the compiler then knows the call walk is
+	// wave-uniform and reads the calls with scalar loads, which wait on
+	// lgkmcnt -- a vector load there would need vmcnt(0), draining the
+	// prefetch and the block stores)
+	const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id(), grp = lane / kB,
+	               slot = lane & (kB - 1);
+	uint32_t seq = 0;
+	auto wg_or = [&](bool pred) -> bool {  // workgroup OR in one barrier (k_agg_scatter_blk)
+		uint32_t* r = s_or[seq++ & 1];
+		const bool any = __ballot(pred) != 0;
+		if (lane == 0)
+			r[w] = any;
+		__syncthreads();
+		return __ballot(lane < kWaves && r[lane < kWaves ? lane : 0] != 0) != 0;
+	};
+	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << g.ibits) - 1) >> g.ibits;
+	if (*cc.ovf)
+		return;  // the run is already void
+	bool spilled = false;
+	uint32_t rnd = 0;
+	if (threadIdx.x < 2)
+		nfl[threadIdx.x] = 0;
+	for (uint32_t i = threadIdx.x; i < 256; i += kT)
+		s_lvl[i] = lm.lvl[i];
+	// work items: (chunk, slice); with two slices, items 16k + i and 16k + 8 + i
+	// (i < 8) are the two halves of chunk 8k + i -- the same XCD (blockIdx % 8)
+	const uint64_t nitems = kSlices == 1 ? nchunks : ((nchunks + 7) & ~7ull) * 2;
+	for (uint64_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+		const uint64_t ch = kSlices == 1 ? it : (it >> 4) * 8 + (it & 7);
+		const uint32_t slice = kSlices == 1 ? 0 : (uint32_t)(it >> 3) & 1;
+		if (ch >= nchunks)
+			continue;  // (uniform over the workgroup)
+		const uint64_t cbeg = ch << g.ibits;
+		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << g.ibits);
+		const uint32_t cap = cc.cap[ch];
+		const uint64_t cbase = cc.base[ch];
+		for (uint32_t i = threadIdx.x; i < Pl; i += kT) {
+			fillc[i] = 0;
+			written[i] = 0;
+		}
+		__syncthreads();
+		// this wave's call walk (wave-uniform): call j of the chunk, offset wo
+		uint32_t j = w, wo = 0, clen = 0, cmeta = 0;
+		uint64_t cstart = 0;
+		auto open_call = [&]() {
+			while (j < nc) {
+				const uint64_t c = c0 + cbeg + j;
+				clen = call_len[c];
+				if (clen) {
+					cstart = call_start[c];
+					// the prio byte through a scalar dword load of its aligned word
+					// (a byte load would be a vector load, waited for with vmcnt(0))
+					const uintptr_t pa = (uintptr_t)(call_prio + c);
+					const uint32_t word =
+					    *(const __attribute__((address_space(4))) uint32_t*)(pa & ~(uintptr_t)3);  // (constant: s_load)
+					cmeta = g.meta(s_lvl[(word >> (8 * (pa & 3))) & 0xFF], cbeg + j);
+					return;
+				}
+				j += kWaves;
+			}
+		};
+		open_call();
+		// the next tile's loads: v[] and its scalars (records n, meta); n = 0: none
+		auto fetch = [&](uint32_t (&v)[kK], uint32_t& n, uint32_t& meta) {
+			n = j < nc ? min(kTile, clen - wo) : 0u;
+			meta = cmeta;
+			const uint32_t* src = sigs + cstart + wo;
+			const uint32_t last = n ? n - 1 : 0;
+#pragma unroll
+			for (uint32_t u = 0; u < kK; u++)
+				v[u] = __builtin_nontemporal_load(&src[min(u * 64 + lane, last)]);
+			if (n) {
+				wo += n;
+				if (wo == clen) {
+					wo = 0;
+					j += kWaves;
+					open_call();
+				}
+			}
+		};
+		auto flush = [&]() {
+			const uint32_t nf = nfl[rnd & 1];
+			if (threadIdx.x == 0)
+				nfl[(rnd + 1) & 1] = 0;
+			for (uint32_t jb = 0; jb < nf; jb += 4 * kWaves * kG) {
+				uint32_t pp[4], wr[4], vv[4];
+#pragma unroll
+				for (uint32_t t = 0; t < 4; t++)
+					pp[t] = flist[min(jb + t * kWaves * kG + w * kG + grp, nf - 1)];
+#pragma unroll
+				for (uint32_t t = 0; t < 4; t++) {
+					wr[t] = written[pp[t]];
+					vv[t] = buf[pp[t] * kB + slot];
+				}
+#pragma unroll
+				for (uint32_t t = 0; t < 4; t++) {
+					const bool ok = jb + t * kWaves * kG + w * kG + grp < nf, fits = wr[t] + kB <= cap;
+					spilled |= ok && !fits;
+					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)(slice * Pl + pp[t]) * cap + wr[t]
+					                         : cc.dummy + (blockIdx.x % kDummyLines) * kBlk;
+					d[slot] = vv[t];
+				}
+				__builtin_amdgcn_wave_barrier();
+				if (slot == 0) {
+#pragma unroll
+					for (uint32_t t = 0; t < 4; t++) {
+						const uint32_t q = jb + t * kWaves * kG + w * kG + grp < nf ? pp[t] : kMaxP;
+						written[q] = wr[t] + kB;
+						fillc[q] = 0;
+					}
+				}
+			}
+			rnd++;
+		};
+		auto pack = [&](const uint32_t (&v)[kK], uint32_t n, uint32_t meta, uint32_t (&rec)[kK],
+		                uint32_t (&pt)[kK]) -> uint32_t {
+			uint32_t pend = 0;
+#pragma unroll
+			for (uint32_t u = 0; u < kK; u++) {
+				const uint32_t h = fmix32(v[u]), p = g.part(h);
+				pt[u] = kSlices == 1 ? p : p & (Pl - 1);
+				rec[u] = g.rec(h, meta);
+				const bool mine = kSlices == 1 || (p >> lpbits) == slice;
+				pend |= (uint32_t)(u * 64 + lane < n && mine) << u;
+			}
+			return pend;
+		};
+		auto place = [&](const auto& rec, const auto& pt, uint32_t pend) -> uint32_t {
+			constexpr uint32_t M = sizeof(rec) / sizeof(rec[0]);
+			uint32_t sl[M], full = 0;
+#pragma unroll
+			for (uint32_t u = 0; u < M; u++)
+				sl[u] = (pend >> u) & 1 ? atomicAdd(&fillc[pt[u]], 1u) : kB;
+#pragma unroll
+			for (uint32_t u = 0; u < M; u++) {
+				if (sl[u] < kB) {
+					buf[pt[u] * kB + sl[u]] = rec[u];
+					pend &= ~(1u << u);
+					full |= (uint32_t)(sl[u] == kB - 1) << u;
+				}
+			}
+			while (__ballot(full != 0)) {
+				const bool has = full != 0;
+				const uint32_t cu = __builtin_ctz(full | (1u << M));
+				uint32_t pf = 0;
+#pragma unroll
+				for (uint32_t u = 0; u < M; u++)
+					pf = cu == u ? pt[u] : pf;
+				const uint64_t m = __ballot(has);
+				uint32_t base = 0;
+				if (lane == 0)
+					base = atomicAdd(&nfl[rnd & 1], (uint32_t)__popcll(m));
+				base = __shfl(base, 0, 64);
+				if (has)
+					flist[base + lane_rank(m)] = (uint16_t)pf;
+				full &= full - 1;
+			}
+			return pend;
+		};
+		// Carried records (kC > 0): a tile's records that found their block
+		// full wait in registers for the next tile's sub-round instead of a
+		// second sub-round of their own (two barriers and a flush for ~10 % of
+		// the records), as long as no lane has more than kC of them.
+		uint32_t crec[kC ? kC : 1], cpt[kC ? kC : 1], cpend = 0;
+		auto carry = [&](const uint32_t (&rec)[kK], const uint32_t (&pt)[kK], uint32_t pend) {
+			// pend's records and the still-pending carried ones -> the carry slots
+			uint32_t nc2 = 0;
+#pragma unroll
+			for (uint32_t k = 0; k < kC; k++) {  // compact the carried ones first
+				const bool live = (cpend >> k) & 1;
+#pragma unroll
+				for (uint32_t q = 0; q < kC; q++) {
+					if (q <= k) {  // (a carried record only moves down)
+						crec[q] = live && nc2 == q ? crec[k] : crec[q];
+						cpt[q] = live && nc2 == q ? cpt[k] : cpt[q];
+					}
+				}
+				nc2 += live;
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < kK; u++) {
+				const bool live = (pend >> u) & 1;
+#pragma unroll
+				for (uint32_t q = 0; q < kC; q++) {
+					crec[q] = live && nc2 == q ? rec[u] : crec[q];
+					cpt[q] = live && nc2 == q ? pt[u] : cpt[q];
+				}
+				nc2 += live;
+			}
+			cpend = (1u << nc2) - 1;
+		};
+		// one tile: the carried records and the tile's own in sub-rounds
+		auto tile = [&](const uint32_t (&v)[kK], uint32_t n, uint32_t meta) {
+			uint32_t rec[kK], pt[kK];
+			uint32_t pend = pack(v, n, meta, rec, pt);
+			for (;;) {
+				if (kC)
+					cpend = place(crec, cpt, cpend);
+				pend = place(rec, pt, pend);
+				const uint32_t left = (uint32_t)__popc(pend) + (uint32_t)__popc(cpend);
+				const bool more = wg_or(kC ? left > kC : pend != 0);
+				flush();
+				if (!more) {
+					if (kC)
+						carry(rec, pt, pend);
+					break;
+				}
+				__syncthreads();
+			}
+		};
+		// two register buffers in turn (static indices: the prefetch lands
+		// where it is consumed, no moves that would wait for it)
+		uint32_t va[kK], vb[kK], na, nb, ma, mb;
+		fetch(va, na, ma);
+		for (;;) {
+			fetch(vb, nb, mb);
+			tile(va, na, ma);
+			if (!wg_or(nb != 0 || cpend != 0))  // (its barrier also ends the last flush)
+				break;
+			fetch(va, na, ma);
+			tile(vb, nb, mb);
+			if (!wg_or(na != 0 || cpend != 0))
+				break;
+		}
+		// the chunk's last partial block of every cell of this slice, and the cell counts
+		for (uint32_t p = w * kG + grp; p < Pl; p += kWaves * kG) {
+			const uint32_t c = fillc[p], wr = written[p];
+			const uint32_t pg = slice * Pl + p;
+			if (wr + c > cap)
+				spilled = true;
+			else if (slot < c)
+				recs[cbase + (uint64_t)pg * cap + wr + slot] = buf[p * kB + slot];
+			if (slot == 0)
+				cc.cnt[(uint64_t)pg * cc.nchunks + ch] = min(wr + c, cap);
+		}
+		__syncthreads();  // fillc/written/buf are reset by the next work item
+	}
+	if (spilled)
+		*cc.ovf = 1u;
+}
+
+#ifndef SYZ_SCAT3  // triage runs: 0 = k_agg_scatter_blk, 1 = k_scat3, 2 = k_scat3 in two partition halves
+#define SYZ_SCAT3 0
+#endif
+#ifndef SYZ_SCAT3_K  // records per lane per tile
+#define SYZ_SCAT3_K 16
+#endif
+#ifndef SYZ_SCAT3_C  // records a lane carries to the next tile instead of a second sub-round (0: none)
+#define SYZ_SCAT3_C 0
+#endif
+#ifndef SYZ_SCAT3_T  // threads per workgroup (1024: 4 waves per SIMD, 128 registers; 768: 3, 168; 512: 2, 256)
+#define SYZ_SCAT3_T 1024
+#endif
+
 // The scatter's write-combining blocks fill the same 128 KB of LDS: 64 B per
 // partition at 2048 partitions, whole 128-B lines at <= 1024.
 #ifndef SYZ_SCAT_WIDE
@@ -764,6 +1049,16 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 #ifndef SYZ_SCAT_2WG  // <= 1024 partitions: 64-B blocks, two workgroups per CU (experiment)
 #define SYZ_SCAT_2WG 0
 #endif
+// The triage runs' scatter (kEntry = false): k_scat3 when built with
+// SYZ_SCAT3 (at most kAggMaxParts partitions), else k_agg_scatter_blk.
+static void scatter_triage(uint64_t nchunks, hipStream_t s, uint32_t pbits, const uint32_t* sigs,
+                           const uint64_t* call_start, const uint32_t* call_len, const uint8_t* call_prio, LevelMap lm,
+                           uint64_t c0, uint64_t c1, AggGeom g, AggSrc x, CapCells cc, uint32_t* recs, uint32_t dbg);
+static uint64_t nchunks_of(uint64_t ncalls, uint32_t ibits)
+{
+	return (ncalls + (1ull << ibits) - 1) >> ibits;
+}
+
 template <bool kEntry, typename... A>
 static void scatter_blk(uint32_t grid, hipStream_t s, uint32_t pbits, A... a)
 {
@@ -775,6 +1070,24 @@ static void scatter_blk(uint32_t grid, hipStream_t s, uint32_t pbits, A... a)
 		k_agg_scatter_blk<kEntry, 32><<<grid, kAggThreads, 0, s>>>(a...);
 	else
 		k_agg_scatter_blk<kEntry, 16><<<grid, kAggThreads, 0, s>>>(a...);
+}
+
+static void scatter_triage(uint64_t nchunks, hipStream_t s, uint32_t pbits, const uint32_t* sigs,
+                           const uint64_t* call_start, const uint32_t* call_len, const uint8_t* call_prio, LevelMap lm,
+                           uint64_t c0, uint64_t c1, AggGeom g, AggSrc x, CapCells cc, uint32_t* recs, uint32_t dbg)
+{
+	if (SYZ_SCAT3 == 2 && pbits >= 1) {
+		const uint64_t items = ((nchunks + 7) & ~7ull) * 2;
+		k_scat3<2, 512, SYZ_SCAT3_K, 4, SYZ_SCAT3_C><<<(uint32_t)std::min<uint64_t>(items, 4096), 512, 0, s>>>(
+		    sigs, call_start, call_len, call_prio, lm, c0, c1, g, cc, recs);
+	} else if (SYZ_SCAT3 == 1) {
+		constexpr uint32_t kT = SYZ_SCAT3_T, kWpe = kT / 256;  // one workgroup per CU
+		k_scat3<1, kT, SYZ_SCAT3_K, kWpe, SYZ_SCAT3_C><<<(uint32_t)std::min<uint64_t>(nchunks, 2048), kT, 0, s>>>(
+		    sigs, call_start, call_len, call_prio, lm, c0, c1, g, cc, recs);
+	} else {
+		scatter_blk<false>((uint32_t)std::min<uint64_t>(nchunks, 2048), s, pbits, sigs, call_start, call_len,
+		                   call_prio, lm, c0, c1, g, x, cc, recs, dbg);
+	}
 }
 
 // Capped cells of a run: records per chunk -> cell capacity and chunk base.
@@ -982,6 +1295,10 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 	// resolve the queue: find-or-insert each element, then its level first
 	auto flush_queue = [&]() {
 		uint32_t ins = 0;
+		if (!SYZ_AGG_OVF_EACH && lds_flag(&L.s_ovf)) {  // overflowed: the partition is redone, skip the probes
+			qn = 0;
+			return;
+		}
 		if (lane < qn) {
 			const uint2 e = wq[lane];
 			const uint32_t hb = __umulhi(e.x << g.pbits, kAggBuckets);
@@ -1163,7 +1480,11 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 					fetch(buf[(t + D) % (D + 1)], o0 + D * U * 64);
 					absorb(buf[t], o0);
 					o0 += U * 64;
-					more = o0 < n && !lds_flag(&L.s_ovf);
+					// (the overflow flag is an LDS read, and its wait would also wait
+					// for this batch's ds_min: checked once per group of cells
+					// unless SYZ_AGG_OVF_EACH -- a full table ends every probe
+					// chain at once anyway, agg_find_insert)
+					more = o0 < n && (!SYZ_AGG_OVF_EACH || !lds_flag(&L.s_ovf));
 				}
 			}
 		}
@@ -2032,9 +2353,8 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 		scatter_blk<true>(pg, s, gs.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
 		                                                   c1, gs, *xp, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 	else
-		scatter_blk<false>(pg, s, gs.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
-		                                                    c1, gs, AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs,
-		                                                    ctx->agg_dbg >> 10);
+		scatter_triage(nchunks_of(c1 - c0, gs.ibits), s, gs.pbits, b->sigs, b->call_start, b->call_len, b->call_prio,
+		               lm, c0, c1, gs, AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
@@ -2381,9 +2701,8 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap);
 	}
 	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
-	scatter_blk<false>((uint32_t)std::min<uint64_t>(nchunks, 2048), s, g.pbits,
-	    b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, g, AggSrc{nullptr, 1, 0, 0}, cc,
-	    (uint32_t*)recs, ctx->agg_dbg >> 10);
+	scatter_triage(nchunks, s, g.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, g,
+	               AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
@@ -3011,9 +3330,8 @@ int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial
 		                                              b->nrec, sizes, (uint64_t*)dpart, b->call_new, lm);
 		k_cell_plan_fast<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap, (const uint64_t*)dpart, b->nrec, 0, sc);
 		const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
-		scatter_blk<false>((uint32_t)std::min<uint64_t>(nchunks, 2048), s, g.pbits,
-		    b->sigs, b->call_start, b->call_len, b->call_prio, lm, 0, b->ncalls, g, AggSrc{nullptr, 1, 0, 0}, cc,
-		    (uint32_t*)recs, ctx->agg_dbg >> 10);
+		scatter_triage(nchunks, s, g.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, 0, b->ncalls, g,
+		               AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 		const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),
 		                  ovf, sc};
 		k_agg<kAggU, kAggD, true><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
