@@ -16,7 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run
 echo "[trace] exit $?" | tee -a "$OUT/status.log"
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" ${EXTRA_PMC:-}; do
 	tag=$(echo "$grp" | tr ' ' '_')
-	timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex "${PMC_KERNELS:-k_agg|k_fin|k_ns_def|k_edge|k_min|k_chunk_sizes|k_cell_plan|k_fast_prep|k_count_u8}" -f csv \
+	timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex "${PMC_KERNELS:-k_agg|k_scat3|k_fin|k_ns_def|k_edge|k_min|k_chunk_sizes|k_cell_plan|k_fast_prep|k_count_u8}" -f csv \
 		-d "$OUT/pmc_$tag" -o run -- python3 $CMD $ARGS > "$OUT/pmc_$tag.log" 2>&1
 	rc=$?
 	echo "[pmc $grp] exit $rc" | tee -a "$OUT/status.log"

@@ -86,8 +86,11 @@ constexpr uint32_t kAggGroup = SYZ_AGG_GROUP;  // cells per wave work item of k_
 #define SYZ_AGG_D 2
 #endif
 constexpr uint32_t kAggU = SYZ_AGG_U, kAggD = SYZ_AGG_D;
+#ifndef SYZ_AGG_LEAN  // k_agg walks a group's cells one by one with scalar bases (1) or as one virtual run (0)
+#define SYZ_AGG_LEAN 0
+#endif
 #ifndef SYZ_AGG_OVF_EACH  // k_agg tests its overflow flag after every batch (1) or per group of cells (0)
-#define SYZ_AGG_OVF_EACH 1
+#define SYZ_AGG_OVF_EACH 0
 #endif
 
 // Partition geometry of one run (see the header).
@@ -887,6 +890,9 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 					spilled |= ok && !fits;
 					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)(slice * Pl + pp[t]) * cap + wr[t]
 					                         : cc.dummy + (blockIdx.x % kDummyLines) * kBlk;
+#if defined(SYZ_EXPERIMENTS) && defined(SYZ_SCAT3_DBG)  // timing only: 2 = blocks not stored
+					if (SYZ_SCAT3_DBG != 2)
+#endif
 					d[slot] = vv[t];
 				}
 				__builtin_amdgcn_wave_barrier();
@@ -912,6 +918,10 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 				const bool mine = kSlices == 1 || (p >> lpbits) == slice;
 				pend |= (uint32_t)(u * 64 + lane < n && mine) << u;
 			}
+#if defined(SYZ_EXPERIMENTS) && defined(SYZ_SCAT3_DBG)  // timing only (results wrong): 1 = nothing placed
+			if (SYZ_SCAT3_DBG == 1)
+				pend = 0;
+#endif
 			return pend;
 		};
 		auto place = [&](const auto& rec, const auto& pt, uint32_t pend) -> uint32_t {
@@ -1029,7 +1039,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 }
 
 #ifndef SYZ_SCAT3  // triage runs: 0 = k_agg_scatter_blk, 1 = k_scat3, 2 = k_scat3 in two partition halves
-#define SYZ_SCAT3 0
+#define SYZ_SCAT3 1
 #endif
 #ifndef SYZ_SCAT3_K  // records per lane per tile
 #define SYZ_SCAT3_K 16
@@ -1365,6 +1375,98 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 		const uint32_t n = __builtin_amdgcn_readlane(lvs, gsz - 1);
 		if (n == 0)
 			continue;
+		if constexpr (SYZ_AGG_LEAN) {
+			// Cell by cell: every batch lies in ONE cell, so its base and its
+			// chunk's serial bits are scalars (no per-record cell mapping); a
+			// batch past the cell's end re-reads the cell's last record (a second
+			// copy of a record changes nothing: min is idempotent) and its lanes
+			// are masked.  A scalar cursor (fc, fo) runs D batches ahead across
+			// the group's cells, so the prefetch does not restart per cell.
+			uint32_t fc = 0, fo = 0;
+			auto fetch_l = [&](uint32_t (&bv)[U], uint32_t& nb, uint32_t& sb) {
+				uint32_t len = 0;
+				for (; fc < gsz; fc++, fo = 0) {
+					len = __builtin_amdgcn_readlane(llen, fc);
+					if (fo < len)
+						break;
+				}
+				if (fc >= gsz) {
+					nb = 0;
+					sb = 0;
+					return;
+				}
+				const uint64_t base = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(lbase >> 32), fc) << 32 |
+				                      __builtin_amdgcn_readlane((uint32_t)lbase, fc);
+				nb = min(U * 64, len - fo);
+				sb = (uint32_t)((ch0 + fc) >> ilog) << g.cbits();
+				const uint32_t* src = recs + base + fo;
+				const uint32_t last = nb - 1;
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					bv[u] = __builtin_nontemporal_load(&src[min(u * 64 + lane, last)]);
+				fo += nb;
+			};
+			auto absorb_l = [&](const uint32_t (&bv)[U], uint32_t nb, uint32_t sb) {
+				uint32_t key[U], lv[U], k[U], hb[U], slot[U];
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++) {
+					const uint32_t r = bv[u];
+					k[u] = sb | g.local(r);
+					key[u] = g.resid(r);
+					lv[u] = g.level(r);
+					hb[u] = __umulhi(r & ~((1u << g.pbits) - 1), kAggBuckets);
+				}
+				KBucket B[U];
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					B[u] = kb[hb[u]];
+				bool any_need = false;
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++) {
+					const uint32_t f = bucket_find(B[u], key[u]);
+					const bool valid = u * 64 + lane < nb;
+					slot[u] = f < kAggBW ? hb[u] * kAggBW + f : kAggNoSlot;
+					any_need |= valid && f >= kAggBW;
+				}
+				if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(any_need) != 0))) {
+#pragma unroll
+					for (uint32_t u = 0; u < U; u++) {
+						const bool nd = u * 64 + lane < nb && slot[u] == kAggNoSlot;
+						const uint64_t m = __ballot(nd);
+						if (!m)
+							continue;
+						const uint32_t c = (uint32_t)__popcll(m);
+						if (qn + c > 64)
+							flush_queue();
+						if (nd)
+							wq[qn + lane_rank(m)] = make_uint2(key[u], (lv[u] << 24) | k[u]);
+						qn += c;
+					}
+					__builtin_amdgcn_wave_barrier();
+				}
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					if (u * 64 + lane < nb && slot[u] != kAggNoSlot)
+						atomicMin(&fl[lv[u]][slot[u]], k[u]);
+			};
+			uint32_t bl[D + 1][U], nbl[D + 1], sbl[D + 1];
+#pragma unroll
+			for (uint32_t d = 0; d < D; d++)
+				fetch_l(bl[d], nbl[d], sbl[d]);
+			bool more = nbl[0] != 0;
+			while (more) {
+#pragma unroll
+				for (uint32_t t = 0; t <= D; t++) {
+					if (more) {
+						const uint32_t nx = (t + D) % (D + 1);
+						fetch_l(bl[nx], nbl[nx], sbl[nx]);
+						absorb_l(bl[t], nbl[t], sbl[t]);
+						more = nbl[(t + 1) % (D + 1)] != 0 && (!SYZ_AGG_OVF_EACH || !lds_flag(&L.s_ovf));
+					}
+				}
+			}
+			continue;
+		}
 		lvs -= llen;
 		const uint64_t ldelta = lbase - lvs;
 		const uint32_t nl = n - 1;
