@@ -358,7 +358,49 @@ struct CapCells {
 	uint32_t* ovf;         // set to 1 by a cell overflow
 	uint64_t nchunks;
 	uint32_t* dummy;       // one 64-B line per block: the target of stores that are not made
+	// Two triage scatters over one run (round 6): with split set, k_scat3 takes
+	// the work items its one-call tiles would fill (scat3_takes: sizes[] =
+	// records, tiles[] = k_scat3 tiles per item) and k_agg_scatter_blk the
+	// rest, each skipping the other's items
+	const uint64_t* sizes = nullptr;
+	const uint32_t* tiles = nullptr;
+	bool split = false;
 };
+
+#ifndef SYZ_SCAT3  // triage runs: 0 = k_agg_scatter_blk, 1 = k_scat3, 2 = k_scat3 in two partition halves
+#define SYZ_SCAT3 1
+#endif
+#ifndef SYZ_SCAT3_K  // records per lane per tile
+#define SYZ_SCAT3_K 16
+#endif
+#ifndef SYZ_SCAT3_FB
+#define SYZ_SCAT3_FB 4
+#endif
+#ifndef SYZ_SCAT3_FILL  // % of its tiles' lanes an item must fill for k_scat3 to take it
+#define SYZ_SCAT3_FILL 85
+#endif
+#ifndef SYZ_SCAT3_FL  // the flush list appended with one LDS atomic per wave (1) or per round of filled blocks (0)
+#define SYZ_SCAT3_FL 1
+#endif
+#ifndef SYZ_SCAT3_C  // records a lane carries to the next tile instead of a second sub-round (0: none)
+#define SYZ_SCAT3_C 0
+#endif
+#ifndef SYZ_SCAT3_T  // threads per workgroup (1024: 4 waves per SIMD, 128 registers; 768: 3, 168; 512: 2, 256)
+#define SYZ_SCAT3_T 1024
+#endif
+
+// k_scat3's tiles of one work item (every call in ceil(len / tile) tiles), and
+// the split between the two triage scatters: k_scat3 takes an item whose tiles
+// would be at least SYZ_SCAT3_FILL % full, k_agg_scatter_blk the others.
+constexpr uint32_t kScat3Tile = SYZ_SCAT3_K * 64;
+__host__ __device__ inline uint64_t scat3_tiles(uint32_t len)
+{
+	return (len + kScat3Tile - 1) / kScat3Tile;
+}
+__device__ inline bool scat3_takes(uint64_t recs, uint32_t tiles)
+{
+	return recs * 100 >= (uint64_t)tiles * kScat3Tile * SYZ_SCAT3_FILL;
+}
 
 template <bool kEntry>
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __restrict__ sigs,
@@ -586,6 +628,8 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
 		const uint64_t cbeg = ch << ib;
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
+		if (!kEntry && cc.split && scat3_takes(cc.sizes[ch], cc.tiles[ch]))
+			continue;  // long calls: k_scat3's item
 		const uint32_t cap = cc.cap[ch];
 		const uint64_t cbase = cc.base[ch];
 		for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
@@ -781,6 +825,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 {
 	constexpr uint32_t kWaves = kT / 64, kB = kBlk, kG = 64 / kB, kTile = kK * 64;
 	constexpr uint32_t kMaxP = kAggMaxParts / kSlices;
+	constexpr uint32_t kFB = SYZ_SCAT3_FB;  // blocks per lane group in flight in a flush iteration
 	static_assert(kK <= 31 && kC <= 8, "pending masks are 32-bit");
 	__shared__ uint32_t buf[kMaxP * kB];      // per partition: the block being filled
 	__shared__ uint32_t fillc[kMaxP + 1];     // slots handed out in it (may overshoot kB)
@@ -824,6 +869,8 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 			continue;  // (uniform over the workgroup)
 		const uint64_t cbeg = ch << g.ibits;
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << g.ibits);
+		if (cc.split && !scat3_takes(cc.sizes[ch], cc.tiles[ch]))
+			continue;  // short calls: k_agg_scatter_blk's item
 		const uint32_t cap = cc.cap[ch];
 		const uint64_t cbase = cc.base[ch];
 		for (uint32_t i = threadIdx.x; i < Pl; i += kT) {
@@ -874,18 +921,18 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 			const uint32_t nf = nfl[rnd & 1];
 			if (threadIdx.x == 0)
 				nfl[(rnd + 1) & 1] = 0;
-			for (uint32_t jb = 0; jb < nf; jb += 4 * kWaves * kG) {
-				uint32_t pp[4], wr[4], vv[4];
+			for (uint32_t jb = 0; jb < nf; jb += kFB * kWaves * kG) {
+				uint32_t pp[kFB], wr[kFB], vv[kFB];
 #pragma unroll
-				for (uint32_t t = 0; t < 4; t++)
+				for (uint32_t t = 0; t < kFB; t++)
 					pp[t] = flist[min(jb + t * kWaves * kG + w * kG + grp, nf - 1)];
 #pragma unroll
-				for (uint32_t t = 0; t < 4; t++) {
+				for (uint32_t t = 0; t < kFB; t++) {
 					wr[t] = written[pp[t]];
 					vv[t] = buf[pp[t] * kB + slot];
 				}
 #pragma unroll
-				for (uint32_t t = 0; t < 4; t++) {
+				for (uint32_t t = 0; t < kFB; t++) {
 					const bool ok = jb + t * kWaves * kG + w * kG + grp < nf, fits = wr[t] + kB <= cap;
 					spilled |= ok && !fits;
 					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)(slice * Pl + pp[t]) * cap + wr[t]
@@ -898,7 +945,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 				__builtin_amdgcn_wave_barrier();
 				if (slot == 0) {
 #pragma unroll
-					for (uint32_t t = 0; t < 4; t++) {
+					for (uint32_t t = 0; t < kFB; t++) {
 						const uint32_t q = jb + t * kWaves * kG + w * kG + grp < nf ? pp[t] : kMaxP;
 						written[q] = wr[t] + kB;
 						fillc[q] = 0;
@@ -937,6 +984,32 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 					pend &= ~(1u << u);
 					full |= (uint32_t)(sl[u] == kB - 1) << u;
 				}
+			}
+			if constexpr (SYZ_SCAT3_FL) {
+				// the blocks this lane filled go to the flush list at its offset in
+				// the wave (a prefix sum of the counts through ballots, bit by bit:
+				// no LDS round trip), with one LDS atomic per wave
+				const uint32_t c = (uint32_t)__popc(full);
+				uint32_t pre = 0, tot = 0;
+#pragma unroll
+				for (uint32_t bit = 0; (1u << bit) <= M; bit++) {
+					const uint64_t m = __ballot((c >> bit) & 1);
+					pre += lane_rank(m) << bit;
+					tot += (uint32_t)__popcll(m) << bit;
+				}
+				if (tot) {
+					uint32_t base = 0;
+					if (lane == 0)
+						base = atomicAdd(&nfl[rnd & 1], tot);
+					uint32_t pos = __shfl(base, 0, 64) + pre;
+#pragma unroll
+					for (uint32_t u = 0; u < M; u++) {
+						if ((full >> u) & 1)
+							flist[pos] = (uint16_t)pt[u];
+						pos += (full >> u) & 1;
+					}
+				}
+				return pend;
 			}
 			while (__ballot(full != 0)) {
 				const bool has = full != 0;
@@ -1038,18 +1111,6 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 		*cc.ovf = 1u;
 }
 
-#ifndef SYZ_SCAT3  // triage runs: 0 = k_agg_scatter_blk, 1 = k_scat3, 2 = k_scat3 in two partition halves
-#define SYZ_SCAT3 1
-#endif
-#ifndef SYZ_SCAT3_K  // records per lane per tile
-#define SYZ_SCAT3_K 16
-#endif
-#ifndef SYZ_SCAT3_C  // records a lane carries to the next tile instead of a second sub-round (0: none)
-#define SYZ_SCAT3_C 0
-#endif
-#ifndef SYZ_SCAT3_T  // threads per workgroup (1024: 4 waves per SIMD, 128 registers; 768: 3, 168; 512: 2, 256)
-#define SYZ_SCAT3_T 1024
-#endif
 
 // The scatter's write-combining blocks fill the same 128 KB of LDS: 64 B per
 // partition at 2048 partitions, whole 128-B lines at <= 1024.
@@ -1091,9 +1152,18 @@ static void scatter_triage(uint64_t nchunks, hipStream_t s, uint32_t pbits, cons
 		k_scat3<2, 512, SYZ_SCAT3_K, 4, SYZ_SCAT3_C><<<(uint32_t)std::min<uint64_t>(items, 4096), 512, 0, s>>>(
 		    sigs, call_start, call_len, call_prio, lm, c0, c1, g, cc, recs);
 	} else if (SYZ_SCAT3 == 1) {
+		// k_scat3's tiles hold one call's records: calls a little longer than a
+		// tile leave lanes idle there, so items whose tiles would be less than
+		// SYZ_SCAT3_FILL % full go to k_agg_scatter_blk, decided per item on the
+		// device (both kernels are launched; each skips the other's items)
+		CapCells c2 = cc;
+		c2.split = cc.sizes && cc.tiles;
 		constexpr uint32_t kT = SYZ_SCAT3_T, kWpe = kT / 256;  // one workgroup per CU
 		k_scat3<1, kT, SYZ_SCAT3_K, kWpe, SYZ_SCAT3_C><<<(uint32_t)std::min<uint64_t>(nchunks, 2048), kT, 0, s>>>(
-		    sigs, call_start, call_len, call_prio, lm, c0, c1, g, cc, recs);
+		    sigs, call_start, call_len, call_prio, lm, c0, c1, g, c2, recs);
+		if (c2.split)
+			scatter_blk<false>((uint32_t)std::min<uint64_t>(nchunks, 2048), s, pbits, sigs, call_start, call_len,
+			                   call_prio, lm, c0, c1, g, x, c2, recs, dbg);
 	} else {
 		scatter_blk<false>((uint32_t)std::min<uint64_t>(nchunks, 2048), s, pbits, sigs, call_start, call_len,
 		                   call_prio, lm, c0, c1, g, x, cc, recs, dbg);
@@ -1106,19 +1176,27 @@ static void scatter_triage(uint64_t nchunks, hipStream_t s, uint32_t pbits, cons
 // 1.25 * records + nchunks * P * (sd^2 + 128), an upper bound of the sum
 // (sd * sqrt(m) <= m / 4 + sd^2).
 __global__ __launch_bounds__(256) void k_chunk_sizes(const uint32_t* __restrict__ call_len, uint64_t c0, uint64_t c1,
-                                                     uint32_t cbits, uint64_t* sizes)
+                                                     uint32_t cbits, uint64_t* sizes, uint32_t* tiles)
 {
 	const uint64_t ch = blockIdx.x, cbeg = c0 + (ch << cbits), cend = min<uint64_t>(c1, cbeg + (1ull << cbits));
-	uint64_t s = 0;
-	for (uint64_t c = cbeg + threadIdx.x; c < cend; c += blockDim.x)
+	uint64_t s = 0, t = 0;
+	for (uint64_t c = cbeg + threadIdx.x; c < cend; c += blockDim.x) {
 		s += call_len[c];
+		t += scat3_tiles(call_len[c]);
+	}
 	s = wave_sum_u64(s);
-	__shared__ uint64_t ws[4];
-	if (lane_id() == 0)
-		ws[threadIdx.x >> 6] = s;
+	t = wave_sum_u64(t);
+	__shared__ uint64_t ws[4][2];
+	if (lane_id() == 0) {
+		ws[threadIdx.x >> 6][0] = s;
+		ws[threadIdx.x >> 6][1] = t;
+	}
 	__syncthreads();
-	if (threadIdx.x == 0)
-		sizes[ch] = ws[0] + ws[1] + ws[2] + ws[3];
+	if (threadIdx.x == 0) {
+		sizes[ch] = ws[0][0] + ws[1][0] + ws[2][0] + ws[3][0];
+		if (tiles)
+			tiles[ch] = (uint32_t)min<uint64_t>(ws[0][1] + ws[1][1] + ws[2][1] + ws[3][1], 0xFFFFFFFFu);
+	}
 }
 
 __device__ __forceinline__ void cell_plan(const uint64_t* __restrict__ sizes, uint64_t nchunks, uint32_t P, float sd,
@@ -1174,14 +1252,15 @@ __global__ __launch_bounds__(256) void k_fast_prep(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ call_len,
                                                    const uint8_t* __restrict__ call_prio, uint64_t c0, uint64_t c1,
                                                    uint32_t ibits, uint64_t nrec_space, uint64_t* sizes,
-                                                   uint64_t* part, uint8_t* call_new, LevelMap lm)
+                                                   uint64_t* part, uint8_t* call_new, LevelMap lm, uint32_t* tiles)
 {
 	const uint64_t ch = blockIdx.x, cbeg = c0 + (ch << ibits), cend = min<uint64_t>(c1, cbeg + (1ull << ibits));
-	uint64_t tot = 0, bad = 0, other = 0;
+	uint64_t tot = 0, bad = 0, other = 0, nt = 0;
 	for (uint64_t c = cbeg + threadIdx.x; c < cend; c += blockDim.x) {
 		const uint64_t st = call_start[c];
 		const uint32_t ln = call_len[c];
 		tot += ln;
+		nt += scat3_tiles(ln);
 		bad += st > nrec_space || ln > nrec_space - st || ln > kSerialMask;
 		other |= lm.lvl[call_prio[c]] == 0xff;
 		call_new[c] = 0;
@@ -1189,21 +1268,26 @@ __global__ __launch_bounds__(256) void k_fast_prep(const uint64_t* __restrict__ 
 	tot = wave_sum_u64(tot);
 	bad = wave_sum_u64(bad);
 	other = wave_sum_u64(other);
-	__shared__ uint64_t ws[4][3];
+	nt = wave_sum_u64(nt);
+	__shared__ uint64_t ws[4][4];
 	if (lane_id() == 0) {
 		ws[threadIdx.x >> 6][0] = tot;
 		ws[threadIdx.x >> 6][1] = bad;
 		ws[threadIdx.x >> 6][2] = other;
+		ws[threadIdx.x >> 6][3] = nt;
 	}
 	__syncthreads();
 	if (threadIdx.x == 0) {
-		uint64_t t = 0, b = 0, o = 0;
+		uint64_t t = 0, b = 0, o = 0, tl = 0;
 		for (int w = 0; w < 4; w++) {
 			t += ws[w][0];
 			b += ws[w][1];
 			o += ws[w][2];
+			tl += ws[w][3];
 		}
 		sizes[ch] = t;
+		if (tiles)
+			tiles[ch] = (uint32_t)min<uint64_t>(tl, 0xFFFFFFFFu);
 		part[2 * ch] = t;
 		part[2 * ch + 1] = b | (o ? 1ull << 63 : 0);
 	}
@@ -2434,12 +2518,13 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	const uint64_t bound = run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
 	void *recs, *cm, *de, *df, *dc;
 	SYZ_TRY(ws_get(ctx, 16, (bound + kDummyLines * kBlk) * 4, &recs));
-	SYZ_TRY(ws_get(ctx, 17, nchunks * 20 + (uint64_t)S * nchunks * 4 + 256, &cm));
+	SYZ_TRY(ws_get(ctx, 17, nchunks * 24 + (uint64_t)S * nchunks * 4 + 256, &cm));
 	uint64_t* sizes = (uint64_t*)cm;
 	uint64_t* cbase = sizes + nchunks;
 	uint32_t* ccap = (uint32_t*)(cbase + nchunks);
 	uint32_t* ccnt = ccap + nchunks;
 	uint32_t* ovf = ccnt + (uint64_t)S * nchunks;
+	uint32_t* tiles = ovf + 1;
 	SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 	SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
@@ -2447,9 +2532,9 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
 	SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
-	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, gs.ibits, sizes);
+	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, gs.ibits, sizes, tiles);
 	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, tight ? -1.0f : sd, cbase, ccap);
-	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
+	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound, sizes, tiles};
 	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
 	if (xp)
 		scatter_blk<true>(pg, s, gs.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
@@ -2765,12 +2850,13 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 	const uint64_t bound = run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
 	void *recs, *cm, *dc, *pr, *dd, *dn;
 	SYZ_TRY(ws_get(ctx, 16, (bound + kDummyLines * kBlk) * 4, &recs));
-	SYZ_TRY(ws_get(ctx, 17, nchunks * 20 + (uint64_t)S * nchunks * 4 + 256, &cm));
+	SYZ_TRY(ws_get(ctx, 17, nchunks * 24 + (uint64_t)S * nchunks * 4 + 256, &cm));
 	uint64_t* sizes = (uint64_t*)cm;
 	uint64_t* cbase = sizes + nchunks;
 	uint32_t* ccap = (uint32_t*)(cbase + nchunks);
 	uint32_t* ccnt = ccap + nchunks;
 	uint32_t* ovf = ccnt + (uint64_t)S * nchunks;
+	uint32_t* tiles = ovf + 1;
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
 	if (fast && *npairs_io == 0 && b->new_pairs && b->new_pairs_cap >= 4 * d_max) {
 		pr = b->new_pairs;  // every possible pair fits the caller's buffer: no copy afterwards
@@ -2791,7 +2877,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		SYZ_TRY(ws_get(ctx, 54, nchunks * 16 + 64, &dpart));
 		ovf = (uint32_t*)&ctx->d_cnt[kCntSpill];
 		k_fast_prep<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_start, b->call_len, b->call_prio, c0, c1, g.ibits, b->nrec,
-		                                              sizes, (uint64_t*)dpart, b->call_new, lm);
+		                                              sizes, (uint64_t*)dpart, b->call_new, lm, tiles);
 		k_cell_plan_fast<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap, (const uint64_t*)dpart, run_recs,
 		                                    *npairs_io, ctx->d_cnt);
 	} else {
@@ -2799,10 +2885,10 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		memcpy(ctx->h_pin + kPinPairs, npairs_io, 8);  // consumed before the counters_fetch below
 		SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], ctx->h_pin + kPinPairs, 8, hipMemcpyHostToDevice, s));
 		SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
-		k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.ibits, sizes);
+		k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.ibits, sizes, tiles);
 		k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap);
 	}
-	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
+	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound, sizes, tiles};
 	scatter_triage(nchunks, s, g.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, g,
 	               AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 	SYZ_HIP(hipGetLastError());
@@ -3418,7 +3504,7 @@ int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial
 		const uint64_t bound = b->nrec + b->nrec / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
 		void *recs, *cm, *dc, *de, *df, *dpart;
 		SYZ_TRY(ws_get(ctx, 16, (bound + kDummyLines * kBlk) * 4, &recs));
-		SYZ_TRY(ws_get(ctx, 17, nchunks * 20 + (uint64_t)S * nchunks * 4 + 256, &cm));
+		SYZ_TRY(ws_get(ctx, 17, nchunks * 24 + (uint64_t)S * nchunks * 4 + 256, &cm));
 		SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
 		SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 		SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
@@ -3427,11 +3513,12 @@ int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial
 		uint64_t* cbase = sizes + nchunks;
 		uint32_t* ccap = (uint32_t*)(cbase + nchunks);
 		uint32_t* ccnt = ccap + nchunks;
+		uint32_t* tiles = ccnt + (uint64_t)S * nchunks;
 		uint32_t* ovf = (uint32_t*)&sc[kCntSpill];
 		k_fast_prep<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_start, b->call_len, b->call_prio, 0, b->ncalls, g.ibits,
-		                                              b->nrec, sizes, (uint64_t*)dpart, b->call_new, lm);
+		                                              b->nrec, sizes, (uint64_t*)dpart, b->call_new, lm, tiles);
 		k_cell_plan_fast<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap, (const uint64_t*)dpart, b->nrec, 0, sc);
-		const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound};
+		const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound, sizes, tiles};
 		scatter_triage(nchunks, s, g.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, 0, b->ncalls, g,
 		               AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 		const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),

@@ -554,6 +554,22 @@ int syzsig_set_clone(syzsig_ctx* ctx, const syzsig_set* s, syzsig_set** out)
 	return SYZSIG_OK;
 }
 
+// Whole-table copy (the benchmark's maxSignal reset to M0, 268 MB at C2): one
+// 16-B element per lane over a grid that covers the table, nontemporal -- the
+// form of runtime.hip's k_copy16 that measured 6.2-6.6 TB/s on 1 GiB
+// (DESIGN.md 7), against ~4.4 TB/s for the runtime's device copy.
+#ifndef SYZ_TBL_COPY_KERNEL
+#define SYZ_TBL_COPY_KERNEL 1
+#endif
+typedef uint32_t tbl_v4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_tbl_copy16(const tbl_v4u* __restrict__ src, tbl_v4u* __restrict__ dst,
+                                                    uint64_t n)
+{
+	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+	for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+		__builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
+}
+
 // Whole-table clear as 16-B stores, four per thread (the runtime's fill kernel
 // reaches ~2 TB/s on a 64 MB table, this one ~2.7).
 // Tables are a whole number of 16-B buckets and hipMalloc'd (256-B aligned).
@@ -596,8 +612,15 @@ int syzsig_set_copy_from(syzsig_ctx* ctx, syzsig_set* dst, const syzsig_set* src
 	SYZ_TRY(set_check_idle(src));
 	if (dst->nbuckets != src->nbuckets)
 		return fail(SYZSIG_EINVAL, "set_copy_from: capacity mismatch");
-	SYZ_HIP(hipMemcpyAsync(dst->slots, src->slots, src->nslots() * sizeof(uint64_t), hipMemcpyDeviceToDevice,
-	                       ctx->stream));  // (the runtime's copy: ~4.4 TB/s; a 4 x 16-B-per-thread kernel ran 3.8)
+	const uint64_t n16 = src->nslots() * sizeof(uint64_t) / 16;  // (tables are whole 16-B buckets)
+	if (SYZ_TBL_COPY_KERNEL && n16) {
+		const uint32_t grid = (uint32_t)std::min<uint64_t>((n16 + 255) / 256, 1u << 22);
+		k_tbl_copy16<<<grid, 256, 0, ctx->stream>>>((const tbl_v4u*)src->slots, (tbl_v4u*)dst->slots, n16);
+		SYZ_HIP(hipGetLastError());
+	} else {
+		SYZ_HIP(hipMemcpyAsync(dst->slots, src->slots, src->nslots() * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+		                       ctx->stream));  // (the runtime's copy: ~4.4 TB/s; a 4 x 16-B-per-thread kernel ran 3.8)
+	}
 	dst->len = src->len;
 	return SYZSIG_OK;
 }
