@@ -800,7 +800,8 @@ def dist_parity(dev, sharded, batch, pool0, pairs, reset, ns, m0e, m0p, rank, wo
     reset()
     ns.clear()
     _, cnew, st = sharded.step(batch, pool0[3], rank * P * C)
-    torch.cuda.synchronize()
+    if dev.dev.type == "cuda":
+        torch.cuda.synchronize()
     tot = torch.tensor([ns.Len(), st["changed"], st["new_pairs"], int(cnew.to(torch.int64).sum().item())],
                        dtype=torch.int64, device=cdev)
     dist.all_reduce(tot)

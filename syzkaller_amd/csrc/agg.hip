@@ -379,9 +379,6 @@ struct CapCells {
 #ifndef SYZ_SCAT3_FILL  // % of its tiles' lanes an item must fill for k_scat3 to take it
 #define SYZ_SCAT3_FILL 85
 #endif
-#ifndef SYZ_SCAT3_FL  // the flush list appended with one LDS atomic per wave (1) or per round of filled blocks (0)
-#define SYZ_SCAT3_FL 1
-#endif
 #ifndef SYZ_SCAT3_C  // records a lane carries to the next tile instead of a second sub-round (0: none)
 #define SYZ_SCAT3_C 0
 #endif
@@ -400,6 +397,35 @@ __host__ __device__ inline uint64_t scat3_tiles(uint32_t len)
 __device__ inline bool scat3_takes(uint64_t recs, uint32_t tiles)
 {
 	return recs * 100 >= (uint64_t)tiles * kScat3Tile * SYZ_SCAT3_FILL;
+}
+
+// The blocks a lane filled this sub-round (bit u of full: partition pt[u]) to
+// the flush list with one LDS atomic per wave: each lane's offset is a prefix
+// sum of the lanes' counts through ballots, bit by bit (no LDS round trip),
+// instead of one atomic round per filled block of the busiest lane.
+template <uint32_t M>
+__device__ __forceinline__ void flist_append(uint32_t full, const uint32_t (&pt)[M], uint32_t* nfl, uint16_t* flist)
+{
+	const uint32_t c = (uint32_t)__popc(full);
+	uint32_t pre = 0, tot = 0;
+#pragma unroll
+	for (uint32_t bit = 0; (1u << bit) <= M; bit++) {
+		const uint64_t m = __ballot((c >> bit) & 1);
+		pre += lane_rank(m) << bit;
+		tot += (uint32_t)__popcll(m) << bit;
+	}
+	if (tot) {  // (uniform)
+		uint32_t base = 0;
+		if (lane_id() == 0)
+			base = atomicAdd(nfl, tot);
+		uint32_t pos = __shfl(base, 0, 64) + pre;
+#pragma unroll
+		for (uint32_t u = 0; u < M; u++) {
+			if ((full >> u) & 1)
+				flist[pos] = (uint16_t)pt[u];
+			pos += (full >> u) & 1;
+		}
+	}
 }
 
 template <bool kEntry>
@@ -753,22 +779,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 					full |= (uint32_t)(sl[u] == kB - 1) << u;
 				}
 			}
-			while (__ballot(full != 0)) {
-				const bool has = full != 0;
-				const uint32_t cu = __builtin_ctz(full | (1u << kPer));
-				uint32_t pf = 0;
-#pragma unroll
-				for (uint32_t u = 0; u < kPer; u++)
-					pf = cu == u ? pt[u] : pf;
-				const uint64_t m = __ballot(has);
-				uint32_t base = 0;
-				if (lane == 0)
-					base = atomicAdd(&nfl[rnd & 1], (uint32_t)__popcll(m));
-				base = __shfl(base, 0, 64);
-				if (has)
-					flist[base + lane_rank(m)] = (uint16_t)pf;
-				full &= full - 1;
-			}
+			flist_append(full, pt, &nfl[rnd & 1], flist);
 			return pend;
 		};
 		uint32_t ev[kPer], loc[kPer];
@@ -985,48 +996,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 					full |= (uint32_t)(sl[u] == kB - 1) << u;
 				}
 			}
-			if constexpr (SYZ_SCAT3_FL) {
-				// the blocks this lane filled go to the flush list at its offset in
-				// the wave (a prefix sum of the counts through ballots, bit by bit:
-				// no LDS round trip), with one LDS atomic per wave
-				const uint32_t c = (uint32_t)__popc(full);
-				uint32_t pre = 0, tot = 0;
-#pragma unroll
-				for (uint32_t bit = 0; (1u << bit) <= M; bit++) {
-					const uint64_t m = __ballot((c >> bit) & 1);
-					pre += lane_rank(m) << bit;
-					tot += (uint32_t)__popcll(m) << bit;
-				}
-				if (tot) {
-					uint32_t base = 0;
-					if (lane == 0)
-						base = atomicAdd(&nfl[rnd & 1], tot);
-					uint32_t pos = __shfl(base, 0, 64) + pre;
-#pragma unroll
-					for (uint32_t u = 0; u < M; u++) {
-						if ((full >> u) & 1)
-							flist[pos] = (uint16_t)pt[u];
-						pos += (full >> u) & 1;
-					}
-				}
-				return pend;
-			}
-			while (__ballot(full != 0)) {
-				const bool has = full != 0;
-				const uint32_t cu = __builtin_ctz(full | (1u << M));
-				uint32_t pf = 0;
-#pragma unroll
-				for (uint32_t u = 0; u < M; u++)
-					pf = cu == u ? pt[u] : pf;
-				const uint64_t m = __ballot(has);
-				uint32_t base = 0;
-				if (lane == 0)
-					base = atomicAdd(&nfl[rnd & 1], (uint32_t)__popcll(m));
-				base = __shfl(base, 0, 64);
-				if (has)
-					flist[base + lane_rank(m)] = (uint16_t)pf;
-				full &= full - 1;
-			}
+			flist_append(full, pt, &nfl[rnd & 1], flist);
 			return pend;
 		};
 		// Carried records (kC > 0): a tile's records that found their block
