@@ -295,6 +295,9 @@ def minimize_line(dev, n, mean=2000, U=1 << 22, seed=2018, reps=3, cpu_s=0.0):
 
 
 POLL_BYTES_PER_ENTRY = 5.0  # Poll: a polled (elem u32, prio i8) entry (SURVEY 8(d)'s Minimize-style figure)
+# the batch's kernels (csrc/poll.hip, and recs.hip's grouping); the Serialize of the replies is not among them
+POLL_KERNELS = ("k_poll_recpoll+k_poll_x+k_rp_one_seg+k_rp_count+k_rp_colsum+k_rp_scan+k_rp_coloffs+k_rp_scatter_idx"
+                "+k_poll_part_walk+k_poll_fanout+k_poll_pre+k_poll_count+k_poll_commit+k_poll_scatter")
 
 
 def poll_cpu(e0, p0, polls, F, target_s):
@@ -361,17 +364,21 @@ def poll_line(dev, F=16, K=256, per=16384, fresh=0.05, m0=10_000_000, reps=3, se
     cpu = poll_cpu(e0, p0, polls, F, cpu_s) if cpu_s > 0 else None
     n = K * per
     achieved = POLL_BYTES_PER_ENTRY * n / (dms * 1e-3) / 1e9
+    wl = (f"{K} polls from {F} fuzzers x {per} entries ({fresh:.0%} new, the rest already in maxSignal) vs a "
+          f"{m0}-element maxSignal, one batch (host Serials: upload and replies' Serialize included)")
+    # HBM bytes of the batch's kernels from the newest PMC summary of this line
+    # (the stream time also holds copies and host round trips, so the
+    # profiled kernels' time is not compared with it)
+    traffic, src, note = pmc_traffic(["syz::" + k for k in POLL_KERNELS.split("+")], {"workload": wl}, ("workload",))
     return {"metric": "manager Poll: polled entries/sec (Diff into maxSignal, Merge, fan-out)",
             "value": n / wall, "unit": "entries/s", "higher_is_better": True, "ms": wall * 1e3, "dtype": "u32",
             "library_stream_ms": dms, "cpu": cpu,
-            "config": {"workload": f"{K} polls from {F} fuzzers x {per} entries ({fresh:.0%} new, the rest already in "
-                                   f"maxSignal) vs a {m0}-element maxSignal, one batch (host Serials: upload and "
-                                   "replies' Serialize included)",
-                       "entries": n, "reply_entries": nrep},
+            "config": {"workload": wl, "entries": n, "reply_entries": nrep},
             "roofline": {"bound": "hbm", "kernel": "syzsig_manager_poll_batch's stream work (uploads, kernels, the "
-                                                    "host round trips between; HIP events)",
+                                                    "host round trips between; HIP events); traffic: " + POLL_KERNELS,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "bytes_per_unit": POLL_BYTES_PER_ENTRY, "units_per_launch": n,
+                         "traffic": traffic, "traffic_source": src, "traffic_note": note,
+                         "bytes_per_unit": POLL_BYTES_PER_ENTRY, "units_per_launch": n,
                          "avg_launch_ms": dms}}
 
 
