@@ -86,9 +86,6 @@ constexpr uint32_t kAggGroup = SYZ_AGG_GROUP;  // cells per wave work item of k_
 #define SYZ_AGG_D 2
 #endif
 constexpr uint32_t kAggU = SYZ_AGG_U, kAggD = SYZ_AGG_D;
-#ifndef SYZ_AGG_LEAN  // k_agg walks a group's cells one by one with scalar bases (1) or as one virtual run (0)
-#define SYZ_AGG_LEAN 0
-#endif
 #ifndef SYZ_AGG_OVF_EACH  // k_agg tests its overflow flag after every batch (1) or per group of cells (0)
 #define SYZ_AGG_OVF_EACH 0
 #endif
@@ -1429,98 +1426,6 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 		const uint32_t n = __builtin_amdgcn_readlane(lvs, gsz - 1);
 		if (n == 0)
 			continue;
-		if constexpr (SYZ_AGG_LEAN) {
-			// Cell by cell: every batch lies in ONE cell, so its base and its
-			// chunk's serial bits are scalars (no per-record cell mapping); a
-			// batch past the cell's end re-reads the cell's last record (a second
-			// copy of a record changes nothing: min is idempotent) and its lanes
-			// are masked.  A scalar cursor (fc, fo) runs D batches ahead across
-			// the group's cells, so the prefetch does not restart per cell.
-			uint32_t fc = 0, fo = 0;
-			auto fetch_l = [&](uint32_t (&bv)[U], uint32_t& nb, uint32_t& sb) {
-				uint32_t len = 0;
-				for (; fc < gsz; fc++, fo = 0) {
-					len = __builtin_amdgcn_readlane(llen, fc);
-					if (fo < len)
-						break;
-				}
-				if (fc >= gsz) {
-					nb = 0;
-					sb = 0;
-					return;
-				}
-				const uint64_t base = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(lbase >> 32), fc) << 32 |
-				                      __builtin_amdgcn_readlane((uint32_t)lbase, fc);
-				nb = min(U * 64, len - fo);
-				sb = (uint32_t)((ch0 + fc) >> ilog) << g.cbits();
-				const uint32_t* src = recs + base + fo;
-				const uint32_t last = nb - 1;
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++)
-					bv[u] = __builtin_nontemporal_load(&src[min(u * 64 + lane, last)]);
-				fo += nb;
-			};
-			auto absorb_l = [&](const uint32_t (&bv)[U], uint32_t nb, uint32_t sb) {
-				uint32_t key[U], lv[U], k[U], hb[U], slot[U];
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++) {
-					const uint32_t r = bv[u];
-					k[u] = sb | g.local(r);
-					key[u] = g.resid(r);
-					lv[u] = g.level(r);
-					hb[u] = __umulhi(r & ~((1u << g.pbits) - 1), kAggBuckets);
-				}
-				KBucket B[U];
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++)
-					B[u] = kb[hb[u]];
-				bool any_need = false;
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++) {
-					const uint32_t f = bucket_find(B[u], key[u]);
-					const bool valid = u * 64 + lane < nb;
-					slot[u] = f < kAggBW ? hb[u] * kAggBW + f : kAggNoSlot;
-					any_need |= valid && f >= kAggBW;
-				}
-				if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(any_need) != 0))) {
-#pragma unroll
-					for (uint32_t u = 0; u < U; u++) {
-						const bool nd = u * 64 + lane < nb && slot[u] == kAggNoSlot;
-						const uint64_t m = __ballot(nd);
-						if (!m)
-							continue;
-						const uint32_t c = (uint32_t)__popcll(m);
-						if (qn + c > 64)
-							flush_queue();
-						if (nd)
-							wq[qn + lane_rank(m)] = make_uint2(key[u], (lv[u] << 24) | k[u]);
-						qn += c;
-					}
-					__builtin_amdgcn_wave_barrier();
-				}
-#pragma unroll
-				for (uint32_t u = 0; u < U; u++)
-					if (u * 64 + lane < nb && slot[u] != kAggNoSlot)
-						atomicMin(&fl[lv[u]][slot[u]], k[u]);
-			};
-			uint32_t bl[D + 1][U], nbl[D + 1], sbl[D + 1];
-#pragma unroll
-			for (uint32_t d = 0; d < D; d++)
-				fetch_l(bl[d], nbl[d], sbl[d]);
-			bool more = nbl[0] != 0;
-			while (more) {
-#pragma unroll
-				for (uint32_t t = 0; t <= D; t++) {
-					if (more) {
-						const uint32_t nx = (t + D) % (D + 1);
-						fetch_l(bl[nx], nbl[nx], sbl[nx]);
-						absorb_l(bl[t], nbl[t], sbl[t]);
-						more = nbl[(t + 1) % (D + 1)] != 0 && (!SYZ_AGG_OVF_EACH || !lds_flag(&L.s_ovf));
-					}
-				}
-			}
-			continue;
-		}
 		lvs -= llen;
 		const uint64_t ldelta = lbase - lvs;
 		const uint32_t nl = n - 1;
