@@ -17,7 +17,7 @@ run() {
 }
 for w in ${WHICH:-head min poll c5 c4 rw}; do
 	case $w in
-	head) run r06_prof || exit $? ;;
+	head) run r06_prof BENCH_ARGS="--steps 3 --warmup 1 --no-cpu --no-min --no-c5 --no-c4 --no-c1 --no-gw --no-pipe --no-poll" || exit $? ;;
 	min) run r06_prof_min PROF_CMD=scripts/min_only.py || exit $? ;;
 	poll) run r06_prof_poll PROF_CMD=scripts/line_only.py BENCH_ARGS=poll PMC_KERNELS="k_poll|k_rp_" || exit $? ;;
 	c5) run r06_prof_c5 PROF_CMD=scripts/line_only.py BENCH_ARGS=c5 || exit $? ;;
