@@ -364,7 +364,7 @@ struct CapCells {
 	bool split = false;
 };
 
-#ifndef SYZ_SCAT3  // triage runs: 0 = k_agg_scatter_blk, 1 = k_scat3, 2 = k_scat3 in two partition halves
+#ifndef SYZ_SCAT3  // triage runs: 0 = k_agg_scatter_blk only, 1 = k_scat3 for the items it fills
 #define SYZ_SCAT3 1
 #endif
 #ifndef SYZ_SCAT3_K  // records per lane per tile
@@ -375,9 +375,6 @@ struct CapCells {
 #endif
 #ifndef SYZ_SCAT3_FILL  // % of its tiles' lanes an item must fill for k_scat3 to take it
 #define SYZ_SCAT3_FILL 85
-#endif
-#ifndef SYZ_SCAT3_C  // records a lane carries to the next tile instead of a second sub-round (0: none)
-#define SYZ_SCAT3_C 0
 #endif
 #ifndef SYZ_SCAT3_T  // threads per workgroup (1024: 4 waves per SIMD, 128 registers; 768: 3, 168; 512: 2, 256)
 #define SYZ_SCAT3_T 1024
@@ -820,11 +817,10 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 // tiles of up to kK * 64 records of ONE call: the tile's start, level and
 // serial are wave-uniform scalars (s_load of the call, no LDS call table),
 // so a record costs its load, fmix32, one ds_add_rtn and one ds_write.
-// kSlices = 2: two workgroups per CU (kT = 512 threads each, half the LDS),
-// each placing the records of one half of the partitions of the same chunk
-// (both read every record of the chunk; the pair is scheduled on one XCD,
-// 8 work items apart, so the second read is an L2 hit).
-template <uint32_t kSlices, uint32_t kT, uint32_t kK, uint32_t kWpe, uint32_t kC>
+// Variants measured slower and removed: two
+// workgroups per CU each placing one half of the partitions, and records
+// that met a full block carried in registers to the next tile.
+template <uint32_t kT, uint32_t kK, uint32_t kWpe>
 __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__ sigs,
                                                     const uint64_t* __restrict__ call_start,
                                                     const uint32_t* __restrict__ call_len,
@@ -832,9 +828,9 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
                                                     uint64_t c1, AggGeom g, CapCells cc, uint32_t* recs)
 {
 	constexpr uint32_t kWaves = kT / 64, kB = kBlk, kG = 64 / kB, kTile = kK * 64;
-	constexpr uint32_t kMaxP = kAggMaxParts / kSlices;
+	constexpr uint32_t kMaxP = kAggMaxParts;
 	constexpr uint32_t kFB = SYZ_SCAT3_FB;  // blocks per lane group in flight in a flush iteration
-	static_assert(kK <= 31 && kC <= 8, "pending masks are 32-bit");
+	static_assert(kK <= 31, "pending masks are 32-bit");
 	__shared__ uint32_t buf[kMaxP * kB];      // per partition: the block being filled
 	__shared__ uint32_t fillc[kMaxP + 1];     // slots handed out in it (may overshoot kB)
 	__shared__ uint32_t written[kMaxP + 1];   // records of the cell written so far (+ a spare)
@@ -842,7 +838,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	__shared__ uint32_t nfl[2];               // their count, by sub-round parity
 	__shared__ uint32_t s_or[2][kWaves];
 	__shared__ uint8_t s_lvl[256];            // prio -> level (an LDS read: lgkmcnt, not vmcnt)
-	const uint32_t Pl = (1u << g.pbits) / kSlices, lpbits = g.pbits - (kSlices == 2 ? 1 : 0);
+	const uint32_t Pl = 1u << g.pbits;
 	// (w through readfirstlane: the compiler then knows the call walk is
 	// wave-uniform and reads the calls with scalar loads, which wait on
 	// lgkmcnt -- a vector load there would need vmcnt(0), draining the
@@ -867,14 +863,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 		nfl[threadIdx.x] = 0;
 	for (uint32_t i = threadIdx.x; i < 256; i += kT)
 		s_lvl[i] = lm.lvl[i];
-	// work items: (chunk, slice); with two slices, items 16k + i and 16k + 8 + i
-	// (i < 8) are the two halves of chunk 8k + i -- the same XCD (blockIdx % 8)
-	const uint64_t nitems = kSlices == 1 ? nchunks : ((nchunks + 7) & ~7ull) * 2;
-	for (uint64_t it = blockIdx.x; it < nitems; it += gridDim.x) {
-		const uint64_t ch = kSlices == 1 ? it : (it >> 4) * 8 + (it & 7);
-		const uint32_t slice = kSlices == 1 ? 0 : (uint32_t)(it >> 3) & 1;
-		if (ch >= nchunks)
-			continue;  // (uniform over the workgroup)
+	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {  // work items
 		const uint64_t cbeg = ch << g.ibits;
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << g.ibits);
 		if (cc.split && !scat3_takes(cc.sizes[ch], cc.tiles[ch]))
@@ -943,7 +932,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 				for (uint32_t t = 0; t < kFB; t++) {
 					const bool ok = jb + t * kWaves * kG + w * kG + grp < nf, fits = wr[t] + kB <= cap;
 					spilled |= ok && !fits;
-					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)(slice * Pl + pp[t]) * cap + wr[t]
+					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp[t] * cap + wr[t]
 					                         : cc.dummy + (blockIdx.x % kDummyLines) * kBlk;
 #if defined(SYZ_EXPERIMENTS) && defined(SYZ_SCAT3_DBG)  // timing only: 2 = blocks not stored
 					if (SYZ_SCAT3_DBG != 2)
@@ -968,10 +957,9 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 #pragma unroll
 			for (uint32_t u = 0; u < kK; u++) {
 				const uint32_t h = fmix32(v[u]), p = g.part(h);
-				pt[u] = kSlices == 1 ? p : p & (Pl - 1);
+				pt[u] = p;
 				rec[u] = g.rec(h, meta);
-				const bool mine = kSlices == 1 || (p >> lpbits) == slice;
-				pend |= (uint32_t)(u * 64 + lane < n && mine) << u;
+				pend |= (uint32_t)(u * 64 + lane < n) << u;
 			}
 #if defined(SYZ_EXPERIMENTS) && defined(SYZ_SCAT3_DBG)  // timing only (results wrong): 1 = nothing placed
 			if (SYZ_SCAT3_DBG == 1)
@@ -996,54 +984,16 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 			flist_append(full, pt, &nfl[rnd & 1], flist);
 			return pend;
 		};
-		// Carried records (kC > 0): a tile's records that found their block
-		// full wait in registers for the next tile's sub-round instead of a
-		// second sub-round of their own (two barriers and a flush for ~10 % of
-		// the records), as long as no lane has more than kC of them.
-		uint32_t crec[kC ? kC : 1], cpt[kC ? kC : 1], cpend = 0;
-		auto carry = [&](const uint32_t (&rec)[kK], const uint32_t (&pt)[kK], uint32_t pend) {
-			// pend's records and the still-pending carried ones -> the carry slots
-			uint32_t nc2 = 0;
-#pragma unroll
-			for (uint32_t k = 0; k < kC; k++) {  // compact the carried ones first
-				const bool live = (cpend >> k) & 1;
-#pragma unroll
-				for (uint32_t q = 0; q < kC; q++) {
-					if (q <= k) {  // (a carried record only moves down)
-						crec[q] = live && nc2 == q ? crec[k] : crec[q];
-						cpt[q] = live && nc2 == q ? cpt[k] : cpt[q];
-					}
-				}
-				nc2 += live;
-			}
-#pragma unroll
-			for (uint32_t u = 0; u < kK; u++) {
-				const bool live = (pend >> u) & 1;
-#pragma unroll
-				for (uint32_t q = 0; q < kC; q++) {
-					crec[q] = live && nc2 == q ? rec[u] : crec[q];
-					cpt[q] = live && nc2 == q ? pt[u] : cpt[q];
-				}
-				nc2 += live;
-			}
-			cpend = (1u << nc2) - 1;
-		};
-		// one tile: the carried records and the tile's own in sub-rounds
+		// one tile: place in sub-rounds until every record is in a block
 		auto tile = [&](const uint32_t (&v)[kK], uint32_t n, uint32_t meta) {
 			uint32_t rec[kK], pt[kK];
 			uint32_t pend = pack(v, n, meta, rec, pt);
 			for (;;) {
-				if (kC)
-					cpend = place(crec, cpt, cpend);
 				pend = place(rec, pt, pend);
-				const uint32_t left = (uint32_t)__popc(pend) + (uint32_t)__popc(cpend);
-				const bool more = wg_or(kC ? left > kC : pend != 0);
+				const bool more = wg_or(pend != 0);
 				flush();
-				if (!more) {
-					if (kC)
-						carry(rec, pt, pend);
+				if (!more)
 					break;
-				}
 				__syncthreads();
 			}
 		};
@@ -1054,17 +1004,17 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 		for (;;) {
 			fetch(vb, nb, mb);
 			tile(va, na, ma);
-			if (!wg_or(nb != 0 || cpend != 0))  // (its barrier also ends the last flush)
+			if (!wg_or(nb != 0))  // (its barrier also ends the last flush)
 				break;
 			fetch(va, na, ma);
 			tile(vb, nb, mb);
-			if (!wg_or(na != 0 || cpend != 0))
+			if (!wg_or(na != 0))
 				break;
 		}
-		// the chunk's last partial block of every cell of this slice, and the cell counts
+		// the chunk's last partial block of every cell, and the cell counts
 		for (uint32_t p = w * kG + grp; p < Pl; p += kWaves * kG) {
 			const uint32_t c = fillc[p], wr = written[p];
-			const uint32_t pg = slice * Pl + p;
+			const uint32_t pg = p;
 			if (wr + c > cap)
 				spilled = true;
 			else if (slot < c)
@@ -1084,9 +1034,6 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 #ifndef SYZ_SCAT_WIDE
 #define SYZ_SCAT_WIDE 1
 #endif
-#ifndef SYZ_SCAT_2WG  // <= 1024 partitions: 64-B blocks, two workgroups per CU (experiment)
-#define SYZ_SCAT_2WG 0
-#endif
 // The triage runs' scatter (kEntry = false): k_scat3 when built with
 // SYZ_SCAT3 (at most kAggMaxParts partitions), else k_agg_scatter_blk.
 static void scatter_triage(uint64_t nchunks, hipStream_t s, uint32_t pbits, const uint32_t* sigs,
@@ -1100,11 +1047,7 @@ static uint64_t nchunks_of(uint64_t ncalls, uint32_t ibits)
 template <bool kEntry, typename... A>
 static void scatter_blk(uint32_t grid, hipStream_t s, uint32_t pbits, A... a)
 {
-	if (SYZ_SCAT_2WG == 2 && pbits < kAggMaxBits)  // two 512-thread workgroups per CU
-		k_agg_scatter_blk<kEntry, 16, kAggMaxParts / 2, 4, 512><<<grid, 512, 0, s>>>(a...);
-	else if (SYZ_SCAT_2WG && pbits < kAggMaxBits)
-		k_agg_scatter_blk<kEntry, 16, kAggMaxParts / 2, 8><<<grid, kAggThreads, 0, s>>>(a...);
-	else if (SYZ_SCAT_WIDE && pbits < kAggMaxBits)
+	if (SYZ_SCAT_WIDE && pbits < kAggMaxBits)
 		k_agg_scatter_blk<kEntry, 32><<<grid, kAggThreads, 0, s>>>(a...);
 	else
 		k_agg_scatter_blk<kEntry, 16><<<grid, kAggThreads, 0, s>>>(a...);
@@ -1114,11 +1057,7 @@ static void scatter_triage(uint64_t nchunks, hipStream_t s, uint32_t pbits, cons
                            const uint64_t* call_start, const uint32_t* call_len, const uint8_t* call_prio, LevelMap lm,
                            uint64_t c0, uint64_t c1, AggGeom g, AggSrc x, CapCells cc, uint32_t* recs, uint32_t dbg)
 {
-	if (SYZ_SCAT3 == 2 && pbits >= 1) {
-		const uint64_t items = ((nchunks + 7) & ~7ull) * 2;
-		k_scat3<2, 512, SYZ_SCAT3_K, 4, SYZ_SCAT3_C><<<(uint32_t)std::min<uint64_t>(items, 4096), 512, 0, s>>>(
-		    sigs, call_start, call_len, call_prio, lm, c0, c1, g, cc, recs);
-	} else if (SYZ_SCAT3 == 1) {
+	if (SYZ_SCAT3 == 1) {
 		// k_scat3's tiles hold one call's records: calls a little longer than a
 		// tile leave lanes idle there, so items whose tiles would be less than
 		// SYZ_SCAT3_FILL % full go to k_agg_scatter_blk, decided per item on the
@@ -1126,7 +1065,7 @@ static void scatter_triage(uint64_t nchunks, hipStream_t s, uint32_t pbits, cons
 		CapCells c2 = cc;
 		c2.split = cc.sizes && cc.tiles;
 		constexpr uint32_t kT = SYZ_SCAT3_T, kWpe = kT / 256;  // one workgroup per CU
-		k_scat3<1, kT, SYZ_SCAT3_K, kWpe, SYZ_SCAT3_C><<<(uint32_t)std::min<uint64_t>(nchunks, 2048), kT, 0, s>>>(
+		k_scat3<kT, SYZ_SCAT3_K, kWpe><<<(uint32_t)std::min<uint64_t>(nchunks, 2048), kT, 0, s>>>(
 		    sigs, call_start, call_len, call_prio, lm, c0, c1, g, c2, recs);
 		if (c2.split)
 			scatter_blk<false>((uint32_t)std::min<uint64_t>(nchunks, 2048), s, pbits, sigs, call_start, call_len,
