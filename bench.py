@@ -36,7 +36,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PROBE_BYTES_PER_REC = 12.0  # 4 B element read + 8 B maxSignal slot read
 # the K3 pipeline of one step on one GPU (csrc/agg.hip); roofline.avg_launch_ms is
 # their summed device time (HIP events), roofline.traffic their summed PMC bytes
-K3_KERNELS = "k_fast_prep+k_cell_plan_fast+k_scat3+k_agg+k_agg_finalize_x+k_fin_deferred"
+# (two scatters over one run, each taking the work items the other skips: csrc/agg.hip scatter_triage)
+K3_KERNELS = "k_fast_prep+k_cell_plan_fast+k_scat3+k_agg_scatter_blk+k_agg+k_agg_finalize_x+k_fin_deferred"
 EDGE_BYTES_PER_PC = 12.0  # K1+K2: 8 B u64 PC in + 4 B u32 signal out
 # Minimize's chain on its aggregation path (csrc/minimize.hip header); the
 # keys sort and k_min_calls are negligible (200k contexts)
@@ -44,7 +45,7 @@ MIN_KERNELS = ("k_min_calls+k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg"
                "+k_min_from_dist+k_count_u8")
 MIN_BYTES_PER_ENTRY, MIN_BYTES_PER_DISTINCT = 5.0, 4.0  # Minimize: (elem, prio) entry + covered[e]
 # N > 1: the source's aggregation, then the owner's records-mode triage of the staircases
-K3_DIST_KERNELS = ("k_fast_prep+k_cell_plan_fast+k_scat3+k_agg+k_stair_bucket+k_stair_heads"
+K3_DIST_KERNELS = ("k_fast_prep+k_cell_plan_fast+k_scat3+k_agg_scatter_blk+k_agg+k_stair_bucket+k_stair_heads"
                    "+k_step_heads+k_rp_count+k_rp_colsum+k_rp_scan+k_rp_coloffs+k_rp_scatter+k_rp_agg+k_rp_elems+k_rp_reduce+k_rp_flags+k_step_status"
                    "+k_step_back")
 
