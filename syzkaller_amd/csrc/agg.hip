@@ -362,6 +362,7 @@ struct CapCells {
 	const uint64_t* sizes = nullptr;
 	const uint32_t* tiles = nullptr;
 	bool split = false;
+	uint32_t tile = 1024;  // records per k_scat3 tile the tiles[] were counted in (set with tiles)
 };
 
 #ifndef SYZ_SCAT3  // triage runs: 0 = k_agg_scatter_blk only, 1 = k_scat3 for the items it fills
@@ -371,7 +372,10 @@ struct CapCells {
 #define SYZ_SCAT3_K 16
 #endif
 #ifndef SYZ_SCAT3_FB
-#define SYZ_SCAT3_FB 4
+#define SYZ_SCAT3_FB 2
+#endif
+#ifndef SYZ_SCAT3_ENTRY  // Minimize's work items (one shard) through k_scat3 too, split as for triage
+#define SYZ_SCAT3_ENTRY 0
 #endif
 #ifndef SYZ_SCAT3_FILL  // % of its tiles' lanes an item must fill for k_scat3 to take it
 #define SYZ_SCAT3_FILL 85
@@ -383,14 +387,17 @@ struct CapCells {
 // k_scat3's tiles of one work item (every call in ceil(len / tile) tiles), and
 // the split between the two triage scatters: k_scat3 takes an item whose tiles
 // would be at least SYZ_SCAT3_FILL % full, k_agg_scatter_blk the others.
-constexpr uint32_t kScat3Tile = SYZ_SCAT3_K * 64;
-__host__ __device__ inline uint64_t scat3_tiles(uint32_t len)
+#ifndef SYZ_SCAT3_KE  // records per lane per tile with per-record levels (Minimize: the prios take registers)
+#define SYZ_SCAT3_KE 10
+#endif
+constexpr uint32_t kScat3Tile = SYZ_SCAT3_K * 64, kScat3TileEntry = SYZ_SCAT3_KE * 64;
+__host__ __device__ inline uint64_t scat3_tiles(uint32_t len, uint32_t tile)
 {
-	return (len + kScat3Tile - 1) / kScat3Tile;
+	return (len + tile - 1) / tile;
 }
-__device__ inline bool scat3_takes(uint64_t recs, uint32_t tiles)
+__device__ inline bool scat3_takes(uint64_t recs, uint32_t tiles, uint32_t tile)
 {
-	return recs * 100 >= (uint64_t)tiles * kScat3Tile * SYZ_SCAT3_FILL;
+	return recs * 100 >= (uint64_t)tiles * tile * SYZ_SCAT3_FILL;
 }
 
 // The blocks a lane filled this sub-round (bit u of full: partition pt[u]) to
@@ -648,7 +655,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
 		const uint64_t cbeg = ch << ib;
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
-		if (!kEntry && cc.split && scat3_takes(cc.sizes[ch], cc.tiles[ch]))
+		if (cc.split && scat3_takes(cc.sizes[ch], cc.tiles[ch], cc.tile))
 			continue;  // long calls: k_scat3's item
 		const uint32_t cap = cc.cap[ch];
 		const uint64_t cbase = cc.base[ch];
@@ -820,15 +827,19 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 // Variants measured slower and removed: two
 // workgroups per CU each placing one half of the partitions, and records
 // that met a full block carried in registers to the next tile.
-template <uint32_t kT, uint32_t kK, uint32_t kWpe>
+template <uint32_t kT, uint32_t kK, uint32_t kWpe, bool kEntry = false, uint32_t kB = kBlk>
 __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__ sigs,
                                                     const uint64_t* __restrict__ call_start,
                                                     const uint32_t* __restrict__ call_len,
                                                     const uint8_t* __restrict__ call_prio, LevelMap lm, uint64_t c0,
-                                                    uint64_t c1, AggGeom g, CapCells cc, uint32_t* recs)
+                                                    uint64_t c1, AggGeom g, CapCells cc, uint32_t* recs, AggSrc x)
 {
-	constexpr uint32_t kWaves = kT / 64, kB = kBlk, kG = 64 / kB, kTile = kK * 64;
-	constexpr uint32_t kMaxP = kAggMaxParts;
+	// kEntry (Minimize, one shard): every record's level comes from its own
+	// prio (x.elem_prio, parallel to sigs); kB = 32: 128-B blocks for <= 1024
+	// partitions (the same 128 KB of LDS)
+	constexpr uint32_t kWaves = kT / 64, kG = 64 / kB, kTile = kK * 64;
+	constexpr uint32_t kMaxP = kAggMaxParts * kBlk / kB;
+	static_assert(kB == 16 || kB == 32, "block of 64 or 128 B");
 	constexpr uint32_t kFB = SYZ_SCAT3_FB;  // blocks per lane group in flight in a flush iteration
 	static_assert(kK <= 31, "pending masks are 32-bit");
 	__shared__ uint32_t buf[kMaxP * kB];      // per partition: the block being filled
@@ -857,7 +868,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << g.ibits) - 1) >> g.ibits;
 	if (*cc.ovf)
 		return;  // the run is already void
-	bool spilled = false;
+	bool spilled = false, badlv = false;
 	uint32_t rnd = 0;
 	if (threadIdx.x < 2)
 		nfl[threadIdx.x] = 0;
@@ -866,7 +877,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {  // work items
 		const uint64_t cbeg = ch << g.ibits;
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << g.ibits);
-		if (cc.split && !scat3_takes(cc.sizes[ch], cc.tiles[ch]))
+		if (cc.split && !scat3_takes(cc.sizes[ch], cc.tiles[ch], cc.tile))
 			continue;  // short calls: k_agg_scatter_blk's item
 		const uint32_t cap = cc.cap[ch];
 		const uint64_t cbase = cc.base[ch];
@@ -889,7 +900,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 					const uintptr_t pa = (uintptr_t)(call_prio + c);
 					const uint32_t word =
 					    *(const __attribute__((address_space(4))) uint32_t*)(pa & ~(uintptr_t)3);  // (constant: s_load)
-					cmeta = g.meta(s_lvl[(word >> (8 * (pa & 3))) & 0xFF], cbeg + j);
+					cmeta = g.meta(kEntry ? 0 : s_lvl[(word >> (8 * (pa & 3))) & 0xFF], cbeg + j);
 					return;
 				}
 				j += kWaves;
@@ -897,7 +908,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 		};
 		open_call();
 		// the next tile's loads: v[] and its scalars (records n, meta); n = 0: none
-		auto fetch = [&](uint32_t (&v)[kK], uint32_t& n, uint32_t& meta) {
+		auto fetch = [&](uint32_t (&v)[kK], uint32_t (&pv)[kEntry ? kK : 1], uint32_t& n, uint32_t& meta) {
 			n = j < nc ? min(kTile, clen - wo) : 0u;
 			meta = cmeta;
 			const uint32_t* src = sigs + cstart + wo;
@@ -905,6 +916,12 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 #pragma unroll
 			for (uint32_t u = 0; u < kK; u++)
 				v[u] = __builtin_nontemporal_load(&src[min(u * 64 + lane, last)]);
+			if constexpr (kEntry) {
+				const int8_t* psrc = x.elem_prio + cstart + wo;
+#pragma unroll
+				for (uint32_t u = 0; u < kK; u++)
+					pv[u] = (uint8_t)__builtin_nontemporal_load(&psrc[min(u * 64 + lane, last)]);
+			}
 			if (n) {
 				wo += n;
 				if (wo == clen) {
@@ -933,7 +950,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 					const bool ok = jb + t * kWaves * kG + w * kG + grp < nf, fits = wr[t] + kB <= cap;
 					spilled |= ok && !fits;
 					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp[t] * cap + wr[t]
-					                         : cc.dummy + (blockIdx.x % kDummyLines) * kBlk;
+					                         : cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
 #if defined(SYZ_EXPERIMENTS) && defined(SYZ_SCAT3_DBG)  // timing only: 2 = blocks not stored
 					if (SYZ_SCAT3_DBG != 2)
 #endif
@@ -951,14 +968,20 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 			}
 			rnd++;
 		};
-		auto pack = [&](const uint32_t (&v)[kK], uint32_t n, uint32_t meta, uint32_t (&rec)[kK],
-		                uint32_t (&pt)[kK]) -> uint32_t {
+		auto pack = [&](const uint32_t (&v)[kK], const uint32_t (&pv)[kEntry ? kK : 1], uint32_t n, uint32_t meta,
+		                uint32_t (&rec)[kK], uint32_t (&pt)[kK]) -> uint32_t {
 			uint32_t pend = 0;
 #pragma unroll
 			for (uint32_t u = 0; u < kK; u++) {
 				const uint32_t h = fmix32(v[u]), p = g.part(h);
 				pt[u] = p;
-				rec[u] = g.rec(h, meta);
+				uint32_t m = meta;
+				if constexpr (kEntry) {
+					const uint32_t lv = s_lvl[pv[kEntry ? u : 0]];
+					badlv |= u * 64 + lane < n && lv == 0xff;
+					m |= (lv & 3) << g.cbits();
+				}
+				rec[u] = g.rec(h, m);
 				pend |= (uint32_t)(u * 64 + lane < n) << u;
 			}
 #if defined(SYZ_EXPERIMENTS) && defined(SYZ_SCAT3_DBG)  // timing only (results wrong): 1 = nothing placed
@@ -985,9 +1008,9 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 			return pend;
 		};
 		// one tile: place in sub-rounds until every record is in a block
-		auto tile = [&](const uint32_t (&v)[kK], uint32_t n, uint32_t meta) {
+		auto tile = [&](const uint32_t (&v)[kK], const uint32_t (&pv)[kEntry ? kK : 1], uint32_t n, uint32_t meta) {
 			uint32_t rec[kK], pt[kK];
-			uint32_t pend = pack(v, n, meta, rec, pt);
+			uint32_t pend = pack(v, pv, n, meta, rec, pt);
 			for (;;) {
 				pend = place(rec, pt, pend);
 				const bool more = wg_or(pend != 0);
@@ -999,15 +1022,15 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 		};
 		// two register buffers in turn (static indices: the prefetch lands
 		// where it is consumed, no moves that would wait for it)
-		uint32_t va[kK], vb[kK], na, nb, ma, mb;
-		fetch(va, na, ma);
+		uint32_t va[kK], vb[kK], pa[kEntry ? kK : 1], pb[kEntry ? kK : 1], na, nb, ma, mb;
+		fetch(va, pa, na, ma);
 		for (;;) {
-			fetch(vb, nb, mb);
-			tile(va, na, ma);
+			fetch(vb, pb, nb, mb);
+			tile(va, pa, na, ma);
 			if (!wg_or(nb != 0))  // (its barrier also ends the last flush)
 				break;
-			fetch(va, na, ma);
-			tile(vb, nb, mb);
+			fetch(va, pa, na, ma);
+			tile(vb, pb, nb, mb);
 			if (!wg_or(na != 0))
 				break;
 		}
@@ -1026,6 +1049,8 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	}
 	if (spilled)
 		*cc.ovf = 1u;
+	if (kEntry && x.bad_level && __ballot(badlv) && lane == 0)
+		atomicOr(x.bad_level, 1u);
 }
 
 
@@ -1066,7 +1091,7 @@ static void scatter_triage(uint64_t nchunks, hipStream_t s, uint32_t pbits, cons
 		c2.split = cc.sizes && cc.tiles;
 		constexpr uint32_t kT = SYZ_SCAT3_T, kWpe = kT / 256;  // one workgroup per CU
 		k_scat3<kT, SYZ_SCAT3_K, kWpe><<<(uint32_t)std::min<uint64_t>(nchunks, 2048), kT, 0, s>>>(
-		    sigs, call_start, call_len, call_prio, lm, c0, c1, g, c2, recs);
+		    sigs, call_start, call_len, call_prio, lm, c0, c1, g, c2, recs, x);
 		if (c2.split)
 			scatter_blk<false>((uint32_t)std::min<uint64_t>(nchunks, 2048), s, pbits, sigs, call_start, call_len,
 			                   call_prio, lm, c0, c1, g, x, c2, recs, dbg);
@@ -1082,13 +1107,13 @@ static void scatter_triage(uint64_t nchunks, hipStream_t s, uint32_t pbits, cons
 // 1.25 * records + nchunks * P * (sd^2 + 128), an upper bound of the sum
 // (sd * sqrt(m) <= m / 4 + sd^2).
 __global__ __launch_bounds__(256) void k_chunk_sizes(const uint32_t* __restrict__ call_len, uint64_t c0, uint64_t c1,
-                                                     uint32_t cbits, uint64_t* sizes, uint32_t* tiles)
+                                                     uint32_t cbits, uint64_t* sizes, uint32_t* tiles, uint32_t tile)
 {
 	const uint64_t ch = blockIdx.x, cbeg = c0 + (ch << cbits), cend = min<uint64_t>(c1, cbeg + (1ull << cbits));
 	uint64_t s = 0, t = 0;
 	for (uint64_t c = cbeg + threadIdx.x; c < cend; c += blockDim.x) {
 		s += call_len[c];
-		t += scat3_tiles(call_len[c]);
+		t += scat3_tiles(call_len[c], tile);
 	}
 	s = wave_sum_u64(s);
 	t = wave_sum_u64(t);
@@ -1166,7 +1191,7 @@ __global__ __launch_bounds__(256) void k_fast_prep(const uint64_t* __restrict__ 
 		const uint64_t st = call_start[c];
 		const uint32_t ln = call_len[c];
 		tot += ln;
-		nt += scat3_tiles(ln);
+		nt += scat3_tiles(ln, kScat3Tile);
 		bad += st > nrec_space || ln > nrec_space - st || ln > kSerialMask;
 		other |= lm.lvl[call_prio[c]] == 0xff;
 		call_new[c] = 0;
@@ -2346,11 +2371,25 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[0], s));
 	SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
-	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, gs.ibits, sizes, tiles);
+	const uint32_t tile = xp ? kScat3TileEntry : kScat3Tile;
+	k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, gs.ibits, sizes, tiles, tile);
 	k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, tight ? -1.0f : sd, cbase, ccap);
-	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound, sizes, tiles};
+	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound, sizes, tiles, false, tile};
 	const int pg = (int)std::min<uint64_t>(nchunks, 2048);
-	if (xp)
+	if (xp && SYZ_SCAT3_ENTRY && xp->nshards == 1) {
+		// Minimize: the contexts in rank order (Len desc), so the heavy first
+		// work items fill k_scat3's one-call tiles; the split as for triage
+		CapCells c2 = cc;
+		c2.split = true;
+		if (gs.pbits < kAggMaxBits)
+			k_scat3<kAggThreads, SYZ_SCAT3_KE, 4, true, 32><<<pg, kAggThreads, 0, s>>>(
+			    b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, gs, c2, (uint32_t*)recs, *xp);
+		else
+			k_scat3<kAggThreads, SYZ_SCAT3_KE, 4, true, 16><<<pg, kAggThreads, 0, s>>>(
+			    b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, gs, c2, (uint32_t*)recs, *xp);
+		scatter_blk<true>(pg, s, gs.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, gs, *xp, c2,
+		                  (uint32_t*)recs, ctx->agg_dbg >> 10);
+	} else if (xp)
 		scatter_blk<true>(pg, s, gs.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0,
 		                                                   c1, gs, *xp, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 	else
@@ -2699,10 +2738,10 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		memcpy(ctx->h_pin + kPinPairs, npairs_io, 8);  // consumed before the counters_fetch below
 		SYZ_HIP(hipMemcpyAsync(&ctx->d_cnt[kCntAux2], ctx->h_pin + kPinPairs, 8, hipMemcpyHostToDevice, s));
 		SYZ_HIP(hipMemsetAsync(ovf, 0, 4, s));
-		k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.ibits, sizes, tiles);
+		k_chunk_sizes<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_len, c0, c1, g.ibits, sizes, tiles, kScat3Tile);
 		k_cell_plan<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap);
 	}
-	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound, sizes, tiles};
+	const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound, sizes, tiles, false, kScat3Tile};
 	scatter_triage(nchunks, s, g.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, c0, c1, g,
 	               AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 	SYZ_HIP(hipGetLastError());
@@ -3332,7 +3371,7 @@ int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial
 		k_fast_prep<<<(uint32_t)nchunks, 256, 0, s>>>(b->call_start, b->call_len, b->call_prio, 0, b->ncalls, g.ibits,
 		                                              b->nrec, sizes, (uint64_t*)dpart, b->call_new, lm, tiles);
 		k_cell_plan_fast<<<1, 1024, 0, s>>>(sizes, nchunks, S, sd, cbase, ccap, (const uint64_t*)dpart, b->nrec, 0, sc);
-		const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound, sizes, tiles};
+		const CapCells cc{cbase, ccap, ccnt, ovf, nchunks, (uint32_t*)recs + bound, sizes, tiles, false, kScat3Tile};
 		scatter_triage(nchunks, s, g.pbits, b->sigs, b->call_start, b->call_len, b->call_prio, lm, 0, b->ncalls, g,
 		               AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 		const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),
