@@ -375,7 +375,7 @@ struct CapCells {
 #define SYZ_SCAT3_FB 2
 #endif
 #ifndef SYZ_SCAT3_ENTRY  // Minimize's work items (one shard) through k_scat3 too, split as for triage
-#define SYZ_SCAT3_ENTRY 0
+#define SYZ_SCAT3_ENTRY 1
 #endif
 #ifndef SYZ_SCAT3_FILL  // % of its tiles' lanes an item must fill for k_scat3 to take it
 #define SYZ_SCAT3_FILL 85
