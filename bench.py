@@ -41,7 +41,7 @@ K3_KERNELS = "k_fast_prep+k_cell_plan_fast+k_scat3+k_agg_scatter_blk+k_agg+k_agg
 EDGE_BYTES_PER_PC = 12.0  # K1+K2: 8 B u64 PC in + 4 B u32 signal out
 # Minimize's chain on its aggregation path (csrc/minimize.hip header); the
 # keys sort and k_min_calls are negligible (200k contexts)
-MIN_KERNELS = ("k_min_calls+k_chunk_sizes+k_cell_plan+k_agg_scatter_blk+k_agg"
+MIN_KERNELS = ("k_min_calls+k_chunk_sizes+k_cell_plan+k_scat3+k_agg_scatter_blk+k_agg"
                "+k_min_from_dist+k_count_u8")
 MIN_BYTES_PER_ENTRY, MIN_BYTES_PER_DISTINCT = 5.0, 4.0  # Minimize: (elem, prio) entry + covered[e]
 # N > 1: the source's aggregation, then the owner's records-mode triage of the staircases
