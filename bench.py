@@ -459,7 +459,10 @@ def c5_line(dev, pairs, programs=8192, calls=64, pcs=1024, nbatches=4, reps=3, m
             "config": {"workload": wl,
                        "records": total, "batches": nbatches,
                        "retries": [x["retries"] for x in sts], "runs": [x["runs"] for x in sts],
-                       "new_per_batch": [x["changed"] for x in sts], "distinct": [x["distinct"] for x in sts]},
+                       "new_per_batch": [x["changed"] for x in sts], "distinct": [x["distinct"] for x in sts],
+                       "note": ("SURVEY 8(d)'s global walk reaches every edge of the universe in the first "
+                                "batch, so the later batches find almost nothing new: they time checkNewSignal's "
+                                "DiffRaw with next to no Merge (new_per_batch)") if walk == "global" else None},
             "roofline": {"bound": "hbm", "kernel": K3_KERNELS, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
                          "traffic_note": note,
