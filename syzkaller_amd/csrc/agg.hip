@@ -372,7 +372,7 @@ struct CapCells {
 #define SYZ_SCAT3_K 16
 #endif
 #ifndef SYZ_SCAT3_FB
-#define SYZ_SCAT3_FB 2
+#define SYZ_SCAT3_FB 1
 #endif
 #ifndef SYZ_SCAT3_ENTRY  // Minimize's work items (one shard) through k_scat3 too, split as for triage
 #define SYZ_SCAT3_ENTRY 1
@@ -380,6 +380,13 @@ struct CapCells {
 #ifndef SYZ_SCAT3_FILL  // % of its tiles' lanes an item must fill for k_scat3 to take it
 #define SYZ_SCAT3_FILL 85
 #endif
+#ifndef SYZ_SCAT3_V  // k_scat3's flush: dwords per lane (1, or 4: 16-B lanes)
+#define SYZ_SCAT3_V 4
+#endif
+#ifndef SYZ_SCAT_V  // the same for k_agg_scatter_blk
+#define SYZ_SCAT_V 4
+#endif
+typedef uint32_t scat_v4u __attribute__((ext_vector_type(4)));
 #ifndef SYZ_SCAT3_T  // threads per workgroup (1024: 4 waves per SIMD, 128 registers; 768: 3, 168; 512: 2, 256)
 #define SYZ_SCAT3_T 1024
 #endif
@@ -617,7 +624,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 	constexpr uint32_t kG = 64 / kB;  // blocks a wave writes per store (kB lanes each)
 	static_assert(kB == 16 || kB == 32, "block of 64 or 128 B");
 	constexpr uint32_t kChunkMax = kMaxP / 4;        // calls per chunk (cbits = pbits - 2)
-	__shared__ uint32_t buf[kMaxP * (kMaxP == kAggMaxParts ? kBlk : kB)];  // per partition: the block being filled
+	__shared__ __align__(16) uint32_t buf[kMaxP * (kMaxP == kAggMaxParts ? kBlk : kB)];  // per partition: the block being filled
 	__shared__ uint32_t fillc[kMaxP + 1];   // slots handed out in it (may overshoot kB)
 	__shared__ uint32_t written[kMaxP + 1]; // records of the cell written so far (+ a spare)
 	__shared__ uint16_t flist[kMaxP];       // partitions whose block filled this sub-round
@@ -628,7 +635,11 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 	__shared__ uint8_t s_lvl[kEntry ? 256 : 1];
 	__shared__ uint32_t s_or[2][kWaves];
 	const uint32_t P = 1u << g.pbits, cb = g.cbits(), ib = g.ibits;
-	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), grp = lane / kB, slot = lane & (kB - 1);
+	// the flush: kV dwords per lane (16-B lanes as in k_scat3), kFL blocks per lane group in flight
+	constexpr uint32_t kV = SYZ_SCAT_V, kLB = kB / kV, kGF = 64 / kLB, kFL = 4 / kV;
+	using FV = std::conditional_t<kV == 4, scat_v4u, uint32_t>;
+	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), grp = lane / kB, slot = lane & (kB - 1), fgrp = lane / kLB,
+	               fq = lane % kLB;
 	// Workgroup OR in one barrier (__syncthreads_or takes three): every wave
 	// writes its flag to a row, all read the row; two rows alternate, so a row
 	// is rewritten only after every wave passed the barrier of the call between.
@@ -706,37 +717,38 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 			}
 			return q;
 		};
-		// write out the blocks that filled in this sub-round: 16 lanes per block,
-		// four blocks per lane group in flight
+		// write out the blocks that filled in this sub-round: kLB lanes per block,
+		// kFL blocks per lane group in flight
 		auto flush = [&]() {
 			const uint32_t nf = nfl[rnd & 1];
 			if (threadIdx.x == 0)
 				nfl[(rnd + 1) & 1] = 0;  // the next sub-round's list (last read a sub-round ago)
 			// a uniform loop; a lane group past the list stores its block to this
 			// block's dummy line instead (a store without a branch)
-			for (uint32_t jb = 0; jb < nf; jb += 4 * kWaves * kG) {
-				uint32_t pp[4], wr[4], v[4];
+			for (uint32_t jb = 0; jb < nf; jb += kFL * kWaves * kGF) {
+				uint32_t pp[kFL], wr[kFL];
+				FV v[kFL];
 #pragma unroll
-				for (uint32_t t = 0; t < 4; t++)
-					pp[t] = flist[min(jb + t * kWaves * kG + w * kG + grp, nf - 1)];
+				for (uint32_t t = 0; t < kFL; t++)
+					pp[t] = flist[min(jb + t * kWaves * kGF + w * kGF + fgrp, nf - 1)];
 #pragma unroll
-				for (uint32_t t = 0; t < 4; t++) {
+				for (uint32_t t = 0; t < kFL; t++) {
 					wr[t] = written[pp[t]];
-					v[t] = buf[pp[t] * kB + slot];
+					v[t] = *reinterpret_cast<const FV*>(&buf[pp[t] * kB + fq * kV]);
 				}
 #pragma unroll
-				for (uint32_t t = 0; t < 4; t++) {
-					const bool ok = jb + t * kWaves * kG + w * kG + grp < nf, fits = wr[t] + kB <= cap;
+				for (uint32_t t = 0; t < kFL; t++) {
+					const bool ok = jb + t * kWaves * kGF + w * kGF + fgrp < nf, fits = wr[t] + kB <= cap;
 					spilled |= ok && !fits;  // the cell is full: the run is redone with counted cells
 					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp[t] * cap + wr[t]
 					                         : cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
-					d[slot] = v[t];
+					*reinterpret_cast<FV*>(d + fq * kV) = v[t];
 				}
 				__builtin_amdgcn_wave_barrier();
-				if (slot == 0) {  // (a group past the list updates the spare entry kMaxP)
+				if (fq == 0) {  // (a group past the list updates the spare entry kMaxP)
 #pragma unroll
-					for (uint32_t t = 0; t < 4; t++) {
-						const uint32_t q = jb + t * kWaves * kG + w * kG + grp < nf ? pp[t] : kMaxP;
+					for (uint32_t t = 0; t < kFL; t++) {
+						const uint32_t q = jb + t * kWaves * kGF + w * kGF + fgrp < nf ? pp[t] : kMaxP;
 						written[q] = wr[t] + kB;
 						fillc[q] = 0;
 					}
@@ -824,9 +836,15 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 // tiles of up to kK * 64 records of ONE call: the tile's start, level and
 // serial are wave-uniform scalars (s_load of the call, no LDS call table),
 // so a record costs its load, fmix32, one ds_add_rtn and one ds_write.
+// The kernel is bound by VALU issue (about 1,200 vector instructions per
+// wave and tile of 16 records per lane), so the flush moves 16 B per lane
+// (ds_read_b128, global_store_dwordx4: a quarter of its instructions of 4-B
+// lanes) and the pending mask comes from the record count.
 // Variants measured slower and removed: two
-// workgroups per CU each placing one half of the partitions, and records
-// that met a full block carried in registers to the next tile.
+// workgroups per CU each placing one half of the partitions, records that
+// met a full block carried in registers to the next tile, and one slot claim
+// per record with the claims past a full block written into its next fill
+// (half the barriers, no second claim, but more instructions per tile).
 template <uint32_t kT, uint32_t kK, uint32_t kWpe, bool kEntry = false, uint32_t kB = kBlk>
 __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__ sigs,
                                                     const uint64_t* __restrict__ call_start,
@@ -841,8 +859,13 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	constexpr uint32_t kMaxP = kAggMaxParts * kBlk / kB;
 	static_assert(kB == 16 || kB == 32, "block of 64 or 128 B");
 	constexpr uint32_t kFB = SYZ_SCAT3_FB;  // blocks per lane group in flight in a flush iteration
+	// a flush lane moves kV dwords (4: 16-B LDS reads and block stores, kB / 4
+	// lanes per block -- a quarter of the flush's instructions of 4-B lanes)
+	constexpr uint32_t kV = SYZ_SCAT3_V, kLB = kB / kV, kGF = 64 / kLB;
+	using FV = std::conditional_t<kV == 4, scat_v4u, uint32_t>;
+	static_assert(kV == 1 || kV == 4, "flush lanes of 4 or 16 B");
 	static_assert(kK <= 31, "pending masks are 32-bit");
-	__shared__ uint32_t buf[kMaxP * kB];      // per partition: the block being filled
+	__shared__ __align__(16) uint32_t buf[kMaxP * kB];  // per partition: the block being filled
 	__shared__ uint32_t fillc[kMaxP + 1];     // slots handed out in it (may overshoot kB)
 	__shared__ uint32_t written[kMaxP + 1];   // records of the cell written so far (+ a spare)
 	__shared__ uint16_t flist[kMaxP];         // partitions whose block filled this sub-round
@@ -855,7 +878,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	// lgkmcnt -- a vector load there would need vmcnt(0), draining the
 	// prefetch and the block stores)
 	const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id(), grp = lane / kB,
-	               slot = lane & (kB - 1);
+	               slot = lane & (kB - 1), fgrp = lane / kLB, fq = lane % kLB;
 	uint32_t seq = 0;
 	auto wg_or = [&](bool pred) -> bool {  // workgroup OR in one barrier (k_agg_scatter_blk)
 		uint32_t* r = s_or[seq++ & 1];
@@ -935,32 +958,33 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 			const uint32_t nf = nfl[rnd & 1];
 			if (threadIdx.x == 0)
 				nfl[(rnd + 1) & 1] = 0;
-			for (uint32_t jb = 0; jb < nf; jb += kFB * kWaves * kG) {
-				uint32_t pp[kFB], wr[kFB], vv[kFB];
+			for (uint32_t jb = 0; jb < nf; jb += kFB * kWaves * kGF) {
+				uint32_t pp[kFB], wr[kFB];
+				FV vv[kFB];
 #pragma unroll
 				for (uint32_t t = 0; t < kFB; t++)
-					pp[t] = flist[min(jb + t * kWaves * kG + w * kG + grp, nf - 1)];
+					pp[t] = flist[min(jb + t * kWaves * kGF + w * kGF + fgrp, nf - 1)];
 #pragma unroll
 				for (uint32_t t = 0; t < kFB; t++) {
 					wr[t] = written[pp[t]];
-					vv[t] = buf[pp[t] * kB + slot];
+					vv[t] = *reinterpret_cast<const FV*>(&buf[pp[t] * kB + fq * kV]);
 				}
 #pragma unroll
 				for (uint32_t t = 0; t < kFB; t++) {
-					const bool ok = jb + t * kWaves * kG + w * kG + grp < nf, fits = wr[t] + kB <= cap;
+					const bool ok = jb + t * kWaves * kGF + w * kGF + fgrp < nf, fits = wr[t] + kB <= cap;
 					spilled |= ok && !fits;
 					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp[t] * cap + wr[t]
 					                         : cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
 #if defined(SYZ_EXPERIMENTS) && defined(SYZ_SCAT3_DBG)  // timing only: 2 = blocks not stored
 					if (SYZ_SCAT3_DBG != 2)
 #endif
-					d[slot] = vv[t];
+						*reinterpret_cast<FV*>(d + fq * kV) = vv[t];
 				}
 				__builtin_amdgcn_wave_barrier();
-				if (slot == 0) {
+				if (fq == 0) {
 #pragma unroll
 					for (uint32_t t = 0; t < kFB; t++) {
-						const uint32_t q = jb + t * kWaves * kG + w * kG + grp < nf ? pp[t] : kMaxP;
+						const uint32_t q = jb + t * kWaves * kGF + w * kGF + fgrp < nf ? pp[t] : kMaxP;
 						written[q] = wr[t] + kB;
 						fillc[q] = 0;
 					}
@@ -982,7 +1006,10 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 					m |= (lv & 3) << g.cbits();
 				}
 				rec[u] = g.rec(h, m);
-				pend |= (uint32_t)(u * 64 + lane < n) << u;
+			}
+			{  // records u * 64 + lane < n: the lane's first nu (a mask, not a compare per record)
+				const uint32_t nu = n > lane ? (n - lane + 63) >> 6 : 0u;  // (<= kK <= 31)
+				pend = (1u << nu) - 1;
 			}
 #if defined(SYZ_EXPERIMENTS) && defined(SYZ_SCAT3_DBG)  // timing only (results wrong): 1 = nothing placed
 			if (SYZ_SCAT3_DBG == 1)
@@ -2354,7 +2381,7 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 	float& slack = xp ? ctx->cap_sd_entry : ctx->cap_sd;
 	const float sd = tight ? 0.0f : slack;
 	// upper bound of sum_c S * cap[c] (k_cell_plan): 1.25 records + per cell sd^2 + 128
-	const uint64_t bound = run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
+	const uint64_t bound = (run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 127) & ~63ull;  // (the dummy lines after it: 16-B stores)
 	void *recs, *cm, *de, *df, *dc;
 	SYZ_TRY(ws_get(ctx, 16, (bound + kDummyLines * kBlk) * 4, &recs));
 	SYZ_TRY(ws_get(ctx, 17, nchunks * 24 + (uint64_t)S * nchunks * 4 + 256, &cm));
@@ -2700,7 +2727,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		return SYZSIG_OK;
 	}
 	const float sd = ctx->cap_sd;
-	const uint64_t bound = run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 64;
+	const uint64_t bound = (run_recs + run_recs / 4 + nchunks * S * (uint64_t)(sd * sd + 128.0f) + 127) & ~63ull;  // (the dummy lines after it: 16-B stores)
 	void *recs, *cm, *dc, *pr, *dd, *dn;
 	SYZ_TRY(ws_get(ctx, 16, (bound + kDummyLines * kBlk) * 4, &recs));
 	SYZ_TRY(ws_get(ctx, 17, nchunks * 24 + (uint64_t)S * nchunks * 4 + 256, &cm));
