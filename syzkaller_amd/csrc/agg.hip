@@ -86,6 +86,9 @@ constexpr uint32_t kAggGroup = SYZ_AGG_GROUP;  // cells per wave work item of k_
 #define SYZ_AGG_D 2
 #endif
 constexpr uint32_t kAggU = SYZ_AGG_U, kAggD = SYZ_AGG_D;
+#ifndef SYZ_AGG_RING_EXIT  // k_agg's batch ring left by a jump at the last batch
+#define SYZ_AGG_RING_EXIT 0
+#endif
 #ifndef SYZ_AGG_OVF_EACH  // k_agg tests its overflow flag after every batch (1) or per group of cells (0)
 #define SYZ_AGG_OVF_EACH 0
 #endif
@@ -370,9 +373,6 @@ struct CapCells {
 #endif
 #ifndef SYZ_SCAT3_K  // records per lane per tile
 #define SYZ_SCAT3_K 16
-#endif
-#ifndef SYZ_SCAT3_FB
-#define SYZ_SCAT3_FB 1
 #endif
 #ifndef SYZ_SCAT3_ENTRY  // Minimize's work items (one shard) through k_scat3 too, split as for triage
 #define SYZ_SCAT3_ENTRY 1
@@ -836,10 +836,13 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 // tiles of up to kK * 64 records of ONE call: the tile's start, level and
 // serial are wave-uniform scalars (s_load of the call, no LDS call table),
 // so a record costs its load, fmix32, one ds_add_rtn and one ds_write.
-// The kernel is bound by VALU issue (about 1,200 vector instructions per
-// wave and tile of 16 records per lane), so the flush moves 16 B per lane
+// The kernel was bound by VALU issue (about 1,200 vector instructions per
+// wave and tile of 16 records per lane), so: the flush moves 16 B per lane
 // (ds_read_b128, global_store_dwordx4: a quarter of its instructions of 4-B
-// lanes) and the pending mask comes from the record count.
+// lanes), the pending mask comes from the record count, and no flush list is
+// built while placing (no per-record "block full" test, no list append):
+// after the sub-round's barrier each wave scans the counts of its own share
+// of the partitions and flushes the blocks of its share that filled.
 // Variants measured slower and removed: two
 // workgroups per CU each placing one half of the partitions, records that
 // met a full block carried in registers to the next tile, and one slot claim
@@ -858,7 +861,6 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	constexpr uint32_t kWaves = kT / 64, kG = 64 / kB, kTile = kK * 64;
 	constexpr uint32_t kMaxP = kAggMaxParts * kBlk / kB;
 	static_assert(kB == 16 || kB == 32, "block of 64 or 128 B");
-	constexpr uint32_t kFB = SYZ_SCAT3_FB;  // blocks per lane group in flight in a flush iteration
 	// a flush lane moves kV dwords (4: 16-B LDS reads and block stores, kB / 4
 	// lanes per block -- a quarter of the flush's instructions of 4-B lanes)
 	constexpr uint32_t kV = SYZ_SCAT3_V, kLB = kB / kV, kGF = 64 / kLB;
@@ -868,8 +870,12 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	__shared__ __align__(16) uint32_t buf[kMaxP * kB];  // per partition: the block being filled
 	__shared__ uint32_t fillc[kMaxP + 1];     // slots handed out in it (may overshoot kB)
 	__shared__ uint32_t written[kMaxP + 1];   // records of the cell written so far (+ a spare)
-	__shared__ uint16_t flist[kMaxP];         // partitions whose block filled this sub-round
-	__shared__ uint32_t nfl[2];               // their count, by sub-round parity
+	// No flush list is built while placing: after the sub-round's barrier
+	// every wave scans its own share of the partitions' counts (partition
+	// i * kT + w * 64 + lane) and flushes the blocks of its share that filled,
+	// listed in its own slice of flist
+	constexpr uint32_t kShare = (kMaxP + kT - 1) / kT;  // partitions per lane in the scan
+	__shared__ uint16_t flist[kShare * kT];   // per wave: partitions whose block filled this sub-round
 	__shared__ uint32_t s_or[2][kWaves];
 	__shared__ uint8_t s_lvl[256];            // prio -> level (an LDS read: lgkmcnt, not vmcnt)
 	const uint32_t Pl = 1u << g.pbits;
@@ -892,9 +898,6 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	if (*cc.ovf)
 		return;  // the run is already void
 	bool spilled = false, badlv = false;
-	uint32_t rnd = 0;
-	if (threadIdx.x < 2)
-		nfl[threadIdx.x] = 0;
 	for (uint32_t i = threadIdx.x; i < 256; i += kT)
 		s_lvl[i] = lm.lvl[i];
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {  // work items
@@ -955,42 +958,34 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 			}
 		};
 		auto flush = [&]() {
-			const uint32_t nf = nfl[rnd & 1];
-			if (threadIdx.x == 0)
-				nfl[(rnd + 1) & 1] = 0;
-			for (uint32_t jb = 0; jb < nf; jb += kFB * kWaves * kGF) {
-				uint32_t pp[kFB], wr[kFB];
-				FV vv[kFB];
+			uint16_t* wl = flist + w * kShare * 64;  // this wave's list
+			uint32_t nw = 0;
 #pragma unroll
-				for (uint32_t t = 0; t < kFB; t++)
-					pp[t] = flist[min(jb + t * kWaves * kGF + w * kGF + fgrp, nf - 1)];
-#pragma unroll
-				for (uint32_t t = 0; t < kFB; t++) {
-					wr[t] = written[pp[t]];
-					vv[t] = *reinterpret_cast<const FV*>(&buf[pp[t] * kB + fq * kV]);
-				}
-#pragma unroll
-				for (uint32_t t = 0; t < kFB; t++) {
-					const bool ok = jb + t * kWaves * kGF + w * kGF + fgrp < nf, fits = wr[t] + kB <= cap;
-					spilled |= ok && !fits;
-					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp[t] * cap + wr[t]
-					                         : cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
-#if defined(SYZ_EXPERIMENTS) && defined(SYZ_SCAT3_DBG)  // timing only: 2 = blocks not stored
-					if (SYZ_SCAT3_DBG != 2)
-#endif
-						*reinterpret_cast<FV*>(d + fq * kV) = vv[t];
-				}
+			for (uint32_t i = 0; i < kShare; i++) {
+				const uint32_t p = i * kT + w * 64 + lane;
+				const bool f = p < Pl && fillc[p] >= kB;
+				const uint64_t m = __ballot(f);
+				if (f)
+					wl[nw + lane_rank(m)] = (uint16_t)p;
+				nw += (uint32_t)__popcll(m);
+			}
+			// (the wave's LDS operations run in order: the list is read below as written)
+			for (uint32_t jb = 0; jb < nw; jb += kGF) {
+				const bool ok = jb + fgrp < nw;
+				const uint32_t pp = wl[min(jb + fgrp, nw - 1)];
+				const uint32_t wr = written[pp];
+				const FV vv = *reinterpret_cast<const FV*>(&buf[pp * kB + fq * kV]);
+				const bool fits = wr + kB <= cap;
+				spilled |= ok && !fits;
+				uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp * cap + wr
+				                         : cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
+				*reinterpret_cast<FV*>(d + fq * kV) = vv;
 				__builtin_amdgcn_wave_barrier();
-				if (fq == 0) {
-#pragma unroll
-					for (uint32_t t = 0; t < kFB; t++) {
-						const uint32_t q = jb + t * kWaves * kGF + w * kGF + fgrp < nf ? pp[t] : kMaxP;
-						written[q] = wr[t] + kB;
-						fillc[q] = 0;
-					}
+				if (fq == 0 && ok) {
+					written[pp] = wr + kB;
+					fillc[pp] = 0;
 				}
 			}
-			rnd++;
 		};
 		auto pack = [&](const uint32_t (&v)[kK], const uint32_t (&pv)[kEntry ? kK : 1], uint32_t n, uint32_t meta,
 		                uint32_t (&rec)[kK], uint32_t (&pt)[kK]) -> uint32_t {
@@ -1019,7 +1014,7 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 		};
 		auto place = [&](const auto& rec, const auto& pt, uint32_t pend) -> uint32_t {
 			constexpr uint32_t M = sizeof(rec) / sizeof(rec[0]);
-			uint32_t sl[M], full = 0;
+			uint32_t sl[M];
 #pragma unroll
 			for (uint32_t u = 0; u < M; u++)
 				sl[u] = (pend >> u) & 1 ? atomicAdd(&fillc[pt[u]], 1u) : kB;
@@ -1028,10 +1023,8 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 				if (sl[u] < kB) {
 					buf[pt[u] * kB + sl[u]] = rec[u];
 					pend &= ~(1u << u);
-					full |= (uint32_t)(sl[u] == kB - 1) << u;
 				}
 			}
-			flist_append(full, pt, &nfl[rnd & 1], flist);
 			return pend;
 		};
 		// one tile: place in sub-rounds until every record is in a block
@@ -1463,7 +1456,7 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 		auto absorb = [&](const uint32_t (&buf)[U], uint32_t o0) {
 			uint32_t c0;
 			uint64_t inside;
-			cells(o0, c0, inside);
+			cells(SYZ_AGG_RING_EXIT ? min(o0, nl) : o0, c0, inside);  // (a batch past the group: its last record)
 			uint32_t key[U], lv[U], k[U], hb[U], slot[U], c[U];
 #pragma unroll
 			for (uint32_t u = 0; u < U; u++)
@@ -1524,6 +1517,27 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 #pragma unroll
 		for (uint32_t d = 0; d < D; d++)
 			fetch(buf[d], d * U * 64);
+#if SYZ_AGG_RING_EXIT
+		// Whole rotations of the ring, the exit tested once per rotation: the
+		// batches past the group re-read its last record (absorbing a copy
+		// changes nothing).  An exit test after every batch made the compiler
+		// merge paths whose ring slots differ, and its wait counting then
+		// drained every load in flight (vmcnt(0)) at the top of each rotation.
+		for (uint32_t o0 = 0;;) {
+#pragma unroll
+			for (uint32_t t = 0; t <= D; t++) {
+				fetch(buf[(t + D) % (D + 1)], o0 + (t + D) * U * 64);
+				absorb(buf[t], o0 + t * U * 64);
+			}
+			o0 += (D + 1) * U * 64;
+			if (o0 >= n)
+				break;
+		}
+		// the ring's last prefetches (past the group) are drained here, on the
+		// exit path, so that the next group's ring starts with none of them
+		// outstanding (gfx9 encoding: vmcnt 0, the other counters at maximum)
+		__builtin_amdgcn_s_waitcnt(0x0F70);
+#else
 		bool more = true;
 		for (uint32_t o0 = 0; more;) {
 #pragma unroll
@@ -1540,6 +1554,7 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 				}
 			}
 		}
+#endif
 	}
 	flush_queue();  // every record is absorbed before the barrier
 	__syncthreads();
