@@ -86,9 +86,6 @@ constexpr uint32_t kAggGroup = SYZ_AGG_GROUP;  // cells per wave work item of k_
 #define SYZ_AGG_D 2
 #endif
 constexpr uint32_t kAggU = SYZ_AGG_U, kAggD = SYZ_AGG_D;
-#ifndef SYZ_AGG_RING_EXIT  // k_agg's batch ring left by a jump at the last batch
-#define SYZ_AGG_RING_EXIT 0
-#endif
 #ifndef SYZ_AGG_OVF_EACH  // k_agg tests its overflow flag after every batch (1) or per group of cells (0)
 #define SYZ_AGG_OVF_EACH 0
 #endif
@@ -407,35 +404,6 @@ __device__ inline bool scat3_takes(uint64_t recs, uint32_t tiles, uint32_t tile)
 	return recs * 100 >= (uint64_t)tiles * tile * SYZ_SCAT3_FILL;
 }
 
-// The blocks a lane filled this sub-round (bit u of full: partition pt[u]) to
-// the flush list with one LDS atomic per wave: each lane's offset is a prefix
-// sum of the lanes' counts through ballots, bit by bit (no LDS round trip),
-// instead of one atomic round per filled block of the busiest lane.
-template <uint32_t M>
-__device__ __forceinline__ void flist_append(uint32_t full, const uint32_t (&pt)[M], uint32_t* nfl, uint16_t* flist)
-{
-	const uint32_t c = (uint32_t)__popc(full);
-	uint32_t pre = 0, tot = 0;
-#pragma unroll
-	for (uint32_t bit = 0; (1u << bit) <= M; bit++) {
-		const uint64_t m = __ballot((c >> bit) & 1);
-		pre += lane_rank(m) << bit;
-		tot += (uint32_t)__popcll(m) << bit;
-	}
-	if (tot) {  // (uniform)
-		uint32_t base = 0;
-		if (lane_id() == 0)
-			base = atomicAdd(nfl, tot);
-		uint32_t pos = __shfl(base, 0, 64) + pre;
-#pragma unroll
-		for (uint32_t u = 0; u < M; u++) {
-			if ((full >> u) & 1)
-				flist[pos] = (uint16_t)pt[u];
-			pos += (full >> u) & 1;
-		}
-	}
-}
-
 template <bool kEntry>
 __global__ __launch_bounds__(kAggThreads) void k_agg_scatter(const uint32_t* __restrict__ sigs,
                                                              const uint64_t* __restrict__ call_start,
@@ -627,16 +595,18 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 	__shared__ __align__(16) uint32_t buf[kMaxP * (kMaxP == kAggMaxParts ? kBlk : kB)];  // per partition: the block being filled
 	__shared__ uint32_t fillc[kMaxP + 1];   // slots handed out in it (may overshoot kB)
 	__shared__ uint32_t written[kMaxP + 1]; // records of the cell written so far (+ a spare)
-	__shared__ uint16_t flist[kMaxP];       // partitions whose block filled this sub-round
-	__shared__ uint32_t nfl[2];             // their count, by sub-round parity
+	// full blocks found after the sub-round's barrier by a scan of the counts,
+	// every wave over its own share of the partitions (as in k_scat3)
+	constexpr uint32_t kShare = (kMaxP + kT - 1) / kT;  // partitions per lane in the scan
+	__shared__ uint16_t flist[kShare * kT]; // per wave: partitions whose block filled this sub-round
 	__shared__ uint64_t c_start[kChunkMax]; // the chunk's calls
 	__shared__ uint32_t c_len[kChunkMax];
 	__shared__ uint16_t c_meta[kChunkMax];
 	__shared__ uint8_t s_lvl[kEntry ? 256 : 1];
 	__shared__ uint32_t s_or[2][kWaves];
 	const uint32_t P = 1u << g.pbits, cb = g.cbits(), ib = g.ibits;
-	// the flush: kV dwords per lane (16-B lanes as in k_scat3), kFL blocks per lane group in flight
-	constexpr uint32_t kV = SYZ_SCAT_V, kLB = kB / kV, kGF = 64 / kLB, kFL = 4 / kV;
+	// the flush: kV dwords per lane (16-B lanes as in k_scat3)
+	constexpr uint32_t kV = SYZ_SCAT_V, kLB = kB / kV, kGF = 64 / kLB;
 	using FV = std::conditional_t<kV == 4, scat_v4u, uint32_t>;
 	const uint32_t w = threadIdx.x >> 6, lane = lane_id(), grp = lane / kB, slot = lane & (kB - 1), fgrp = lane / kLB,
 	               fq = lane % kLB;
@@ -660,9 +630,6 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 		for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
 			s_lvl[kEntry ? i : 0] = lm.lvl[i];
 	}
-	uint32_t rnd = 0;  // sub-round parity
-	if (threadIdx.x < 2)
-		nfl[threadIdx.x] = 0;
 	for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
 		const uint64_t cbeg = ch << ib;
 		const uint32_t nc = (uint32_t)min<uint64_t>(ncalls - cbeg, 1ull << ib);
@@ -717,44 +684,37 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 			}
 			return q;
 		};
-		// write out the blocks that filled in this sub-round: kLB lanes per block,
-		// kFL blocks per lane group in flight
+		// write out the blocks of this wave's share that filled in this
+		// sub-round: kLB lanes per block
 		auto flush = [&]() {
-			const uint32_t nf = nfl[rnd & 1];
-			if (threadIdx.x == 0)
-				nfl[(rnd + 1) & 1] = 0;  // the next sub-round's list (last read a sub-round ago)
-			// a uniform loop; a lane group past the list stores its block to this
-			// block's dummy line instead (a store without a branch)
-			for (uint32_t jb = 0; jb < nf; jb += kFL * kWaves * kGF) {
-				uint32_t pp[kFL], wr[kFL];
-				FV v[kFL];
+			uint16_t* wl = flist + w * kShare * 64;  // this wave's list
+			uint32_t nw = 0;
 #pragma unroll
-				for (uint32_t t = 0; t < kFL; t++)
-					pp[t] = flist[min(jb + t * kWaves * kGF + w * kGF + fgrp, nf - 1)];
-#pragma unroll
-				for (uint32_t t = 0; t < kFL; t++) {
-					wr[t] = written[pp[t]];
-					v[t] = *reinterpret_cast<const FV*>(&buf[pp[t] * kB + fq * kV]);
-				}
-#pragma unroll
-				for (uint32_t t = 0; t < kFL; t++) {
-					const bool ok = jb + t * kWaves * kGF + w * kGF + fgrp < nf, fits = wr[t] + kB <= cap;
-					spilled |= ok && !fits;  // the cell is full: the run is redone with counted cells
-					uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp[t] * cap + wr[t]
-					                         : cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
-					*reinterpret_cast<FV*>(d + fq * kV) = v[t];
-				}
+			for (uint32_t i = 0; i < kShare; i++) {
+				const uint32_t p = i * kT + w * 64 + lane;
+				const bool f = p < P && fillc[p] >= kB;
+				const uint64_t m = __ballot(f);
+				if (f)
+					wl[nw + lane_rank(m)] = (uint16_t)p;
+				nw += (uint32_t)__popcll(m);
+			}
+			// (the wave's LDS operations run in order: the list is read below as written)
+			for (uint32_t jb = 0; jb < nw; jb += kGF) {
+				const bool ok = jb + fgrp < nw;
+				const uint32_t pp = wl[min(jb + fgrp, nw - 1)];
+				const uint32_t wr = written[pp];
+				const FV v = *reinterpret_cast<const FV*>(&buf[pp * kB + fq * kV]);
+				const bool fits = wr + kB <= cap;
+				spilled |= ok && !fits;  // the cell is full: the run is redone with counted cells
+				uint32_t* d = ok && fits ? recs + cbase + (uint64_t)pp * cap + wr
+				                         : cc.dummy + (blockIdx.x % (kDummyLines * kBlk / kB)) * kB;
+				*reinterpret_cast<FV*>(d + fq * kV) = v;
 				__builtin_amdgcn_wave_barrier();
-				if (fq == 0) {  // (a group past the list updates the spare entry kMaxP)
-#pragma unroll
-					for (uint32_t t = 0; t < kFL; t++) {
-						const uint32_t q = jb + t * kWaves * kGF + w * kGF + fgrp < nf ? pp[t] : kMaxP;
-						written[q] = wr[t] + kB;
-						fillc[q] = 0;
-					}
+				if (fq == 0 && ok) {
+					written[pp] = wr + kB;
+					fillc[pp] = 0;
 				}
 			}
-			rnd++;
 		};
 		// a tile's records: packed record and partition, and the mask of those to place
 		auto pack = [&](const uint32_t (&ev)[kPer], const uint32_t (&loc)[kPer], uint32_t n, uint32_t (&rec)[kPer],
@@ -777,10 +737,10 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 			return dbg & 2 ? 0u : pend;  // dbg & 2: timing only, records loaded and dropped
 		};
 		// one placement pass: a slot in each record's partition block (all slot
-		// requests in flight together), or it waits for the block's flush; the
-		// blocks this lane filled go to the flush list.  Returns what is left.
+		// requests in flight together), or it waits for the block's flush.
+		// Returns what is left.
 		auto place = [&](const uint32_t (&rec)[kPer], const uint32_t (&pt)[kPer], uint32_t pend) -> uint32_t {
-			uint32_t sl[kPer], full = 0;
+			uint32_t sl[kPer];
 #pragma unroll
 			for (uint32_t u = 0; u < kPer; u++)
 				sl[u] = (pend >> u) & 1 ? atomicAdd(&fillc[pt[u]], 1u) : kB;
@@ -789,10 +749,8 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 				if (sl[u] < kB) {
 					buf[pt[u] * kB + sl[u]] = rec[u];
 					pend &= ~(1u << u);
-					full |= (uint32_t)(sl[u] == kB - 1) << u;
 				}
 			}
-			flist_append(full, pt, &nfl[rnd & 1], flist);
 			return pend;
 		};
 		uint32_t ev[kPer], loc[kPer];
@@ -1456,7 +1414,7 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 		auto absorb = [&](const uint32_t (&buf)[U], uint32_t o0) {
 			uint32_t c0;
 			uint64_t inside;
-			cells(SYZ_AGG_RING_EXIT ? min(o0, nl) : o0, c0, inside);  // (a batch past the group: its last record)
+			cells(o0, c0, inside);
 			uint32_t key[U], lv[U], k[U], hb[U], slot[U], c[U];
 #pragma unroll
 			for (uint32_t u = 0; u < U; u++)
@@ -1517,27 +1475,6 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 #pragma unroll
 		for (uint32_t d = 0; d < D; d++)
 			fetch(buf[d], d * U * 64);
-#if SYZ_AGG_RING_EXIT
-		// Whole rotations of the ring, the exit tested once per rotation: the
-		// batches past the group re-read its last record (absorbing a copy
-		// changes nothing).  An exit test after every batch made the compiler
-		// merge paths whose ring slots differ, and its wait counting then
-		// drained every load in flight (vmcnt(0)) at the top of each rotation.
-		for (uint32_t o0 = 0;;) {
-#pragma unroll
-			for (uint32_t t = 0; t <= D; t++) {
-				fetch(buf[(t + D) % (D + 1)], o0 + (t + D) * U * 64);
-				absorb(buf[t], o0 + t * U * 64);
-			}
-			o0 += (D + 1) * U * 64;
-			if (o0 >= n)
-				break;
-		}
-		// the ring's last prefetches (past the group) are drained here, on the
-		// exit path, so that the next group's ring starts with none of them
-		// outstanding (gfx9 encoding: vmcnt 0, the other counters at maximum)
-		__builtin_amdgcn_s_waitcnt(0x0F70);
-#else
 		bool more = true;
 		for (uint32_t o0 = 0; more;) {
 #pragma unroll
@@ -1554,7 +1491,6 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 				}
 			}
 		}
-#endif
 	}
 	flush_queue();  // every record is absorbed before the barrier
 	__syncthreads();
