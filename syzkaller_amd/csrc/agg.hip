@@ -380,9 +380,6 @@ struct CapCells {
 #ifndef SYZ_SCAT3_V  // k_scat3's flush: dwords per lane (1, or 4: 16-B lanes)
 #define SYZ_SCAT3_V 4
 #endif
-#ifndef SYZ_SCAT3_DEFER  // k_scat3: blocks filled by a tile's later sub-rounds flushed with the next tile's
-#define SYZ_SCAT3_DEFER 0
-#endif
 #ifndef SYZ_SCAT_V  // the same for k_agg_scatter_blk
 #define SYZ_SCAT_V 4
 #endif
@@ -836,7 +833,6 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 	// i * kT + w * 64 + lane) and flushes the blocks of its share that filled,
 	// listed in its own slice of flist
 	constexpr uint32_t kShare = (kMaxP + kT - 1) / kT;  // partitions per lane in the scan
-	constexpr bool kDefer = SYZ_SCAT3_DEFER;
 	__shared__ uint16_t flist[kShare * kT];   // per wave: partitions whose block filled this sub-round
 	__shared__ uint32_t s_or[2][kWaves];
 	__shared__ uint8_t s_lvl[256];            // prio -> level (an LDS read: lgkmcnt, not vmcnt)
@@ -855,15 +851,6 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 			r[w] = any;
 		__syncthreads();
 		return __ballot(lane < kWaves && r[lane < kWaves ? lane : 0] != 0) != 0;
-	};
-	auto wg_or2 = [&](bool a, bool b) -> uint32_t {  // two workgroup ORs in one barrier
-		uint32_t* r = s_or[seq++ & 1];
-		const uint32_t any = (__ballot(a) != 0) | (uint32_t)(__ballot(b) != 0) << 1;
-		if (lane == 0)
-			r[w] = any;
-		__syncthreads();
-		const uint32_t x = lane < kWaves ? r[lane] : 0u;
-		return (__ballot(x & 1) != 0) | (uint32_t)(__ballot(x & 2) != 0) << 1;
 	};
 	const uint64_t ncalls = c1 - c0, nchunks = (ncalls + (1ull << g.ibits) - 1) >> g.ibits;
 	if (*cc.ovf)
@@ -1011,50 +998,19 @@ __global__ __launch_bounds__(kT, kWpe) void k_scat3(const uint32_t* __restrict__
 				__syncthreads();
 			}
 		};
-		// kDefer: the workgroup OR of each sub-round also carries whether
-		// another tile follows, and the blocks filled by a tile's later
-		// sub-rounds are left for the next tile's first flush (its scan finds
-		// them full; the next tile's claims on them overflow and wait) -- no
-		// flush and no barrier of their own.  Returns whether a tile follows.
-		auto tile_d = [&](const uint32_t (&v)[kK], const uint32_t (&pv)[kEntry ? kK : 1], uint32_t n, uint32_t meta,
-		                  bool next) -> bool {
-			uint32_t rec[kK], pt[kK];
-			uint32_t pend = pack(v, pv, n, meta, rec, pt);
-			for (bool first = true;; first = false) {
-				pend = place(rec, pt, pend);
-				const uint32_t f = wg_or2(pend != 0, next);
-				if (!first && !(f & 1))
-					return (f & 2) != 0;
-				flush();
-				__syncthreads();  // the flush's count resets land before the next claims
-				if (!(f & 1))
-					return (f & 2) != 0;
-			}
-		};
 		// two register buffers in turn (static indices: the prefetch lands
 		// where it is consumed, no moves that would wait for it)
 		uint32_t va[kK], vb[kK], pa[kEntry ? kK : 1], pb[kEntry ? kK : 1], na, nb, ma, mb;
 		fetch(va, pa, na, ma);
-		if constexpr (kDefer) {
-			for (;;) {
-				fetch(vb, pb, nb, mb);
-				if (!tile_d(va, pa, na, ma, nb != 0))
-					break;
-				fetch(va, pa, na, ma);
-				if (!tile_d(vb, pb, nb, mb, na != 0))
-					break;
-			}
-		} else {
-			for (;;) {
-				fetch(vb, pb, nb, mb);
-				tile(va, pa, na, ma);
-				if (!wg_or(nb != 0))  // (its barrier also ends the last flush)
-					break;
-				fetch(va, pa, na, ma);
-				tile(vb, pb, nb, mb);
-				if (!wg_or(na != 0))
-					break;
-			}
+		for (;;) {
+			fetch(vb, pb, nb, mb);
+			tile(va, pa, na, ma);
+			if (!wg_or(nb != 0))  // (its barrier also ends the last flush)
+				break;
+			fetch(va, pa, na, ma);
+			tile(vb, pb, nb, mb);
+			if (!wg_or(na != 0))
+				break;
 		}
 		// the chunk's last partial block of every cell, and the cell counts
 		for (uint32_t p = w * kG + grp; p < Pl; p += kWaves * kG) {
