@@ -1279,7 +1279,7 @@ struct AggCells {
 // Aggregate partition p into the LDS table (every thread of the workgroup;
 // ends with a barrier).  Returns false when its distinct elements overflow
 // the table (s_ovf).
-template <uint32_t U, uint32_t D, bool kCap>
+template <uint32_t U, uint32_t D, bool kCap, bool kIdx32>
 __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCells& x, const AggGeom& g)
 {
 	KBucket* kb = L.kb;
@@ -1392,6 +1392,28 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 			uint32_t c0;
 			uint64_t inside;
 			cells(min(o0, nl), c0, inside);  // a prefetch past the group reads its last record
+			if constexpr (kIdx32) {
+				// every cell lies below record 2^32 (host-checked): 32-bit record
+				// indices, the cell deltas taken mod 2^32 (v + delta is the index)
+				const uint32_t d0 = __builtin_amdgcn_readlane((uint32_t)ldelta, c0);
+				uint32_t v[U], d[U];
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++) {
+					v[u] = min(o0 + u * 64 + lane, nl);
+					d[u] = d0;
+				}
+				for (uint64_t m = inside; m; m &= m - 1) {
+					const uint32_t j = __builtin_ctzll(m), vs = __builtin_amdgcn_readlane(lvs, j);
+					const uint32_t dj = __builtin_amdgcn_readlane((uint32_t)ldelta, j);
+#pragma unroll
+					for (uint32_t u = 0; u < U; u++)
+						d[u] = v[u] >= vs ? dj : d[u];
+				}
+#pragma unroll
+				for (uint32_t u = 0; u < U; u++)
+					buf[u] = __builtin_nontemporal_load(&recs[v[u] + d[u]]);
+				return;
+			}
 			const uint64_t d0 = delta_of(c0);
 			uint32_t v[U];
 			uint64_t d[U];
@@ -1507,7 +1529,7 @@ __device__ __forceinline__ bool agg_partition(AggLds& L, uint32_t p, const AggCe
 // dist_*[p * kAggRegion ...], cnt[p] = how many, or kAggOverflow when they do
 // not fit the LDS table.
 // U records per lane per batch, D batches in flight ahead of the one absorbed.
-template <uint32_t U, uint32_t D, bool kCap>
+template <uint32_t U, uint32_t D, bool kCap, bool kIdx32 = false>
 __global__ __launch_bounds__(kAggThreads) void k_agg(AggCells x, AggGeom g, uint32_t* dist_e, uint4* dist_f,
                                                      uint32_t* cnt)
 {
@@ -1517,7 +1539,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(AggCells x, AggGeom g, uint
 	if (x.spill && *x.spill)
 		return;  // a cell spilled: the records are incomplete and the run is redone
 	for (uint32_t p = blockIdx.x; p < P; p += gridDim.x) {
-		if (!agg_partition<U, D, kCap>(L, p, x, g)) {
+		if (!agg_partition<U, D, kCap, kIdx32>(L, p, x, g)) {
 			if (threadIdx.x == 0) {
 				cnt[p] = kAggOverflow;
 				if (x.ctr)
@@ -1551,6 +1573,18 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(AggCells x, AggGeom g, uint
 		}
 		__syncthreads();
 	}
+}
+
+// k_agg over records [0, extent): 32-bit record indices when they fit (fewer
+// vector instructions per record: 1.45 -> 1.40 ms at C2)
+template <bool kCap>
+static void launch_agg(uint64_t extent, uint32_t P, hipStream_t s, const AggCells& xc, const AggGeom& g, void* de,
+                       void* df, void* dc)
+{
+	if (extent <= (1ull << 32))
+		k_agg<kAggU, kAggD, kCap, true><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	else
+		k_agg<kAggU, kAggD, kCap, false><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 }
 
 // ---- fallback: partitions whose distinct elements overflow the LDS table are
@@ -2378,7 +2412,7 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
 	const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, gs.items_per_chunk_log2(),
 	                  agg_group_size(nchunks)};
-	k_agg<kAggU, kAggD, true><<<P, kAggThreads, 0, s>>>(xc, gs, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	launch_agg<true>(bound, P, s, xc, gs, de, df, dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -2490,7 +2524,7 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
 	const AggCells xc{(const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr, nchunks, 0,
 	                  agg_group_size(nchunks)};
-	k_agg<kAggU, kAggD, false><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+	launch_agg<false>(run_recs, P, s, xc, g, de, df, dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -2758,7 +2792,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		void *de, *df;
 		SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 		SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
-		k_agg<kAggU, kAggD, true><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+		launch_agg<true>(bound, P, s, xc, g, de, df, dc);
 		SYZ_HIP(hipGetLastError());
 		if (ctx->timing)
 			SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -3354,7 +3388,7 @@ int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial
 		               AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 		const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),
 		                  ovf, sc};
-		k_agg<kAggU, kAggD, true><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
+		launch_agg<true>(bound, P, s, xc, g, de, df, dc);
 		k_stair_bucket<<<(int)std::min<uint32_t>(P, 2048), 256, 0, s>>>(
 		    (const uint32_t*)de, (const uint4*)df, (const uint32_t*)dc, P, lm.n, nshards, serial_base, cap, cursor,
 		    d_send, sc);
