@@ -96,6 +96,8 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
  * SYZSIG_DEBUG_EDGE_MARKALL / SYZSIG_DEBUG_EDGE_PASSES = syzsig_edge_derive_dev
  * runs the dedup rounds with one marking pass / with marking passes, instead
  * of choosing from the previous launch's duplicate rate.
+ * SYZSIG_DEBUG_AGG_IDX64 = the aggregation reads its records with 64-bit
+ * indices, the path of runs whose cells reach past record 2^32 (tests).
  * Fault injection (an error, never a wrong result):
  * SYZSIG_DEBUG_POLL_FAIL = the sequential Poll loop (syzsig_manager_poll_batch's
  * exact fallback) fails with SYZSIG_EIO before its last poll, so tests can
@@ -108,6 +110,7 @@ int syzsig_ctx_set_agg(syzsig_ctx* ctx, int mode, uint32_t parts);
 #define SYZSIG_DEBUG_EDGE_MARKALL 1024u
 #define SYZSIG_DEBUG_EDGE_PASSES 2048u
 #define SYZSIG_DEBUG_POLL_FAIL 4096u
+#define SYZSIG_DEBUG_AGG_IDX64 8192u
 int syzsig_ctx_set_debug(syzsig_ctx* ctx, uint32_t flags);
 
 /* ---- pkg/signal/signal.go ---- */

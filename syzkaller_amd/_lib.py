@@ -24,6 +24,7 @@ SYZSIG_DEBUG_RECS_GATE = 512
 SYZSIG_DEBUG_EDGE_MARKALL = 1024
 SYZSIG_DEBUG_EDGE_PASSES = 2048
 SYZSIG_DEBUG_POLL_FAIL = 4096
+SYZSIG_DEBUG_AGG_IDX64 = 8192
 
 
 class SyzsigError(RuntimeError):

@@ -734,7 +734,12 @@ __global__ __launch_bounds__(kT, kWpe) void k_agg_scatter_blk(const uint32_t* __
 				rec[u] = g.rec(h, meta);
 				pend |= (uint32_t)(u * 64 + lane < n && keep) << u;
 			}
+#ifdef SYZ_EXPERIMENTS
 			return dbg & 2 ? 0u : pend;  // dbg & 2: timing only, records loaded and dropped
+#else
+			// (the bit is SYZSIG_DEBUG_EDGE_PASSES >> 10 in product builds: ignored here)
+			return pend;
+#endif
 		};
 		// one placement pass: a slot in each record's partition block (all slot
 		// requests in flight together), or it waits for the block's flush.
@@ -1576,12 +1581,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg(AggCells x, AggGeom g, uint
 }
 
 // k_agg over records [0, extent): 32-bit record indices when they fit (fewer
-// vector instructions per record: 1.45 -> 1.40 ms at C2)
+// vector instructions per record: 1.45 -> 1.40 ms at C2; the
+// 64-bit kernel for larger runs, and under SYZSIG_DEBUG_AGG_IDX64 for tests)
 template <bool kCap>
-static void launch_agg(uint64_t extent, uint32_t P, hipStream_t s, const AggCells& xc, const AggGeom& g, void* de,
-                       void* df, void* dc)
+static void launch_agg(const syzsig_ctx* ctx, uint64_t extent, uint32_t P, hipStream_t s, const AggCells& xc,
+                       const AggGeom& g, void* de, void* df, void* dc)
 {
-	if (extent <= (1ull << 32))
+	if (extent <= (1ull << 32) && !(ctx->agg_dbg & SYZSIG_DEBUG_AGG_IDX64))
 		k_agg<kAggU, kAggD, kCap, true><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
 	else
 		k_agg<kAggU, kAggD, kCap, false><<<P, kAggThreads, 0, s>>>(xc, g, (uint32_t*)de, (uint4*)df, (uint32_t*)dc);
@@ -2412,7 +2418,7 @@ static int agg_capped(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint6
 		SYZ_HIP(hipEventRecord(ctx->ev[1], s));
 	const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, gs.items_per_chunk_log2(),
 	                  agg_group_size(nchunks)};
-	launch_agg<true>(bound, P, s, xc, gs, de, df, dc);
+	launch_agg<true>(ctx, bound, P, s, xc, gs, de, df, dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -2524,7 +2530,7 @@ int agg_aggregate(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t c0, uint64_t 
 	SYZ_TRY(ws_get(ctx, 21, (uint64_t)(P + 1) * 4 + 64, &dc));
 	const AggCells xc{(const uint32_t*)recs, rec_base, offsT, nullptr, nullptr, nullptr, nchunks, 0,
 	                  agg_group_size(nchunks)};
-	launch_agg<false>(run_recs, P, s, xc, g, de, df, dc);
+	launch_agg<false>(ctx, run_recs, P, s, xc, g, de, df, dc);
 	SYZ_HIP(hipGetLastError());
 	if (ctx->timing)
 		SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -2792,7 +2798,7 @@ static int agg_triage_fused(syzsig_ctx* ctx, syzsig_set* ms, syzsig_set** ns, co
 		void *de, *df;
 		SYZ_TRY(ws_get(ctx, 19, (uint64_t)P * kAggRegion * 4 + 64, &de));
 		SYZ_TRY(ws_get(ctx, 20, (uint64_t)P * kAggRegion * 16 + 64, &df));
-		launch_agg<true>(bound, P, s, xc, g, de, df, dc);
+		launch_agg<true>(ctx, bound, P, s, xc, g, de, df, dc);
 		SYZ_HIP(hipGetLastError());
 		if (ctx->timing)
 			SYZ_HIP(hipEventRecord(ctx->ev[2], s));
@@ -3388,7 +3394,7 @@ int syzsig_step_send_dev(syzsig_ctx* ctx, const syzsig_batch* b, uint64_t serial
 		               AggSrc{nullptr, 1, 0, 0}, cc, (uint32_t*)recs, ctx->agg_dbg >> 10);
 		const AggCells xc{(const uint32_t*)recs, nullptr, nullptr, cbase, ccap, ccnt, nchunks, 0, agg_group_size(nchunks),
 		                  ovf, sc};
-		launch_agg<true>(bound, P, s, xc, g, de, df, dc);
+		launch_agg<true>(ctx, bound, P, s, xc, g, de, df, dc);
 		k_stair_bucket<<<(int)std::min<uint32_t>(P, 2048), 256, 0, s>>>(
 		    (const uint32_t*)de, (const uint4*)df, (const uint32_t*)dc, P, lm.n, nshards, serial_base, cap, cursor,
 		    d_send, sc);

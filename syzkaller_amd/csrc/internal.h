@@ -72,7 +72,7 @@ struct Workspace {
 // the debug flags that change only the path taken, never a result
 constexpr uint32_t kDebugResultPreserving =
     SYZSIG_DEBUG_FIN_DEFER | SYZSIG_DEBUG_MIN_ATOMIC | SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_CAP_SPILL |
-    SYZSIG_DEBUG_RECS_GATE | SYZSIG_DEBUG_EDGE_MARKALL | SYZSIG_DEBUG_EDGE_PASSES;
+    SYZSIG_DEBUG_RECS_GATE | SYZSIG_DEBUG_EDGE_MARKALL | SYZSIG_DEBUG_EDGE_PASSES | SYZSIG_DEBUG_AGG_IDX64;
 // ... and those a product build accepts: the above plus fault injection
 constexpr uint32_t kDebugAccepted = kDebugResultPreserving | SYZSIG_DEBUG_POLL_FAIL;
 

@@ -196,16 +196,21 @@ def test_triage_finalize_deferred_path(gpu, case):
         assert st["parts"] >= 8 and st["overflow_parts"] == 0, st
 
 
-@pytest.mark.parametrize("mode", ["capped", "capped_split", "counted", "spill", "hot"])
+@pytest.mark.parametrize("mode", ["capped", "capped_split", "counted", "spill", "idx64", "counted_idx64", "edge_passes",
+                                  "hot"])
 def test_triage_cell_layouts(gpu, mode):
     """Both record layouts of the aggregation path against the oracle: capped
     cells (default; capped_split: at 2048 partitions), counted cells (SYZSIG_DEBUG_EXACT_CELLS), capped cells that
-    overflow and are redone counted (SYZSIG_DEBUG_CAP_SPILL), and a batch whose
-    calls repeat one hot element hundreds of times, so that one cell of every
+    overflow and are redone counted (SYZSIG_DEBUG_CAP_SPILL), k_agg's 64-bit
+    record indices (SYZSIG_DEBUG_AGG_IDX64: the path of runs past record 2^32,
+    both layouts), K2's marking-mode flag left set (SYZSIG_DEBUG_EDGE_PASSES:
+    its bit once reached the scatter as a timing-only "drop the records"
+    switch), and a batch whose calls repeat one hot element hundreds of times, so that one cell of every
     chunk overflows its capacity: each batch is redone with counted cells and
     the slack doubles until capped cells are given up -- every batch exact."""
     from syzkaller_amd import synth
-    from syzkaller_amd._lib import SYZSIG_DEBUG_CAP_SPILL, SYZSIG_DEBUG_EXACT_CELLS
+    from syzkaller_amd._lib import (SYZSIG_DEBUG_AGG_IDX64, SYZSIG_DEBUG_CAP_SPILL, SYZSIG_DEBUG_EDGE_PASSES,
+                                    SYZSIG_DEBUG_EXACT_CELLS)
 
     if mode == "hot":
         rng = np.random.default_rng(21)
@@ -233,7 +238,9 @@ def test_triage_cell_layouts(gpu, mode):
     nprog, cpp = 128, 32
     cl = synth.call_lengths(nprog, cpp, 2048)
     m0 = synth.m0(cfg, 2048, 1_000_000)
-    dbg = {"counted": SYZSIG_DEBUG_EXACT_CELLS, "spill": SYZSIG_DEBUG_CAP_SPILL}.get(mode, 0)
+    dbg = {"counted": SYZSIG_DEBUG_EXACT_CELLS, "spill": SYZSIG_DEBUG_CAP_SPILL, "idx64": SYZSIG_DEBUG_AGG_IDX64,
+           "counted_idx64": SYZSIG_DEBUG_EXACT_CELLS | SYZSIG_DEBUG_AGG_IDX64,
+           "edge_passes": SYZSIG_DEBUG_EDGE_PASSES}.get(mode, 0)
     # capped_split: 2048 partitions (the LDS write-combining buffers at their largest)
     parts = 2048 if mode == "capped_split" else 0
     gpu.eng.set_debug(dbg)
